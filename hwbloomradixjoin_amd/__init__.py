@@ -1,0 +1,250 @@
+"""hwbloomradixjoin_amd -- MI355X-native bloom-filtered radix hash join.
+
+Python mirror of the reference's operator interface for the BPRO path
+(Briimbo/HwBloomRadixJoin src/parallel_radix_join_bloom.h:34-36, src/parallel_radix_join.h:33-34,
+src/bloom_filter.h:10,50-55, src/types.h:37-63), bound over ctypes to the C-ABI library
+``libhwbrj.so`` (include/hwbrj.h). The join runs only in the HIP kernels of that library: if the
+library is missing this package raises instead of falling back to anything on the CPU.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass
+from typing import Optional
+
+import numpy as np
+
+__all__ = [
+    "BASIC", "BLOCKED", "SECTORIZED", "BloomFilterArgs", "Relation", "Result", "Stats",
+    "BPRO", "PRO", "assert_args", "join_device", "generate_device", "generate_host",
+    "export_filter", "hash_crc", "hash_crapwow", "lib", "LIB_PATH",
+]
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, "libhwbrj.so")
+CLI_PATH = os.path.join(PKG_DIR, "mchashjoins")
+
+# src/bloom_filter.h:10 (BASIC, BLOCKED) + this build's SECTORIZED
+BASIC, BLOCKED, SECTORIZED = 0, 1, 2
+_VARIANTS = {"basic": BASIC, "blocked": BLOCKED, "sectorized": SECTORIZED}
+
+
+class _Tuple(ctypes.Structure):  # src/types.h:37-40
+    _fields_ = [("key", ctypes.c_int32), ("payload", ctypes.c_int32)]
+
+
+class _Relation(ctypes.Structure):  # src/types.h:46-49
+    _fields_ = [("tuples", ctypes.POINTER(_Tuple)), ("num_tuples", ctypes.c_uint64)]
+
+
+class _Result(ctypes.Structure):  # src/types.h:59-63
+    _fields_ = [("totalresults", ctypes.c_int64), ("resultlist", ctypes.c_void_p),
+                ("nthreads", ctypes.c_int)]
+
+
+class _BloomArgs(ctypes.Structure):  # src/bloom_filter.h:50-55
+    _fields_ = [("variant", ctypes.c_int), ("m", ctypes.c_uint64), ("k", ctypes.c_uint64),
+                ("B", ctypes.c_uint64)]
+
+
+class _Stats(ctypes.Structure):  # include/hwbrj.h hwbrj_stats_t
+    _fields_ = [("filtered", ctypes.c_uint64), ("matches", ctypes.c_int64), ("mode", ctypes.c_int),
+                ("format", ctypes.c_int), ("partitions", ctypes.c_uint32),
+                ("subparts", ctypes.c_uint32), ("slice_segments", ctypes.c_uint32)] + [
+                    (n, ctypes.c_double) for n in (
+                        "ms_total", "ms_r_scatter", "ms_r_index", "ms_build", "ms_s_scatter",
+                        "ms_s_index", "ms_probe", "ms_surv", "ms_join")]
+
+
+_LIB = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load libhwbrj.so (built by __graft_entry__.build()). Raises if it is missing."""
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} is missing: run `python -c 'import __graft_entry__ as g; "
+                              "g.build()'` (the MI355X HIP library is required; there is no CPU "
+                              "fallback)")
+        L = ctypes.CDLL(LIB_PATH)
+        L.BPRO.restype = ctypes.POINTER(_Result)
+        L.BPRO.argtypes = [ctypes.POINTER(_Relation), ctypes.POINTER(_Relation), ctypes.c_int,
+                           ctypes.POINTER(_BloomArgs)]
+        L.PRO.restype = ctypes.POINTER(_Result)
+        L.PRO.argtypes = [ctypes.POINTER(_Relation), ctypes.POINTER(_Relation), ctypes.c_int]
+        L.assert_args.argtypes = [ctypes.POINTER(_BloomArgs)]
+        L.hwbrj_join_device.restype = ctypes.c_int
+        L.hwbrj_join_device.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                        ctypes.c_uint64, ctypes.POINTER(_BloomArgs),
+                                        ctypes.c_void_p, ctypes.POINTER(_Stats)]
+        L.hwbrj_generate_device.restype = ctypes.c_int
+        L.hwbrj_generate_device.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
+                                            ctypes.c_uint64, ctypes.c_uint64, ctypes.c_double,
+                                            ctypes.c_uint64, ctypes.c_void_p]
+        L.hwbrj_generate_host.restype = ctypes.c_int
+        L.hwbrj_generate_host.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
+                                          ctypes.c_uint64, ctypes.c_uint64, ctypes.c_double,
+                                          ctypes.c_uint64, ctypes.c_int]
+        L.hwbrj_export_filter.restype = ctypes.c_int
+        L.hwbrj_export_filter.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
+        L.hwbrj_hash_crc.restype = ctypes.c_uint32
+        L.hwbrj_hash_crc.argtypes = [ctypes.c_uint32, ctypes.c_int32]
+        L.hwbrj_hash_crapwow.restype = ctypes.c_uint32
+        L.hwbrj_hash_crapwow.argtypes = [ctypes.c_uint32, ctypes.c_int32]
+        L.hwbrj_device_count.restype = ctypes.c_int
+        L.hwbrj_set_device.restype = ctypes.c_int
+        L.hwbrj_set_device.argtypes = [ctypes.c_int]
+        L.hwbrj_last_error.restype = ctypes.c_char_p
+        L.hwbrj_version.restype = ctypes.c_char_p
+        L.hwbrj_release.restype = None
+        _LIB = L
+    return _LIB
+
+
+def _err(code: int, what: str):
+    if code != 0:
+        raise RuntimeError(f"{what} failed ({code}): {lib().hwbrj_last_error().decode()}")
+
+
+@dataclass
+class BloomFilterArgs:
+    """src/bloom_filter.h:50-55. Defaults are src/main.c:389-393 (variant BASIC, m=256 Mi, k=8,
+    B=1024)."""
+    variant: int = BASIC
+    m: int = 256 << 20
+    k: int = 8
+    B: int = 1024
+
+    @classmethod
+    def from_flag(cls, b: str, m: int, k: int, B: int = 1024) -> Optional["BloomFilterArgs"]:
+        """The CLI's -b parsing (src/main.c:692-698): 'no' -> None; unknown -> BASIC, except
+        'sectorized' which selects this build's SECTORIZED variant."""
+        if b == "no":
+            return None
+        return cls(_VARIANTS.get(b, BASIC), m, k, B)
+
+    def _c(self) -> _BloomArgs:
+        return _BloomArgs(int(self.variant), int(self.m), int(self.k), int(self.B))
+
+
+@dataclass
+class Result:
+    """src/types.h:59-63 (count-only: resultlist is NULL in the reference's default build)."""
+    totalresults: int
+    nthreads: int
+
+
+@dataclass
+class Stats:
+    filtered: int
+    matches: int
+    mode: int
+    format: int
+    partitions: int
+    subparts: int
+    slice_segments: int
+    ms_total: float
+    ms_r_scatter: float
+    ms_r_index: float
+    ms_build: float
+    ms_s_scatter: float
+    ms_s_index: float
+    ms_probe: float
+    ms_surv: float
+    ms_join: float
+
+
+class Relation:
+    """relation_t over a contiguous (N, 2) int32 array of {key, payload} (src/types.h:37-49)."""
+
+    def __init__(self, tuples: np.ndarray):
+        t = np.ascontiguousarray(tuples, dtype=np.int32)
+        if t.ndim != 2 or t.shape[1] != 2:
+            raise ValueError("tuples must have shape (N, 2): key, payload")
+        self.tuples = t
+        self._c = _Relation(t.ctypes.data_as(ctypes.POINTER(_Tuple)), t.shape[0])
+
+    @property
+    def num_tuples(self) -> int:
+        return self.tuples.shape[0]
+
+
+def assert_args(args: BloomFilterArgs) -> bool:
+    """src/bloom_filter.c:25-34 without the exit(1): True when the reference would accept."""
+    m, B = int(args.m), int(args.B)
+    if m & (m - 1):
+        return False
+    if args.variant != BASIC and (B <= 0 or B & (B - 1) or m % B):
+        return False
+    return True
+
+
+def BPRO(relR: Relation, relS: Relation, nthreads: int, args: BloomFilterArgs) -> Result:
+    """src/parallel_radix_join_bloom.c:1781-1787 on the MI355X (prints the reference's lines)."""
+    a = args._c()
+    r = lib().BPRO(ctypes.byref(relR._c), ctypes.byref(relS._c), int(nthreads), ctypes.byref(a))
+    out = Result(r.contents.totalresults, r.contents.nthreads)
+    ctypes.CDLL(None).free(r)
+    return out
+
+
+def PRO(relR: Relation, relS: Relation, nthreads: int) -> Result:
+    """src/parallel_radix_join.c:1697-1700 (no filter) on the MI355X."""
+    r = lib().PRO(ctypes.byref(relR._c), ctypes.byref(relS._c), int(nthreads))
+    out = Result(r.contents.totalresults, r.contents.nthreads)
+    ctypes.CDLL(None).free(r)
+    return out
+
+
+def _ptr(t) -> int:
+    return int(t.data_ptr())
+
+
+def join_device(R, S, args: Optional[BloomFilterArgs] = None, stream=None) -> Stats:
+    """Join device-resident torch int32 tensors of shape (N, 2) ({key, payload}) in HBM.
+    args=None runs PRO. `stream` is a torch.cuda.Stream (default: the library's own stream)."""
+    for name, t in (("R", R), ("S", S)):
+        if not t.is_cuda or t.dtype.itemsize != 4 or (t.numel() and t.shape[-1] != 2) or not t.is_contiguous():
+            raise ValueError(f"{name} must be a contiguous (N, 2) int32 tensor on the GPU")
+    st = _Stats()
+    a = args._c() if args is not None else None
+    sp = ctypes.c_void_p(stream.cuda_stream) if stream is not None else None
+    rc = lib().hwbrj_join_device(_ptr(R), R.shape[0], _ptr(S), S.shape[0],
+                                 ctypes.byref(a) if a is not None else None, sp, ctypes.byref(st))
+    _err(rc, "hwbrj_join_device")
+    return Stats(**{n: getattr(st, n) for n, _ in _Stats._fields_})
+
+
+def generate_device(out, nthreads: int, maxid: int, threshold: int, selectivity: float,
+                    seed: int, stream=None) -> None:
+    """Fill a (N, 2) int32 GPU tensor with the reference generator's multiset
+    (src/generator.c:304-415), seeded permuted order, payload = row index."""
+    sp = ctypes.c_void_p(stream.cuda_stream) if stream is not None else None
+    _err(lib().hwbrj_generate_device(_ptr(out), out.shape[0], nthreads, maxid, threshold,
+                                     selectivity, seed, sp), "hwbrj_generate_device")
+
+
+def generate_host(n: int, nthreads: int, maxid: int, threshold: int, selectivity: float,
+                  seed: int, host_threads: int = 0) -> np.ndarray:
+    """The same relation as generate_device, on the host: (n, 2) int32."""
+    out = np.empty((n, 2), dtype=np.int32)
+    _err(lib().hwbrj_generate_host(out.ctypes.data, n, nthreads, maxid, threshold, selectivity,
+                                   seed, host_threads), "hwbrj_generate_host")
+    return out
+
+
+def export_filter(m_bits: int) -> np.ndarray:
+    """The last join's filter in the reference's byte layout (m/8 uint8)."""
+    out = np.empty(m_bits // 8, dtype=np.uint8)
+    _err(lib().hwbrj_export_filter(out.ctypes.data, out.nbytes), "hwbrj_export_filter")
+    return out
+
+
+def hash_crc(seed: int, key: int) -> int:
+    return lib().hwbrj_hash_crc(seed, key)
+
+
+def hash_crapwow(seed: int, key: int) -> int:
+    return lib().hwbrj_hash_crapwow(seed, key)

@@ -1,0 +1,218 @@
+// hwbrj_api.cpp -- the C-ABI of libhwbrj.so (include/hwbrj.h): the drop-in BPRO / PRO operator
+// boundary with the reference's stdout contract, plus device-resident entry points.
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <x86intrin.h>
+
+#include <chrono>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "hwbrj_engine.h"
+
+namespace hwbrj {
+
+static thread_local std::string g_last_error;
+void set_last_error(const std::string& s) { g_last_error = s; }
+
+}  // namespace hwbrj
+
+using namespace hwbrj;
+
+extern "C" {
+
+const char* hwbrj_last_error(void) { return g_last_error.c_str(); }
+const char* hwbrj_version(void) { return "hwbloomradixjoin_amd 0.1 (gfx950)"; }
+
+int hwbrj_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int hwbrj_set_device(int device) {
+    hipError_t e = hipSetDevice(device);
+    if (e != hipSuccess) {
+        set_last_error(std::string("hipSetDevice: ") + hipGetErrorString(e));
+        return 1;
+    }
+    return 0;
+}
+
+void hwbrj_release(void) {
+    Engine* e = engine_for_current_device();
+    if (e) e->release();
+}
+
+uint32_t hwbrj_hash_crc(uint32_t seed, int32_t key) { return crc_f_bitwise(seed ^ (uint32_t) key); }
+uint32_t hwbrj_hash_crapwow(uint32_t seed, int32_t key) { return crapwow(seed, (uint32_t) key); }
+
+int hwbrj_join_device(const tuple_t* d_R, uint64_t nR, const tuple_t* d_S, uint64_t nS,
+                      const bloom_filter_args_t* args, void* stream, hwbrj_stats_t* stats) {
+    Engine* e = engine_for_current_device();
+    if (!e) {
+        set_last_error("no HIP device");
+        return 10;
+    }
+    return e->run((const uint2*) d_R, nR, (const uint2*) d_S, nS, args, (hipStream_t) stream, stats);
+}
+
+int hwbrj_generate_device(tuple_t* d_out, uint64_t n, uint32_t nthreads, uint64_t maxid,
+                          uint64_t threshold, double selectivity, uint64_t seed, void* stream) {
+    Engine* e = engine_for_current_device();
+    if (!e) {
+        set_last_error("no HIP device");
+        return 10;
+    }
+    return e->generate((uint2*) d_out, n, nthreads, maxid, threshold, selectivity, seed,
+                       (hipStream_t) stream);
+}
+
+int hwbrj_generate_host(tuple_t* out, uint64_t n, uint32_t nthreads, uint64_t maxid,
+                        uint64_t threshold, double selectivity, uint64_t seed, int host_threads) {
+    std::vector<GenPlan> plan(1);
+    if (make_gen_plan(&plan[0], n, nthreads, maxid, threshold, selectivity)) {
+        set_last_error("invalid generator parameters");
+        return 2;
+    }
+    const Perm perm = make_perm(n, seed);
+    int        T    = host_threads > 0 ? host_threads : (int) std::thread::hardware_concurrency();
+    if (T < 1) T = 1;
+    if ((uint64_t) T > n / 4096 + 1) T = (int) (n / 4096 + 1);
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; t++) {
+        th.emplace_back([&, t] {
+            const uint64_t b = n * t / T, e = n * (t + 1) / T;
+            for (uint64_t i = b; i < e; i++) {
+                out[i].key     = gen_key_at(plan[0], perm_apply(perm, i));
+                out[i].payload = (int32_t) i;
+            }
+        });
+    }
+    for (auto& x : th) x.join();
+    return 0;
+}
+
+int hwbrj_export_filter(uint8_t* host_out, uint64_t nbytes) {
+    Engine* e = engine_for_current_device();
+    if (!e) {
+        set_last_error("no HIP device");
+        return 10;
+    }
+    return e->export_filter(host_out, nbytes);
+}
+
+// src/bloom_filter.c:25-34 -- prints the reference's message and exits(1).
+void assert_args(bloom_filter_args_t* args) {
+    if ((args->m & (args->m - 1)) != 0) {
+        printf("m must be a power of 2");
+        exit(1);
+    }
+    if (args->variant != BASIC) {
+        const uint64_t B = args->B;
+        if (B == 0 || (B & (B - 1)) != 0) {
+            printf("B must be a power 2");
+            exit(1);
+        }
+        if (args->m % B != 0) {
+            printf("m must be a multiple of B");
+            exit(1);
+        }
+    }
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------------ BPRO / PRO (host data)
+static void fatal(const char* what) {
+    printf("[ERROR] %s: %s\n", what, hwbrj_last_error());
+    exit(EXIT_FAILURE);  // the reference's convention (src/parallel_radix_join_bloom.c:64-71)
+}
+
+// src/parallel_radix_join_bloom.c:1509-1547 print_timing, fed with device times.
+static void print_timing(uint64_t total_cyc, uint64_t build_cyc, uint64_t part_cyc,
+                         uint64_t numtuples, int64_t result, double total_usec,
+                         double part_usec, double probe_usec, double join_usec) {
+    const double nsec_per_tuple = total_usec * 1000.0 / (double) (numtuples ? numtuples : 1);
+    fprintf(stdout, "RUNTIME TOTAL, BUILD, PART (cycles): \n");
+    fprintf(stdout, "%llu \t %llu \t %llu ", (unsigned long long) total_cyc,
+            (unsigned long long) build_cyc, (unsigned long long) part_cyc);
+    fprintf(stdout, "\n");
+    fprintf(stdout, "TOTAL-TIME-USECS, TOTAL-TUPLES, NSEC-PER-TUPLE: \n");
+    fprintf(stdout, "%.4lf \t %llu \t ", total_usec, (unsigned long long) result);
+    fprintf(stdout, "%.4lf ", nsec_per_tuple);
+    fprintf(stdout, "\n");
+    fprintf(stdout, "PARTITION-TIME-USECS, PROBE-TIME-USECS, JOIN-TIME-USECS: \n");
+    fprintf(stdout, "%.4lf \t %.4lf\t %.4lf \n", part_usec, probe_usec, join_usec);
+    fflush(stdout);
+}
+
+static result_t* run_host_join(relation_t* relR, relation_t* relS, int nthreads,
+                               bloom_filter_args_t* args) {
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) {
+        set_last_error("no MI355X device visible");
+        fatal("BPRO");
+    }
+    const uint64_t nR = relR->num_tuples, nS = relS->num_tuples;
+    tuple_t *dR = nullptr, *dS = nullptr;
+    if (hipMalloc((void**) &dR, (nR ? nR : 1) * sizeof(tuple_t)) != hipSuccess ||
+        hipMalloc((void**) &dS, (nS ? nS : 1) * sizeof(tuple_t)) != hipSuccess) {
+        set_last_error("hipMalloc of the input relations failed");
+        fatal("BPRO");
+    }
+    // H2D outside the timed region (the reference's timer starts after its allocations).
+    const auto h0 = std::chrono::steady_clock::now();
+    if ((nR && hipMemcpy(dR, relR->tuples, nR * sizeof(tuple_t), hipMemcpyHostToDevice) != hipSuccess) ||
+        (nS && hipMemcpy(dS, relS->tuples, nS * sizeof(tuple_t), hipMemcpyHostToDevice) != hipSuccess)) {
+        set_last_error("H2D copy failed");
+        fatal("BPRO");
+    }
+    const double h2d_usec =
+        std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - h0).count();
+    hwbrj_stats_t st;
+    const uint64_t c0 = __rdtsc();
+    if (hwbrj_join_device(dR, nR, dS, nS, args, nullptr, &st) != 0) fatal("BPRO");
+    const uint64_t c1 = __rdtsc();
+    (void) hipFree(dR);
+    (void) hipFree(dS);
+    if (args) fprintf(stdout, "S-tuples after filter: %d\n", (int) st.filtered);  // :1253
+    const double part_ms = st.ms_total - st.ms_join;
+    const uint64_t total_cyc = c1 - c0;
+    const uint64_t part_cyc  = st.ms_total > 0 ? (uint64_t) (total_cyc * (part_ms / st.ms_total)) : 0;
+    print_timing(total_cyc, total_cyc - part_cyc, part_cyc, nS, st.matches, st.ms_total * 1e3,
+                 part_ms * 1e3, st.ms_join * 1e3, st.ms_join * 1e3);
+    if (getenv("HWBRJ_VERBOSE"))
+        fprintf(stderr,
+                "[hwbrj] mode=%d format=%d F=%u NSUB=%u nseg=%u h2d_usec=%.1f | ms: r_scatter %.3f "
+                "r_index %.3f build %.3f s_scatter %.3f s_index %.3f probe %.3f surv %.3f join %.3f\n",
+                st.mode, st.format, st.partitions, st.subparts, st.slice_segments, h2d_usec,
+                st.ms_r_scatter, st.ms_r_index, st.ms_build, st.ms_s_scatter, st.ms_s_index,
+                st.ms_probe, st.ms_surv, st.ms_join);
+    result_t* res = (result_t*) malloc(sizeof(result_t));
+    if (!res) {
+        set_last_error("malloc");
+        fatal("BPRO");
+    }
+    res->totalresults = st.matches;
+    res->resultlist   = nullptr;
+    res->nthreads     = nthreads;
+    return res;
+}
+
+extern "C" {
+
+// src/parallel_radix_join_bloom.h:34-36
+result_t* BPRO(relation_t* relR, relation_t* relS, int nthreads,
+               bloom_filter_args_t* bloom_filter_args) {
+    return run_host_join(relR, relS, nthreads, bloom_filter_args);
+}
+
+// src/parallel_radix_join.h:33-34
+result_t* PRO(relation_t* relR, relation_t* relS, int nthreads) {
+    return run_host_join(relR, relS, nthreads, nullptr);
+}
+
+}  // extern "C"

@@ -1,0 +1,492 @@
+// hwbrj_engine.cpp -- host orchestration of the MI355X bloom radix join (DESIGN.md "Pipeline").
+//
+// The reference runs R pass-1 (+ bloom add), S pass-1 (+ bloom contains), pass-2 and the
+// bucket-chaining join inside pthreads with barriers (src/parallel_radix_join_bloom.c:1059-1506).
+// Here every barrier is a kernel boundary on one HIP stream, and the task queues are replaced by
+// device-built chunk lists and item tables (no host round trips inside the join).
+#include "hwbrj_engine.h"
+
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <mutex>
+#include <vector>
+
+namespace hwbrj {
+
+#define HWBRJ_CHECK(expr)                                                                 \
+    do {                                                                                  \
+        hipError_t e_ = (expr);                                                           \
+        if (e_ != hipSuccess) {                                                           \
+            set_last_error(std::string(#expr) + ": " + hipGetErrorString(e_));            \
+            return 1;                                                                     \
+        }                                                                                 \
+    } while (0)
+
+// ---------------------------------------------------------------------------- tables
+bool build_crc_tables(CrcTables* t) {
+    uint32_t col[32];  // f(e_i)
+    for (int i = 0; i < 32; i++) col[i] = crc_f_bitwise(1u << i);
+    for (int j = 0; j < 8; j++)
+        for (int v = 0; v < 16; v++) t->fwd[j][v] = crc_f_bitwise((uint32_t) v << (4 * j));
+    // Invert the 32x32 GF(2) matrix whose column i is col[i]: solve f(x) = e_r for every r.
+    // Gauss-Jordan on rows of [M | I] packed as 64-bit rows (row r: bit c of M, bit 32+c of I).
+    uint64_t rows[32];
+    for (int r = 0; r < 32; r++) {
+        uint64_t row = 0;
+        for (int c = 0; c < 32; c++)
+            if ((col[c] >> r) & 1u) row |= 1ull << c;
+        rows[r] = row | (1ull << (32 + r));
+    }
+    for (int c = 0; c < 32; c++) {
+        int piv = -1;
+        for (int r = c; r < 32; r++)
+            if ((rows[r] >> c) & 1ull) {
+                piv = r;
+                break;
+            }
+        if (piv < 0) return false;
+        std::swap(rows[c], rows[piv]);
+        for (int r = 0; r < 32; r++)
+            if (r != c && ((rows[r] >> c) & 1ull)) rows[r] ^= rows[c];
+    }
+    // rows now = [I | M^-1]; column j of M^-1 = finv(e_j)
+    uint32_t icol[32];
+    for (int j = 0; j < 32; j++) {
+        uint32_t v = 0;
+        for (int r = 0; r < 32; r++)
+            if ((rows[r] >> (32 + j)) & 1ull) v |= 1u << r;
+        icol[j] = v;
+    }
+    for (int j = 0; j < 8; j++)
+        for (int v = 0; v < 16; v++) {
+            uint32_t x = (uint32_t) v << (4 * j), r = 0;
+            for (int b = 0; b < 32; b++)
+                if ((x >> b) & 1u) r ^= icol[b];
+            t->inv[j][v] = r;
+        }
+    // self-check on a few values
+    for (uint32_t x : {0u, 1u, 42u, 0xDEADBEEFu, 0x7FFFFFFFu}) {
+        if (nibble_map(&t->inv[0][0], nibble_map(&t->fwd[0][0], x)) != x) return false;
+        if (nibble_map(&t->fwd[0][0], x) != crc_f_bitwise(x)) return false;
+    }
+    return true;
+}
+
+// ------------------------------------------------------------------------- generator plan
+int make_gen_plan(GenPlan* plan, uint64_t num_tuples, uint32_t nthreads, uint64_t maxid,
+                  uint64_t threshold, double selectivity) {
+    // src/generator.c:331-395, integer widths as in the reference
+    if (nthreads == 0 || nthreads > (uint32_t) kMaxGenChunks || threshold == 0) return 1;
+    const unsigned int pagesize      = 4096;
+    unsigned int       npages        = (unsigned int) ((num_tuples * 8u) / pagesize + 1u);
+    unsigned int       npages_perthr = npages / nthreads;
+    uint64_t ntuples_perthr = (uint64_t) npages_perthr * (uint64_t) (pagesize / 8u);
+    uint64_t ntuples_above  = (uint64_t) ((double) num_tuples * (1 - selectivity));
+    if (npages_perthr == 0) ntuples_perthr = num_tuples / nthreads;
+    uint64_t ntuples_above_perthr  = (uint64_t) ((double) ntuples_perthr * (1 - selectivity));
+    uint64_t ntuples_lastthr       = num_tuples - ntuples_perthr * (nthreads - 1);
+    uint64_t ntuples_above_lastthr = ntuples_above - (uint64_t) (nthreads - 1) * ntuples_above_perthr;
+    uint64_t offset = 0, offset_above = 0;
+    plan->nchunks    = nthreads;
+    plan->num_tuples = num_tuples;
+    plan->threshold  = threshold;
+    const uint64_t span = maxid > threshold ? maxid - threshold : 0;
+    for (uint32_t t = 0; t < nthreads; t++) {
+        GenChunk& c  = plan->chunk[t];
+        c.firstkey   = (int64_t) ((offset + 1) % threshold);
+        c.firstabove = (int64_t) (threshold + (offset_above + 1) % (span > 1 ? span : 1));
+        uint64_t na  = (t == nthreads - 1) ? ntuples_above_lastthr : ntuples_above_perthr;
+        c.n          = (t == nthreads - 1) ? ntuples_lastthr : ntuples_perthr;
+        c.start      = offset + offset_above;
+        if (na > c.n || c.start + c.n > num_tuples) return 2;  // the reference would overrun
+        c.n_below = c.n - na;
+        offset += ntuples_perthr - ntuples_above_perthr;
+        offset_above += ntuples_above_perthr;
+    }
+    return 0;
+}
+
+// ------------------------------------------------------------------------------ geometry
+bool plan_geometry(const bloom_filter_args_t* a, uint64_t nR, Geometry* g, std::string* err) {
+    memset(g, 0, sizeof(*g));
+    g->variant = -1;
+    if (!a) {
+        g->mode  = MODE_NOBLOOM;
+        g->log2F = kMaxLog2F;
+    } else {
+        const uint64_t m = a->m, B = a->B, k = a->k;
+        if (m == 0 || (m & (m - 1)) != 0) {
+            *err = "m must be a power of 2";  // src/bloom_filter.c:27
+            return false;
+        }
+        if (m > (1ull << 32)) {
+            *err = "m > 2^32 bits is outside the 32-bit hash contract of src/bloom_filter.c";
+            return false;
+        }
+        if (k > 4096) {
+            *err = "k > 4096 is not supported";
+            return false;
+        }
+        if (a->variant != BASIC && a->variant != BLOCKED && a->variant != SECTORIZED) {
+            *err = "unknown filter variant";
+            return false;
+        }
+        g->variant = (int) a->variant;
+        g->k       = (uint32_t) k;
+        g->m       = m;
+        if (a->variant != BASIC) {
+            if (B == 0 || (B & (B - 1)) != 0) {
+                *err = "B must be a power 2";  // src/bloom_filter.c:30
+                return false;
+            }
+            if (m % B != 0) {
+                *err = "m must be a multiple of B";  // :31
+                return false;
+            }
+            if (B > (1ull << 31)) {
+                *err = "B too large";
+                return false;
+            }
+            g->B          = (uint32_t) B;
+            g->nblocks    = (uint32_t) std::min<uint64_t>(m / B, 0xFFFFFFFFull);
+            g->block_span = (uint32_t) ((B / 8) * 8);
+        }
+        uint64_t F = 0;
+        if (a->variant == BASIC) {
+            if (k == 1 && m >= 32) {
+                g->mode = MODE_SLICE_BASIC;
+                F       = std::min<uint64_t>(1024, m / 32);
+            } else {
+                g->mode = MODE_GLOBAL;
+            }
+        } else {
+            if (B >= 8 && m >= 32 && (m / B) <= 0xFFFFFFFFull) {
+                g->mode = MODE_SLICE_BLOCK;
+                F       = std::min<uint64_t>(std::min<uint64_t>(1024, m / B), m / 32);
+            } else {
+                g->mode = MODE_GLOBAL;
+            }
+        }
+        g->log2F = (g->mode == MODE_GLOBAL) ? kMaxLog2F : ilog2u(F);
+        if (g->mode == MODE_SLICE_BLOCK || g->mode == MODE_SLICE_BASIC) {
+            g->slice_bits = (uint32_t) (m >> g->log2F);
+            g->seg_bits   = std::min(g->slice_bits, kSliceMaxBits);
+            g->nseg       = g->slice_bits / g->seg_bits;
+            g->seg_words  = std::max<uint32_t>(4, g->seg_bits / 32);
+        }
+        if (g->mode == MODE_SLICE_BLOCK && k == 1 && ilog2u(B) <= g->log2F) g->format = FMT_PACKED;
+    }
+    const uint64_t F    = 1ull << g->log2F;
+    const uint64_t rper = (nR + F - 1) / F;
+    uint32_t       l2s  = 0;
+    while (l2s < 6 && (rper >> l2s) > 8192) l2s++;
+    g->log2NSUB   = l2s;
+    g->sub_shift  = (g->mode == MODE_SLICE_BASIC) ? 0 : g->log2F;
+    g->hash_shift = g->sub_shift + g->log2NSUB;
+    return true;
+}
+
+// ---------------------------------------------------------------------------- buffers
+bool DevBuf::ensure(size_t need) {
+    if (need == 0) need = 16;
+    if (need <= bytes) return true;
+    release();
+    if (hipMalloc(&p, need) != hipSuccess) {
+        p     = nullptr;
+        bytes = 0;
+        return false;
+    }
+    bytes = need;
+    return true;
+}
+
+void DevBuf::release() {
+    if (p) (void) hipFree(p);
+    p     = nullptr;
+    bytes = 0;
+}
+
+Engine::Engine(int device) : device_(device) {
+    (void) hipSetDevice(device);
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess) cus_ = prop.multiProcessorCount;
+    (void) hipStreamCreateWithFlags(&own_stream_, hipStreamNonBlocking);
+    for (auto& e : ev_) (void) hipEventCreate(&e);
+    CrcTables t;
+    if (!build_crc_tables(&t)) set_last_error("CRC table inversion failed");
+    (void) hipMalloc((void**) &d_tabs_, sizeof(CrcTables));
+    (void) hipMemcpy(d_tabs_, &t, sizeof(CrcTables), hipMemcpyHostToDevice);
+    (void) hipMalloc((void**) &d_plan_, sizeof(GenPlan));
+}
+
+Engine::~Engine() { release(); }
+
+void Engine::release() {
+    for (DevBuf* b : {&poolR, &metaR, &usedR, &pchR, &pelR, &lstartR, &lcurR, &estartR, &istartR,
+                      &listR, &poolS, &metaS, &usedS, &pchS, &pelS, &lstartS, &lcurS, &estartS,
+                      &istartS, &listS, &slices, &bitmap, &rjoin, &rqs, &surv, &survcnt, &itemoff,
+                      &qstot, &sqs, &sjoin, &dense, &small})
+        b->release();
+    have_filter_ = false;
+}
+
+static uint64_t region_cap(uint64_t n, uint32_t G, uint32_t F) {
+    const uint64_t units = (n + 3) / 4;
+    const uint64_t per   = ((units + G - 1) / G) * 4;
+    return (per + 31) / 32 + F + 1;
+}
+
+int Engine::run(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
+                const bloom_filter_args_t* args, hipStream_t stream, hwbrj_stats_t* st) {
+    HWBRJ_CHECK(hipSetDevice(device_));
+    Geometry    g;
+    std::string err;
+    if (!plan_geometry(args, nR, &g, &err)) {
+        set_last_error(err);
+        return 2;
+    }
+    if (!stream) stream = own_stream_;
+    const uint32_t F = 1u << g.log2F, NSUB = 1u << g.log2NSUB, NJ = F * NSUB;
+    const bool     slice_mode = g.mode == MODE_SLICE_BLOCK || g.mode == MODE_SLICE_BASIC;
+    const uint32_t nseg       = slice_mode ? g.nseg : 1;
+    const uint32_t CH         = 1024;  // chunks per probe item
+    const size_t   sc_lds     = scatter_lds_bytes(g.log2F);
+    const uint32_t G          = (uint32_t) cus_ * (uint32_t) std::max<size_t>(1, std::min<size_t>(2, 163840 / sc_lds));
+    const uint64_t capR = region_cap(nR, G, F), capS = region_cap(nS, G, F);
+    const uint64_t LR = (uint64_t) G * capR, LS = (uint64_t) G * capS;  // max chunks
+    const uint64_t items_max = (LS / CH + F + 1) * nseg;
+    if (LS > 0xFFFFFFFFull || LR > 0xFFFFFFFFull) {
+        set_last_error("relation too large for 32-bit chunk ids");
+        return 3;
+    }
+    bool ok = true;
+    ok &= poolR.ensure(LR * 128) && metaR.ensure(LR * 4) && listR.ensure(LR * 4);
+    ok &= usedR.ensure(G * 4) && pchR.ensure(F * 4) && pelR.ensure(F * 8) && lcurR.ensure(F * 4);
+    ok &= lstartR.ensure((F + 1) * 4) && estartR.ensure((F + 1) * 8) && istartR.ensure((F + 1) * 4);
+    ok &= poolS.ensure(LS * 128) && metaS.ensure(LS * 4) && listS.ensure(LS * 4);
+    ok &= usedS.ensure(G * 4) && pchS.ensure(F * 4) && pelS.ensure(F * 8) && lcurS.ensure(F * 4);
+    ok &= lstartS.ensure((F + 1) * 4) && estartS.ensure((F + 1) * 8) && istartS.ensure((F + 1) * 4);
+    ok &= rjoin.ensure(nR * 4) && rqs.ensure((NJ + 1) * 8ull);
+    ok &= surv.ensure(nseg * LS * 128) && survcnt.ensure(items_max * NSUB * 4) &&
+          itemoff.ensure(items_max * NSUB * 4);
+    ok &= qstot.ensure(NJ * 8ull) && sqs.ensure((NJ + 1) * 8ull) && sjoin.ensure(nS * 4);
+    ok &= small.ensure(64);
+    if (slice_mode) ok &= slices.ensure((uint64_t) F * nseg * g.seg_words * 4);
+    if (g.mode == MODE_GLOBAL) ok &= bitmap.ensure(((g.m + 31) / 32) * 4) && dense.ensure(nS * 4);
+    if (!ok) {
+        set_last_error("hipMalloc failed (device memory)");
+        return 4;
+    }
+    uint64_t* d_result = small.as<uint64_t>();      // [0] matches
+    uint64_t* d_dcount = small.as<uint64_t>() + 1;  // [1] dense survivor count (global mode)
+
+    // zeroing outside the timed region (the reference callocs before its timer, :1583, :1601)
+    HWBRJ_CHECK(hipMemsetAsync(pchR.p, 0, F * 4, stream));
+    HWBRJ_CHECK(hipMemsetAsync(pelR.p, 0, F * 8, stream));
+    HWBRJ_CHECK(hipMemsetAsync(pchS.p, 0, F * 4, stream));
+    HWBRJ_CHECK(hipMemsetAsync(pelS.p, 0, F * 8, stream));
+    HWBRJ_CHECK(hipMemsetAsync(small.p, 0, 64, stream));
+    if (g.mode == MODE_GLOBAL) HWBRJ_CHECK(hipMemsetAsync(bitmap.p, 0, bitmap.bytes, stream));
+
+    ScatterParams sp{};
+    sp.tabs = d_tabs_;
+    sp.g    = g;
+
+    HWBRJ_CHECK(hipEventRecord(ev_[0], stream));
+    // ---------------------------------------------------------------- R: pass-1 (+ filter)
+    if (g.mode == MODE_GLOBAL)
+        launch_build_global(dR, nR, g, d_tabs_, bitmap.as<uint32_t>(), stream);
+    sp.src = dR;
+    sp.n = nR;
+    sp.n_dev = nullptr;
+    sp.pool = poolR.as<uint32_t>();
+    sp.meta = metaR.as<uint32_t>();
+    sp.wg_used = usedR.as<uint32_t>();
+    sp.part_chunks = pchR.as<uint32_t>();
+    sp.part_elems = pelR.as<uint64_t>();
+    sp.cap = capR;
+    launch_scatter(sp, SRC_TUPLES, G, stream);
+    HWBRJ_CHECK(hipEventRecord(ev_[1], stream));
+    launch_plan(pchR.as<uint32_t>(), pelR.as<uint64_t>(), g.log2F, CH, 1, lstartR.as<uint32_t>(),
+                lcurR.as<uint32_t>(), estartR.as<uint64_t>(), istartR.as<uint32_t>(), stream);
+    launch_list_fill(metaR.as<uint32_t>(), usedR.as<uint32_t>(), capR, g.log2F,
+                     lcurR.as<uint32_t>(), listR.as<uint32_t>(), G, stream);
+    HWBRJ_CHECK(hipEventRecord(ev_[2], stream));
+    BuildParams bp{};
+    bp.g          = g;
+    bp.tabs       = d_tabs_;
+    bp.pool       = poolR.as<uint32_t>();
+    bp.meta       = metaR.as<uint32_t>();
+    bp.list       = listR.as<uint32_t>();
+    bp.list_start = lstartR.as<uint32_t>();
+    bp.elem_start = estartR.as<uint64_t>();
+    bp.slices     = slice_mode ? slices.as<uint32_t>() : nullptr;
+    bp.qs_off     = rqs.as<uint64_t>();
+    bp.out_codes  = rjoin.as<uint32_t>();
+    launch_build(bp, F, stream);
+    HWBRJ_CHECK(hipEventRecord(ev_[3], stream));
+    // ---------------------------------------------------------------- S: pass-1 (+ probe)
+    if (g.mode == MODE_GLOBAL) {
+        launch_probe_global(dS, nS, g, d_tabs_, bitmap.as<uint32_t>(), dense.as<uint32_t>(),
+                            d_dcount, stream);
+        sp.src   = dense.p;
+        sp.n     = nS;
+        sp.n_dev = d_dcount;
+    } else {
+        sp.src   = dS;
+        sp.n     = nS;
+        sp.n_dev = nullptr;
+    }
+    sp.pool = poolS.as<uint32_t>();
+    sp.meta = metaS.as<uint32_t>();
+    sp.wg_used = usedS.as<uint32_t>();
+    sp.part_chunks = pchS.as<uint32_t>();
+    sp.part_elems = pelS.as<uint64_t>();
+    sp.cap = capS;
+    launch_scatter(sp, g.mode == MODE_GLOBAL ? SRC_CODES : SRC_TUPLES, G, stream);
+    HWBRJ_CHECK(hipEventRecord(ev_[4], stream));
+    launch_plan(pchS.as<uint32_t>(), pelS.as<uint64_t>(), g.log2F, CH, nseg,
+                lstartS.as<uint32_t>(), lcurS.as<uint32_t>(), estartS.as<uint64_t>(),
+                istartS.as<uint32_t>(), stream);
+    launch_list_fill(metaS.as<uint32_t>(), usedS.as<uint32_t>(), capS, g.log2F,
+                     lcurS.as<uint32_t>(), listS.as<uint32_t>(), G, stream);
+    HWBRJ_CHECK(hipEventRecord(ev_[5], stream));
+    ProbeParams pp{};
+    pp.g               = g;
+    pp.tabs            = d_tabs_;
+    pp.pool            = poolS.as<uint32_t>();
+    pp.meta            = metaS.as<uint32_t>();
+    pp.list            = listS.as<uint32_t>();
+    pp.list_start      = lstartS.as<uint32_t>();
+    pp.item_start      = istartS.as<uint32_t>();
+    pp.slices          = slice_mode ? slices.as<uint32_t>() : nullptr;
+    pp.surv            = surv.as<uint32_t>();
+    pp.surv_seg_stride = LS * 32;
+    pp.surv_cnt        = survcnt.as<uint32_t>();
+    pp.CH              = CH;
+    const size_t   pl_lds = slice_lds_bytes(g);
+    const uint32_t PG = (uint32_t) cus_ * (uint32_t) std::max<size_t>(1, std::min<size_t>(2, 163840 / pl_lds));
+    launch_probe(pp, PG, stream);
+    HWBRJ_CHECK(hipEventRecord(ev_[6], stream));
+    // ------------------------------------------------------- S: pass-2 of the survivors
+    launch_surv_totals(istartS.as<uint32_t>(), survcnt.as<uint32_t>(), g.log2F, g.log2NSUB,
+                       itemoff.as<uint32_t>(), qstot.as<uint64_t>(), stream);
+    launch_scan_u64(qstot.as<uint64_t>(), sqs.as<uint64_t>(), NJ, stream);
+    SurvParams sv{};
+    sv.log2F           = g.log2F;
+    sv.log2NSUB        = g.log2NSUB;
+    sv.sub_shift       = g.sub_shift;
+    sv.nseg            = nseg;
+    sv.CH              = CH;
+    sv.item_start      = istartS.as<uint32_t>();
+    sv.list_start      = lstartS.as<uint32_t>();
+    sv.surv            = surv.as<uint32_t>();
+    sv.surv_seg_stride = LS * 32;
+    sv.surv_cnt        = survcnt.as<uint32_t>();
+    sv.item_off        = itemoff.as<uint32_t>();
+    sv.qs_off          = sqs.as<uint64_t>();
+    sv.out             = sjoin.as<uint32_t>();
+    launch_surv_scatter(sv, (uint32_t) cus_ * 8, stream);
+    HWBRJ_CHECK(hipEventRecord(ev_[7], stream));
+    // -------------------------------------------------------------------------- join
+    JoinParams jp{};
+    jp.r_codes    = rjoin.as<uint32_t>();
+    jp.r_off      = rqs.as<uint64_t>();
+    jp.s_codes    = sjoin.as<uint32_t>();
+    jp.s_off      = sqs.as<uint64_t>();
+    jp.hash_shift = g.hash_shift;
+    jp.result     = d_result;
+    launch_join(jp, NJ, stream);
+    HWBRJ_CHECK(hipEventRecord(ev_[8], stream));
+    HWBRJ_CHECK(hipGetLastError());
+    HWBRJ_CHECK(hipEventSynchronize(ev_[8]));
+
+    uint64_t matches = 0, filtered = 0;
+    HWBRJ_CHECK(hipMemcpy(&matches, d_result, 8, hipMemcpyDeviceToHost));
+    HWBRJ_CHECK(hipMemcpy(&filtered, sqs.as<uint64_t>() + NJ, 8, hipMemcpyDeviceToHost));
+    have_filter_ = args != nullptr;
+    last_g_      = g;
+    if (st) {
+        memset(st, 0, sizeof(*st));
+        st->filtered       = args ? filtered : nS;
+        st->matches        = (int64_t) matches;
+        st->mode           = g.mode;
+        st->format         = g.format;
+        st->partitions     = F;
+        st->subparts       = NSUB;
+        st->slice_segments = nseg;
+        float ms[9];
+        for (int i = 1; i <= 8; i++) HWBRJ_CHECK(hipEventElapsedTime(&ms[i], ev_[i - 1], ev_[i]));
+        HWBRJ_CHECK(hipEventElapsedTime(&ms[0], ev_[0], ev_[8]));
+        st->ms_total     = ms[0];
+        st->ms_r_scatter = ms[1];
+        st->ms_r_index   = ms[2];
+        st->ms_build     = ms[3];
+        st->ms_s_scatter = ms[4];
+        st->ms_s_index   = ms[5];
+        st->ms_probe     = ms[6];
+        st->ms_surv      = ms[7];
+        st->ms_join      = ms[8];
+    }
+    return 0;
+}
+
+int Engine::export_filter(uint8_t* host_out, uint64_t nbytes) {
+    HWBRJ_CHECK(hipSetDevice(device_));
+    if (!have_filter_) {
+        set_last_error("no filter has been built");
+        return 5;
+    }
+    const Geometry& g = last_g_;
+    if (nbytes != g.m / 8) {
+        set_last_error("nbytes must equal m/8");
+        return 6;
+    }
+    if (g.mode == MODE_GLOBAL) {
+        HWBRJ_CHECK(hipMemcpy(host_out, bitmap.p, nbytes, hipMemcpyDeviceToHost));
+        return 0;
+    }
+    const uint64_t nwords = (g.m + 31) / 32;
+    DevBuf tmp;
+    if (!tmp.ensure(nwords * 4)) {
+        set_last_error("hipMalloc failed");
+        return 4;
+    }
+    launch_export(slices.as<uint32_t>(), g, tmp.as<uint32_t>(), nwords, own_stream_);
+    HWBRJ_CHECK(hipStreamSynchronize(own_stream_));
+    HWBRJ_CHECK(hipMemcpy(host_out, tmp.p, nbytes, hipMemcpyDeviceToHost));
+    tmp.release();
+    return 0;
+}
+
+int Engine::generate(uint2* d_out, uint64_t n, uint32_t nthreads, uint64_t maxid,
+                     uint64_t threshold, double selectivity, uint64_t seed, hipStream_t stream) {
+    HWBRJ_CHECK(hipSetDevice(device_));
+    std::vector<GenPlan> plan(1);
+    if (make_gen_plan(&plan[0], n, nthreads, maxid, threshold, selectivity)) {
+        set_last_error("invalid generator parameters");
+        return 2;
+    }
+    if (!stream) stream = own_stream_;
+    HWBRJ_CHECK(hipMemcpyAsync(d_plan_, plan.data(), sizeof(GenPlan), hipMemcpyHostToDevice, stream));
+    launch_gen(d_out, n, d_plan_, make_perm(n, seed), stream);
+    HWBRJ_CHECK(hipGetLastError());
+    HWBRJ_CHECK(hipStreamSynchronize(stream));
+    return 0;
+}
+
+// ----------------------------------------------------------------- per-device singletons
+static std::mutex g_mu;
+static Engine*    g_engines[64] = {};
+
+Engine* engine_for_current_device() {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (!g_engines[dev]) g_engines[dev] = new Engine(dev);
+    return g_engines[dev];
+}
+
+}  // namespace hwbrj

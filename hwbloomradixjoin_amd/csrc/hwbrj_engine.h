@@ -1,0 +1,59 @@
+// hwbrj_engine.h -- host-side orchestration of the MI355X join pipeline (internal C++).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+
+#include "../../include/hwbrj.h"
+#include "hwbrj_common.h"
+#include "hwbrj_kernels.h"
+
+namespace hwbrj {
+
+// Picks mode / partitioning / slice geometry for a filter configuration (DESIGN.md "Modes").
+// Returns false (and sets *err) for configurations outside the reference's contract.
+bool plan_geometry(const bloom_filter_args_t* args, uint64_t nR, Geometry* g, std::string* err);
+
+struct DevBuf {
+    void*  p     = nullptr;
+    size_t bytes = 0;
+    bool   ensure(size_t need);  // grow-only
+    void   release();
+    template <class T> T* as() const { return (T*) p; }
+};
+
+class Engine {
+  public:
+    explicit Engine(int device);
+    ~Engine();
+    // Synchronous join of device-resident tuples. Returns 0 on success.
+    int  run(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
+             const bloom_filter_args_t* args, hipStream_t stream, hwbrj_stats_t* st);
+    int  export_filter(uint8_t* host_out, uint64_t nbytes);
+    int  generate(uint2* d_out, uint64_t n, uint32_t nthreads, uint64_t maxid, uint64_t threshold,
+                  double selectivity, uint64_t seed, hipStream_t stream);
+    void release();
+    int  device() const { return device_; }
+
+  private:
+    int          device_;
+    int          cus_ = 256;
+    hipStream_t  own_stream_ = nullptr;
+    hipEvent_t   ev_[10];
+    bool         have_filter_ = false;
+    Geometry     last_g_{};
+    CrcTables*   d_tabs_ = nullptr;
+    GenPlan*     d_plan_ = nullptr;
+    // R side
+    DevBuf poolR, metaR, usedR, pchR, pelR, lstartR, lcurR, estartR, istartR, listR;
+    // S side
+    DevBuf poolS, metaS, usedS, pchS, pelS, lstartS, lcurS, estartS, istartS, listS;
+    DevBuf slices, bitmap, rjoin, rqs, surv, survcnt, itemoff, qstot, sqs, sjoin, dense, small;
+};
+
+Engine* engine_for_current_device();
+void    set_last_error(const std::string& s);
+
+}  // namespace hwbrj

@@ -1,0 +1,899 @@
+// hwbrj_kernels.hip -- hand-written CDNA4 (gfx950) kernels for the bloom-filtered radix join.
+//
+// Pipeline (DESIGN.md "Pipeline"; reference: src/parallel_radix_join_bloom.c:1059-1506):
+//   k_scatter    R/S tuples -> F radix partitions of 32-element (128 B) chunks, written through a
+//                per-workgroup LDS write-combining stage (the reference's pass-1, :758-852).
+//                The digit is taken from the bloom *block index* bits, so every partition only
+//                touches a 1/F slice of the filter.
+//   k_list_fill  chunk lists per partition (the reference's task creation, :1183-1253).
+//   k_build      per partition: set the filter bits of its R keys in an LDS slice, write the slice
+//                (bloom add, src/bloom_filter.c:73-132), and sub-partition R codes for the join
+//                (pass-2, :703-748).
+//   k_probe      per item (partition, chunk range): test S elements against the LDS slice
+//                (bloom contains, src/bloom_filter.c:92-141), compact survivors.
+//   k_surv_*     sub-partition survivors for the join (pass-2 of S).
+//   k_join       per (partition, sub): LDS open-addressing table of R codes, probe S codes, count
+//                equal keys (bucket_chaining_join, :259-329).
+// Keys travel as 32-bit "codes" = crc32c(42, key): a bijection of the key, so code equality is key
+// equality and the code's low bits ARE the bloom block index.
+#include <hip/hip_runtime.h>
+
+#include "hwbrj_common.h"
+#include "hwbrj_kernels.h"
+
+namespace hwbrj {
+
+// ================================================================== small device helpers
+__device__ __forceinline__ void load_tab(uint32_t* dst, const uint32_t* src) {
+    for (int i = threadIdx.x; i < 128; i += blockDim.x) dst[i] = src[i];
+}
+
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        uint32_t t = __shfl_up(v, off, 64);
+        if (lane >= off) v += t;
+    }
+    return v;
+}
+
+__device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+    return v;
+}
+
+// Element word -> code (see Format in hwbrj_common.h).
+__device__ __forceinline__ uint32_t decode_code(uint32_t w, uint32_t q, const Geometry& g) {
+    if (g.format == FMT_PACKED) {
+        const uint32_t lowbits = 32u - g.log2F;  // log2F >= 3 for PACKED
+        return ((w & ((1u << lowbits) - 1u)) << g.log2F) | q;
+    }
+    return w;
+}
+
+// Where an element's filter bits live inside its partition slice.
+struct Loc {
+    uint32_t seg;   // slice segment
+    uint32_t base;  // bit offset of the block (or the single bit, basic) inside the segment
+    uint32_t h, y;  // enhanced double hashing state (block-relative)
+};
+
+__device__ __forceinline__ Loc locate(uint32_t w, uint32_t q, const Geometry& g,
+                                      const uint32_t* inv) {
+    Loc L;
+    const uint32_t log2seg = ilog2u(g.seg_bits);
+    if (g.mode == MODE_SLICE_BASIC) {
+        const uint32_t key = code_key(inv, w);
+        const uint32_t b   = mod_m(crapwow(kSeed, key), (uint32_t) g.m);  // add_basic k = 1
+        const uint32_t lb  = b >> g.log2F;
+        L.seg  = lb >> log2seg;
+        L.base = lb & (g.seg_bits - 1u);
+        L.h = L.y = 0;
+        return L;
+    }
+    uint32_t lb;
+    if (g.format == FMT_PACKED) {
+        const uint32_t lowbits = 32u - g.log2F;
+        lb  = w & ((g.nblocks >> g.log2F) - 1u);
+        L.h = w >> lowbits;
+        L.y = 0;
+    } else {
+        const uint32_t key = code_key(inv, w);
+        lb  = (w & (g.nblocks - 1u)) >> g.log2F;
+        L.h = crapwow(kSeed, key) & (g.B - 1u);
+        L.y = (key + kSeed) & (g.B - 1u);
+    }
+    const uint32_t sbit = lb * g.B;
+    L.seg  = sbit >> log2seg;
+    L.base = sbit & (g.seg_bits - 1u);
+    return L;
+}
+
+template <bool SET>
+__device__ __forceinline__ bool apply_bits(const Loc& L, const Geometry& g, uint32_t* slice) {
+    if (g.mode == MODE_SLICE_BASIC) {
+        const uint32_t b = L.base;
+        if (SET) {
+            atomicOr(slice + (b >> 5), 1u << (b & 31u));
+            return true;
+        }
+        return (slice[b >> 5] >> (b & 31u)) & 1u;
+    }
+    uint32_t       h    = L.h, y = L.y;
+    const uint32_t mask = g.B - 1u;
+    const uint32_t secw = g.B < 64u ? g.B : 64u;
+    const uint32_t s0   = h / secw;
+    for (uint32_t i = 0; i < g.k; i++) {
+        const uint32_t pos = (g.variant == VAR_SECTORIZED) ? sectorize(h, s0, i, g.B) : h;
+        const uint32_t b   = L.base + pos;
+        if (SET) {
+            atomicOr(slice + (b >> 5), 1u << (b & 31u));
+        } else if (!((slice[b >> 5] >> (b & 31u)) & 1u)) {
+            return false;
+        }
+        h = (h + y) & mask;
+        y = (y + i + 1u) & mask;
+    }
+    return true;
+}
+
+// ========================================================================= K0: generator
+__global__ void k_gen(uint2* out, uint64_t n, const GenPlan* plan, Perm perm) {
+    uint64_t       i      = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x;
+    const uint64_t stride = (uint64_t) gridDim.x * blockDim.x;
+    for (; i < n; i += stride) {
+        const uint64_t g = perm_apply(perm, i);
+        out[i]           = make_uint2((uint32_t) gen_key_at(*plan, g), (uint32_t) i);
+    }
+}
+
+// ============================================== K1/K2: global-bitmap fallback (MODE_GLOBAL)
+// Reference layout: bit b of the filter = bit (b & 31) of 32-bit word b >> 5 (== byte b >> 3,
+// bit b & 7 on little-endian, as bloom_filter.c addresses it).
+__device__ __forceinline__ void global_positions_apply_add(uint32_t key, uint32_t code,
+                                                           const Geometry& g, uint32_t* bm) {
+    uint64_t base;
+    uint32_t size;
+    if (g.variant == VAR_BASIC) {
+        base = 0;
+        size = (uint32_t) g.m;
+    } else {
+        base = (uint64_t) (code & (g.nblocks - 1u)) * g.block_span;
+        size = g.B;
+    }
+    uint32_t       h  = mod_m(crapwow(kSeed, key), size);
+    uint32_t       y  = mod_m(key + kSeed, size);
+    const uint32_t s0 = (g.variant == VAR_SECTORIZED) ? h / (g.B < 64u ? g.B : 64u) : 0u;
+    for (uint32_t i = 0; i < g.k; i++) {
+        const uint32_t pos = (g.variant == VAR_SECTORIZED) ? sectorize(h, s0, i, g.B) : h;
+        const uint64_t b   = base + pos;
+        atomicOr(bm + (b >> 5), 1u << (uint32_t) (b & 31u));
+        h = mod_m(h + y, size);
+        y = mod_m(y + i + 1u, size);
+    }
+}
+
+__device__ __forceinline__ bool global_contains(uint32_t key, uint32_t code, const Geometry& g,
+                                                const uint32_t* bm) {
+    uint64_t base;
+    uint32_t size;
+    if (g.variant == VAR_BASIC) {
+        base = 0;
+        size = (uint32_t) g.m;
+    } else {
+        base = (uint64_t) (code & (g.nblocks - 1u)) * g.block_span;
+        size = g.B;
+    }
+    uint32_t       h  = mod_m(crapwow(kSeed, key), size);
+    uint32_t       y  = mod_m(key + kSeed, size);
+    const uint32_t s0 = (g.variant == VAR_SECTORIZED) ? h / (g.B < 64u ? g.B : 64u) : 0u;
+    for (uint32_t i = 0; i < g.k; i++) {
+        const uint32_t pos = (g.variant == VAR_SECTORIZED) ? sectorize(h, s0, i, g.B) : h;
+        const uint64_t b   = base + pos;
+        if (!((bm[b >> 5] >> (uint32_t) (b & 31u)) & 1u)) return false;
+        h = mod_m(h + y, size);
+        y = mod_m(y + i + 1u, size);
+    }
+    return true;
+}
+
+__global__ __launch_bounds__(256) void k_build_global(const uint2* R, uint64_t n, Geometry g,
+                                                      const CrcTables* tabs, uint32_t* bm) {
+    __shared__ uint32_t fwd[128];
+    load_tab(fwd, &tabs->fwd[0][0]);
+    __syncthreads();
+    uint64_t       i      = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x;
+    const uint64_t stride = (uint64_t) gridDim.x * blockDim.x;
+    for (; i < n; i += stride) {
+        const uint32_t key = R[i].x;
+        global_positions_apply_add(key, key_code(fwd, key), g, bm);
+    }
+}
+
+// Direct probe of the global bitmap; survivors' codes are appended densely (one atomic per block).
+__global__ __launch_bounds__(1024) void k_probe_global(const uint2* S, uint64_t n, Geometry g,
+                                                       const CrcTables* tabs, const uint32_t* bm,
+                                                       uint32_t* out, uint64_t* out_count) {
+    __shared__ uint32_t fwd[128];
+    __shared__ uint32_t wsum[16];
+    __shared__ uint64_t bbase;
+    load_tab(fwd, &tabs->fwd[0][0]);
+    __syncthreads();
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (uint64_t t0 = (uint64_t) blockIdx.x * 1024; t0 < n; t0 += (uint64_t) gridDim.x * 1024) {
+        const uint64_t i    = t0 + threadIdx.x;
+        uint32_t       code = 0;
+        uint32_t       pass = 0;
+        if (i < n) {
+            const uint32_t key = S[i].x;
+            code               = key_code(fwd, key);
+            pass               = global_contains(key, code, g, bm) ? 1u : 0u;
+        }
+        const uint32_t incl = wave_incl_scan(pass);
+        if (lane == 63) wsum[wave] = incl;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t tot = 0;
+            for (int w = 0; w < 16; w++) {
+                uint32_t c = wsum[w];
+                wsum[w]    = tot;
+                tot += c;
+            }
+            bbase = tot ? atomicAdd((unsigned long long*) out_count, (unsigned long long) tot) : 0;
+        }
+        __syncthreads();
+        if (pass) out[bbase + wsum[wave] + incl - 1] = code;
+        __syncthreads();
+    }
+}
+
+// ================================================================= K3: SWWC partitioning
+// One workgroup per CU (the 128 KiB stage fills the LDS). Each round a workgroup takes 4096
+// elements; element e of partition q goes to stage slot fill[q]++. A partition whose stage reaches
+// 32 elements is flushed as one 128-byte chunk into the workgroup's private chunk region (no
+// cross-workgroup coordination); a round that overfills a partition (skew) writes its extra whole
+// chunks directly. Chunk metadata = partition | count << 16.
+constexpr int kScThreads = 1024;
+
+template <int SRC, int MODE, int FMT>
+__device__ __forceinline__ void sc_word(uint32_t x, const Geometry& g, const uint32_t* fwd,
+                                        uint32_t& w, uint32_t& q) {
+    const uint32_t F1 = (1u << g.log2F) - 1u;
+    if (SRC == SRC_CODES) {  // already a code (fallback survivors)
+        w = x;
+        q = x & F1;
+        return;
+    }
+    const uint32_t key  = x;
+    const uint32_t code = key_code(fwd, key);
+    if (MODE == MODE_SLICE_BASIC) {
+        q = mod_m(crapwow(kSeed, key), (uint32_t) g.m) & F1;
+        w = code;
+    } else if (MODE == MODE_SLICE_BLOCK && FMT == FMT_PACKED) {
+        q = code & F1;
+        w = (code >> g.log2F) | ((crapwow(kSeed, key) & (g.B - 1u)) << (32u - g.log2F));
+    } else {
+        q = code & F1;
+        w = code;
+    }
+}
+
+template <int SRC, int MODE, int FMT>
+__global__ __launch_bounds__(kScThreads) void k_scatter(ScatterParams P) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const uint32_t F     = 1u << P.g.log2F;
+    uint32_t*      stage = lds;            // F * 32
+    uint32_t*      fill  = stage + F * 32; // F
+    uint32_t*      ncb   = fill + F;       // F: chunk base | nchunks << 24 (this round)
+    uint32_t*      tch   = ncb + F;        // F: chunks of q (this workgroup)
+    uint32_t*      tel   = tch + F;        // F: elements of q (this workgroup)
+    uint32_t*      flq   = tel + F;        // F: flush queue
+    uint32_t*      fwd   = flq + F;        // 128
+    uint32_t*      misc  = fwd + 128;      // [0] nflush, [1] chunks used
+
+    const int tid = threadIdx.x;
+    for (uint32_t i = tid; i < F; i += kScThreads) {
+        fill[i] = 0;
+        tch[i]  = 0;
+        tel[i]  = 0;
+    }
+    load_tab(fwd, &P.tabs->fwd[0][0]);
+    if (tid == 0) {
+        misc[0] = 0;
+        misc[1] = 0;
+    }
+    __syncthreads();
+
+    const uint64_t n     = P.n_dev ? *P.n_dev : P.n;
+    const uint64_t units = (n + 3) >> 2;
+    const uint64_t G     = gridDim.x, wg = blockIdx.x;
+    const uint64_t e0    = 4 * (wg * units / G);
+    const uint64_t e1r   = 4 * ((wg + 1) * units / G);
+    const uint64_t e1    = e1r < n ? e1r : n;
+    const uint64_t region = wg * P.cap;
+    uint32_t* __restrict__ pool = P.pool;
+
+    // Raw round data is prefetched one round ahead so the loads overlap the barriers below.
+    uint4 pre0 = make_uint4(0, 0, 0, 0), pre1 = make_uint4(0, 0, 0, 0);
+    auto fetch = [&](uint64_t base, uint4& r0, uint4& r1) {
+        if (SRC == SRC_TUPLES) {
+            const uint2* src = (const uint2*) P.src;
+            const uint64_t i0 = base + 2 * tid, i1 = base + 2048 + 2 * tid;
+            if (i0 + 1 < e1) r0 = *(const uint4*) (src + i0);
+            else if (i0 < e1) r0 = make_uint4(src[i0].x, 0, 0, 0);
+            if (i1 + 1 < e1) r1 = *(const uint4*) (src + i1);
+            else if (i1 < e1) r1 = make_uint4(src[i1].x, 0, 0, 0);
+        } else {
+            const uint32_t* src = (const uint32_t*) P.src;
+            const uint64_t  i   = base + 4 * (uint64_t) tid;
+            if (i + 3 < e1) {
+                r0 = *(const uint4*) (src + i);
+            } else {
+                r0.x = i < e1 ? src[i] : 0u;
+                r0.y = i + 1 < e1 ? src[i + 1] : 0u;
+                r0.z = i + 2 < e1 ? src[i + 2] : 0u;
+                r0.w = 0u;
+            }
+        }
+    };
+    if (e0 < e1) fetch(e0, pre0, pre1);
+    for (uint64_t base = e0; base < e1; base += 4096) {
+        uint32_t x[4];
+        bool     v[4];
+        if (SRC == SRC_TUPLES) {
+            const uint64_t i0 = base + 2 * tid, i1 = base + 2048 + 2 * tid;
+            x[0] = pre0.x; x[1] = pre0.z; x[2] = pre1.x; x[3] = pre1.z;
+            v[0] = i0 < e1; v[1] = i0 + 1 < e1; v[2] = i1 < e1; v[3] = i1 + 1 < e1;
+        } else {
+            const uint64_t i = base + 4 * (uint64_t) tid;
+            x[0] = pre0.x; x[1] = pre0.y; x[2] = pre0.z; x[3] = pre0.w;
+#pragma unroll
+            for (int j = 0; j < 4; j++) v[j] = i + j < e1;
+        }
+        if (base + 4096 < e1) fetch(base + 4096, pre0, pre1);
+        uint32_t wv[4], q[4], e[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            sc_word<SRC, MODE, FMT>(x[j], P.g, fwd, wv[j], q[j]);
+            e[j] = v[j] ? atomicAdd(&fill[q[j]], 1u) : 0u;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+            if (v[j] && e[j] < 32) stage[q[j] * 32 + e[j]] = wv[j];
+        for (uint32_t qq = tid; qq < F; qq += kScThreads) {
+            const uint32_t f = fill[qq];
+            if (f >= 32) {
+                const uint32_t c  = f >> 5;
+                const uint32_t cb = atomicAdd(&misc[1], c);
+                ncb[qq]           = cb | (c << 24);
+                tch[qq] += c;
+                tel[qq] += c * 32;
+                fill[qq]          = f & 31u;
+                flq[atomicAdd(&misc[0], 1u)] = qq;
+                for (uint32_t j = 0; j < c; j++) P.meta[region + cb + j] = qq | (32u << 16);
+            }
+        }
+        __syncthreads();
+        const uint32_t nfl = misc[0];
+        for (uint32_t i = tid >> 3; i < nfl; i += kScThreads / 8) {
+            const uint32_t qq = flq[i];
+            const uint32_t l8 = tid & 7;
+            const uint4    vv = *(const uint4*) &stage[qq * 32 + l8 * 4];
+            *(uint4*) &pool[(region + (ncb[qq] & 0xFFFFFFu)) * 32 + l8 * 4] = vv;
+        }
+        __syncthreads();
+        if (tid == 0) misc[0] = 0;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            if (v[j] && e[j] >= 32) {
+                const uint32_t qq = q[j], ch = e[j] >> 5, s = e[j] & 31u;
+                const uint32_t cb = ncb[qq];
+                if (ch < (cb >> 24))
+                    pool[(region + (cb & 0xFFFFFFu) + ch) * 32 + s] = wv[j];
+                else
+                    stage[qq * 32 + s] = wv[j];
+            }
+        }
+    }
+    __syncthreads();
+    for (uint32_t qq = tid; qq < F; qq += kScThreads) {
+        const uint32_t f = fill[qq];
+        if (f > 0) {
+            const uint32_t cb         = atomicAdd(&misc[1], 1u);
+            P.meta[region + cb]       = qq | (f << 16);
+            for (uint32_t s = 0; s < f; s++) pool[(region + cb) * 32 + s] = stage[qq * 32 + s];
+            tch[qq] += 1;
+            tel[qq] += f;
+        }
+    }
+    __syncthreads();
+    if (tid == 0) P.wg_used[wg] = misc[1];
+    for (uint32_t qq = tid; qq < F; qq += kScThreads) {
+        if (tch[qq]) {
+            atomicAdd(&P.part_chunks[qq], tch[qq]);
+            atomicAdd((unsigned long long*) &P.part_elems[qq], (unsigned long long) tel[qq]);
+        }
+    }
+}
+
+// =================================================================== K4: chunk lists
+__global__ __launch_bounds__(1024) void k_list_fill(const uint32_t* meta, const uint32_t* wg_used,
+                                                    uint64_t cap, uint32_t log2F,
+                                                    uint32_t* list_cursor, uint32_t* list) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const uint32_t F   = 1u << log2F;
+    uint32_t*      cnt = lds;
+    uint32_t*      cur = lds + F;
+    for (uint32_t i = threadIdx.x; i < F; i += blockDim.x) cnt[i] = 0;
+    __syncthreads();
+    const uint64_t region = blockIdx.x * cap;
+    const uint32_t used   = wg_used[blockIdx.x];
+    for (uint32_t i = threadIdx.x; i < used; i += blockDim.x)
+        atomicAdd(&cnt[meta[region + i] & 0xFFFFu], 1u);
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < F; i += blockDim.x)
+        if (cnt[i]) cur[i] = atomicAdd(&list_cursor[i], cnt[i]);
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < used; i += blockDim.x) {
+        const uint32_t q   = meta[region + i] & 0xFFFFu;
+        const uint32_t pos = atomicAdd(&cur[q], 1u);
+        list[pos]          = (uint32_t) (region + i);
+    }
+}
+
+// ======================================================= K5: single-block scans / planning
+// After a scatter: list_start = excl-scan(part_chunks), elem_start = excl-scan(part_elems),
+// item_start = excl-scan(ceil(chunks / CH) * nseg). Arrays have F + 1 entries.
+__global__ __launch_bounds__(1024) void k_plan(const uint32_t* part_chunks,
+                                               const uint64_t* part_elems, uint32_t log2F,
+                                               uint32_t CH, uint32_t nseg, uint32_t* list_start,
+                                               uint32_t* list_cursor, uint64_t* elem_start,
+                                               uint32_t* item_start) {
+    __shared__ uint32_t sc[1024];
+    __shared__ uint32_t si[1024];
+    __shared__ uint64_t se[1024];
+    const uint32_t F = 1u << log2F;
+    const uint32_t t = threadIdx.x;
+    uint32_t c = 0, it = 0;
+    uint64_t e = 0;
+    if (t < F) {
+        c  = part_chunks[t];
+        e  = part_elems[t];
+        it = ((c + CH - 1) / CH) * nseg;
+    }
+    sc[t] = c;
+    si[t] = it;
+    se[t] = e;
+    __syncthreads();
+    for (uint32_t off = 1; off < 1024; off <<= 1) {  // Hillis-Steele inclusive scan
+        uint32_t ac = 0, ai = 0;
+        uint64_t ae = 0;
+        if (t >= off) {
+            ac = sc[t - off];
+            ai = si[t - off];
+            ae = se[t - off];
+        }
+        __syncthreads();
+        sc[t] += ac;
+        si[t] += ai;
+        se[t] += ae;
+        __syncthreads();
+    }
+    if (t < F) {
+        list_start[t + 1] = sc[t];
+        item_start[t + 1] = si[t];
+        elem_start[t + 1] = se[t];
+        list_cursor[t]    = sc[t] - c;
+    }
+    if (t == 0) {
+        list_start[0] = 0;
+        item_start[0] = 0;
+        elem_start[0] = 0;
+    }
+}
+
+// Exclusive scan of n (<= 1M) u64 counts by one block: out[i] = sum_{j<i} in[j], out[n] = total.
+__global__ __launch_bounds__(1024) void k_scan_u64(const uint64_t* in, uint64_t* out, uint32_t n) {
+    __shared__ uint64_t part[1024];
+    const uint32_t t   = threadIdx.x;
+    const uint32_t per = (n + 1023) / 1024;
+    const uint32_t b   = t * per, e = min(b + per, n);
+    uint64_t       s   = 0;
+    for (uint32_t i = b; i < e; i++) s += in[i];
+    part[t] = s;
+    __syncthreads();
+    for (uint32_t off = 1; off < 1024; off <<= 1) {
+        uint64_t a = t >= off ? part[t - off] : 0;
+        __syncthreads();
+        part[t] += a;
+        __syncthreads();
+    }
+    uint64_t run = part[t] - s;
+    for (uint32_t i = b; i < e; i++) {
+        out[i] = run;
+        run += in[i];
+    }
+    if (t == 1023) out[n] = part[1023];
+}
+
+// ======================================================== chunk-walking helper (8 lanes)
+// Threads cooperate 8 per chunk: lane8 loads 4 words (16 B). Returns the number of valid words.
+__device__ __forceinline__ uint32_t load_chunk_quad(const uint32_t* pool, const uint32_t* meta,
+                                                    uint32_t cid, uint32_t l8, uint32_t (&w)[4]) {
+    const uint32_t cnt = meta[cid] >> 16;
+    const uint4    v   = *(const uint4*) &pool[(uint64_t) cid * 32 + l8 * 4];
+    w[0] = v.x;
+    w[1] = v.y;
+    w[2] = v.z;
+    w[3] = v.w;
+    const uint32_t first = l8 * 4;
+    return cnt > first ? min(cnt - first, 4u) : 0u;
+}
+
+// ======================================================================== K6: R build
+// One workgroup per partition q. Filter bits of R go into an LDS slice segment (ds_or), the slice
+// is written once (coalesced); then R codes are written grouped by sub-partition.
+__global__ __launch_bounds__(1024) void k_build(BuildParams P) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const Geometry& g      = P.g;
+    const uint32_t  NSUB   = 1u << g.log2NSUB;
+    const bool      slices = g.mode == MODE_SLICE_BLOCK || g.mode == MODE_SLICE_BASIC;
+    const uint32_t  segw   = slices ? g.seg_words : 0;  // multiple of 4
+    uint32_t*       slice  = lds;
+    uint32_t*       inv    = slice + segw;
+    uint32_t*       subh   = inv + 128;   // NSUB
+    uint64_t*       subc   = (uint64_t*) (subh + 64);  // NSUB (8-byte aligned: segw, 128, 64 even)
+    const uint32_t  q      = blockIdx.x;
+    load_tab(inv, &P.tabs->inv[0][0]);
+    for (uint32_t i = threadIdx.x; i < NSUB; i += blockDim.x) subh[i] = 0;
+    const uint32_t l0 = P.list_start[q], l1 = P.list_start[q + 1];
+    const uint32_t l8 = threadIdx.x & 7, cslot = threadIdx.x >> 3;  // 128 chunks per sweep
+    const uint32_t nseg = slices ? g.nseg : 1;
+    for (uint32_t seg = 0; seg < nseg; seg++) {
+        for (uint32_t i = threadIdx.x; i < segw; i += blockDim.x) slice[i] = 0;
+        __syncthreads();
+        const bool last = seg + 1 == nseg;
+        for (uint32_t l = l0 + cslot; l < l1; l += 128) {
+            uint32_t       w[4];
+            const uint32_t nv = load_chunk_quad(P.pool, P.meta, P.list[l], l8, w);
+            for (uint32_t j = 0; j < nv; j++) {
+                if (slices) {
+                    const Loc L = locate(w[j], q, g, inv);
+                    if (L.seg == seg) apply_bits<true>(L, g, slice);
+                }
+                if (last) {
+                    const uint32_t c = decode_code(w[j], q, g);
+                    atomicAdd(&subh[(c >> g.sub_shift) & (NSUB - 1u)], 1u);
+                }
+            }
+        }
+        __syncthreads();
+        if (slices) {
+            uint4*       dst = (uint4*) (P.slices + ((uint64_t) q * g.nseg + seg) * segw);
+            const uint4* src = (const uint4*) slice;
+            for (uint32_t i = threadIdx.x; i < segw / 4; i += blockDim.x) dst[i] = src[i];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        uint64_t run = P.elem_start[q];
+        for (uint32_t s = 0; s < NSUB; s++) {
+            P.qs_off[(uint64_t) q * NSUB + s] = run;
+            subc[s] = run;
+            run += subh[s];
+        }
+        if (q == gridDim.x - 1) P.qs_off[(uint64_t) gridDim.x * NSUB] = run;
+    }
+    __syncthreads();
+    for (uint32_t l = l0 + cslot; l < l1; l += 128) {
+        uint32_t       w[4];
+        const uint32_t nv = load_chunk_quad(P.pool, P.meta, P.list[l], l8, w);
+        for (uint32_t j = 0; j < nv; j++) {
+            const uint32_t c   = decode_code(w[j], q, g);
+            const uint32_t s   = (c >> g.sub_shift) & (NSUB - 1u);
+            const uint64_t pos = atomicAdd((unsigned long long*) &subc[s], 1ull);
+            P.out_codes[pos]   = c;
+        }
+    }
+}
+
+// ======================================================================== K7: S probe
+// Items = (partition q, slice segment, range of <= CH chunks of q's list). Workgroups take
+// contiguous item ranges, so a slice segment is (re)loaded only when (q, seg) changes.
+__device__ __forceinline__ uint32_t find_q(const uint32_t* item_start, uint32_t F, uint32_t it) {
+    uint32_t lo = 0, hi = F - 1;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        if (item_start[mid] <= it) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+}
+
+__global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const Geometry& g      = P.g;
+    const uint32_t  F      = 1u << g.log2F;
+    const uint32_t  NSUB   = 1u << g.log2NSUB;
+    const bool      slices = g.mode == MODE_SLICE_BLOCK || g.mode == MODE_SLICE_BASIC;
+    const uint32_t  segw   = slices ? g.seg_words : 0;  // multiple of 4
+    uint32_t*       slice  = lds;
+    uint32_t*       inv    = slice + segw;
+    uint32_t*       subc   = inv + 128;  // NSUB
+    uint32_t*       misc   = subc + 64;  // [0] survivor cursor, [1] loaded (q,seg) tag
+    load_tab(inv, &P.tabs->inv[0][0]);
+    for (uint32_t i = threadIdx.x; i < NSUB; i += blockDim.x) subc[i] = 0;
+    if (threadIdx.x == 0) {
+        misc[0] = 0;
+        misc[1] = 0xFFFFFFFFu;
+    }
+    __syncthreads();
+    const uint32_t I   = P.item_start[F];
+    const uint32_t it0 = (uint32_t) ((uint64_t) blockIdx.x * I / gridDim.x);
+    const uint32_t it1 = (uint32_t) ((uint64_t) (blockIdx.x + 1) * I / gridDim.x);
+    const uint32_t nseg = slices ? g.nseg : 1;
+    const uint32_t l8 = threadIdx.x & 7, cslot = threadIdx.x >> 3;
+    const int      lane = threadIdx.x & 63;
+    for (uint32_t it = it0; it < it1; it++) {
+        const uint32_t q     = find_q(P.item_start, F, it);
+        const uint32_t local = it - P.item_start[q];
+        const uint32_t seg   = local % nseg;
+        const uint32_t piece = local / nseg;
+        const uint32_t lq0 = P.list_start[q], lq1 = P.list_start[q + 1];
+        const uint32_t lb  = lq0 + piece * P.CH;
+        const uint32_t le  = min(lq1, lb + P.CH);
+        if (slices) {
+            const uint32_t tag = q * nseg + seg;
+            if (misc[1] != tag) {  // uniform: every thread reads the same LDS word
+                const uint4* src = (const uint4*) (P.slices + (uint64_t) tag * segw);
+                uint4*       dst = (uint4*) slice;
+                for (uint32_t i = threadIdx.x; i < segw / 4; i += blockDim.x) dst[i] = src[i];
+                __syncthreads();
+                if (threadIdx.x == 0) misc[1] = tag;
+            }
+        }
+        __syncthreads();
+        uint32_t* __restrict__ out = P.surv + (uint64_t) seg * P.surv_seg_stride + (uint64_t) lb * 32;
+        for (uint32_t l0 = lb; l0 < le; l0 += 128) {
+            const uint32_t l  = l0 + cslot;
+            uint32_t       w[4];
+            uint32_t       nv = 0;
+            if (l < le) nv = load_chunk_quad(P.pool, P.meta, P.list[l], l8, w);
+            uint32_t keep[4];
+            uint32_t ns = 0;
+            for (uint32_t j = 0; j < nv; j++) {
+                bool pass = true;
+                if (slices) {
+                    const Loc L = locate(w[j], q, g, inv);
+                    pass = (L.seg == seg) && apply_bits<false>(L, g, slice);
+                }
+                if (pass) {
+                    const uint32_t c = decode_code(w[j], q, g);
+                    keep[ns++]       = c;
+                    atomicAdd(&subc[(c >> g.sub_shift) & (NSUB - 1u)], 1u);
+                }
+            }
+            const uint32_t incl = wave_incl_scan(ns);
+            uint32_t       wb   = 0;
+            if (lane == 63 && incl) wb = atomicAdd(&misc[0], incl);
+            wb = __shfl(wb, 63, 64);
+            const uint32_t o = wb + incl - ns;
+            for (uint32_t j = 0; j < ns; j++) out[o + j] = keep[j];
+        }
+        __syncthreads();
+        for (uint32_t s = threadIdx.x; s < NSUB; s += blockDim.x) {
+            P.surv_cnt[(uint64_t) it * NSUB + s] = subc[s];
+            subc[s]                             = 0;
+        }
+        if (threadIdx.x == 0) misc[0] = 0;
+        __syncthreads();
+    }
+}
+
+// ============================================ K8: survivor offsets per (q, sub) and per item
+// One block per partition, one thread per sub: relative offsets of each item inside (q, sub)
+// and the (q, sub) totals.
+__global__ void k_surv_totals(const uint32_t* item_start, const uint32_t* surv_cnt,
+                              uint32_t log2NSUB, uint32_t* item_off, uint64_t* qs_tot) {
+    const uint32_t q = blockIdx.x, NSUB = 1u << log2NSUB;
+    const uint32_t i0 = item_start[q], i1 = item_start[q + 1];
+    for (uint32_t s = threadIdx.x; s < NSUB; s += blockDim.x) {
+        uint64_t run = 0;
+        for (uint32_t it = i0; it < i1; it++) {
+            item_off[(uint64_t) it * NSUB + s] = (uint32_t) run;
+            run += surv_cnt[(uint64_t) it * NSUB + s];
+        }
+        qs_tot[(uint64_t) q * NSUB + s] = run;
+    }
+}
+
+// K9: move each item's survivors into the (q, sub)-grouped join layout.
+__global__ __launch_bounds__(256) void k_surv_scatter(SurvParams P) {
+    __shared__ uint64_t cur[64];
+    const uint32_t F = 1u << P.log2F, NSUB = 1u << P.log2NSUB;
+    const uint32_t I = P.item_start[F];
+    for (uint32_t it = blockIdx.x; it < I; it += gridDim.x) {
+        const uint32_t q     = find_q(P.item_start, F, it);
+        const uint32_t local = it - P.item_start[q];
+        const uint32_t seg   = local % P.nseg;
+        const uint32_t piece = local / P.nseg;
+        const uint32_t lb    = P.list_start[q] + piece * P.CH;
+        __syncthreads();
+        uint32_t total = 0;
+        for (uint32_t s = 0; s < NSUB; s++) total += P.surv_cnt[(uint64_t) it * NSUB + s];
+        for (uint32_t s = threadIdx.x; s < NSUB; s += blockDim.x)
+            cur[s] = P.qs_off[(uint64_t) q * NSUB + s] + P.item_off[(uint64_t) it * NSUB + s];
+        __syncthreads();
+        const uint32_t* src = P.surv + (uint64_t) seg * P.surv_seg_stride + (uint64_t) lb * 32;
+        for (uint32_t i = threadIdx.x; i < total; i += blockDim.x) {
+            const uint32_t c   = src[i];
+            const uint32_t s   = (c >> P.sub_shift) & (NSUB - 1u);
+            const uint64_t pos = atomicAdd((unsigned long long*) &cur[s], 1ull);
+            P.out[pos]         = c;
+        }
+    }
+}
+
+// ========================================================================= K10: join
+// One workgroup per (q, sub): R codes -> LDS open-addressing table (linear probing, occupancy
+// bits claimed with ds_or), then every S code walks its cluster counting equal codes. R runs
+// larger than the table are processed in pieces (S is re-streamed per piece).
+constexpr uint32_t kJoinLog2T  = 14;
+constexpr uint32_t kJoinT      = 1u << kJoinLog2T;
+constexpr uint32_t kJoinPiece  = kJoinT / 2;
+
+__device__ __forceinline__ uint32_t join_slot(uint32_t c, uint32_t shift) {
+    return ((c >> shift) * 0x9E3779B1u) >> (32 - kJoinLog2T);
+}
+
+__global__ __launch_bounds__(512) void k_join(JoinParams P) {
+    __shared__ uint32_t keys[kJoinT];
+    __shared__ uint32_t occ[kJoinT / 32];
+    __shared__ uint64_t wsum[8];
+    const uint32_t job = blockIdx.x;
+    const uint64_t r0 = P.r_off[job], r1 = P.r_off[job + 1];
+    const uint64_t s0 = P.s_off[job], s1 = P.s_off[job + 1];
+    if (r1 == r0 || s1 == s0) return;
+    uint64_t cnt = 0;
+    for (uint64_t rb = r0; rb < r1; rb += kJoinPiece) {
+        const uint64_t re = min(r1, rb + kJoinPiece);
+        for (uint32_t i = threadIdx.x; i < kJoinT / 32; i += blockDim.x) occ[i] = 0;
+        __syncthreads();
+        for (uint64_t i = rb + threadIdx.x; i < re; i += blockDim.x) {
+            const uint32_t c = P.r_codes[i];
+            uint32_t       h = join_slot(c, P.hash_shift);
+            while (true) {
+                const uint32_t bit = 1u << (h & 31u);
+                const uint32_t old = atomicOr(&occ[h >> 5], bit);
+                if (!(old & bit)) {
+                    keys[h] = c;
+                    break;
+                }
+                h = (h + 1u) & (kJoinT - 1u);
+            }
+        }
+        __syncthreads();
+        for (uint64_t i = s0 + threadIdx.x; i < s1; i += blockDim.x) {
+            const uint32_t c = P.s_codes[i];
+            uint32_t       h = join_slot(c, P.hash_shift);
+            while ((occ[h >> 5] >> (h & 31u)) & 1u) {
+                cnt += keys[h] == c;
+                h = (h + 1u) & (kJoinT - 1u);
+            }
+        }
+        __syncthreads();
+    }
+    cnt = wave_sum_u64(cnt);
+    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = cnt;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t t = 0;
+        for (uint32_t w = 0; w < blockDim.x / 64; w++) t += wsum[w];
+        if (t) atomicAdd((unsigned long long*) P.result, (unsigned long long) t);
+    }
+}
+
+// ============================================== K11: export the filter in reference layout
+// Output word o holds reference bits 32*o .. 32*o+31 (src/bloom_filter.c byte addressing).
+__global__ void k_export(const uint32_t* slices, Geometry g, uint32_t* out, uint64_t nwords) {
+    uint64_t       o      = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x;
+    const uint64_t stride = (uint64_t) gridDim.x * blockDim.x;
+    const uint32_t log2seg = ilog2u(g.seg_bits), segw = g.seg_words;
+    for (; o < nwords; o += stride) {
+        uint32_t r = 0;
+        for (uint32_t t = 0; t < 32; t++) {
+            const uint64_t gb = o * 32 + t;
+            uint32_t       q, lb;
+            if (g.mode == MODE_SLICE_BASIC) {
+                q  = (uint32_t) (gb & ((1u << g.log2F) - 1u));
+                lb = (uint32_t) (gb >> g.log2F);
+            } else {
+                const uint32_t blk = (uint32_t) (gb / g.B), h = (uint32_t) (gb % g.B);
+                q  = blk & ((1u << g.log2F) - 1u);
+                lb = (blk >> g.log2F) * g.B + h;
+            }
+            const uint32_t seg = lb >> log2seg, off = lb & (g.seg_bits - 1u);
+            const uint32_t* s  = slices + ((uint64_t) q * g.nseg + seg) * segw;
+            r |= ((s[off >> 5] >> (off & 31u)) & 1u) << t;
+        }
+        out[o] = r;
+    }
+}
+
+// ===================================================================== launch wrappers
+void launch_gen(uint2* out, uint64_t n, const GenPlan* d_plan, const Perm& perm, hipStream_t st) {
+    k_gen<<<4096, 256, 0, st>>>(out, n, d_plan, perm);
+}
+
+void launch_build_global(const uint2* R, uint64_t n, const Geometry& g, const CrcTables* tabs,
+                         uint32_t* bm, hipStream_t st) {
+    k_build_global<<<4096, 256, 0, st>>>(R, n, g, tabs, bm);
+}
+
+void launch_probe_global(const uint2* S, uint64_t n, const Geometry& g, const CrcTables* tabs,
+                         const uint32_t* bm, uint32_t* out, uint64_t* out_count, hipStream_t st) {
+    k_probe_global<<<2048, 1024, 0, st>>>(S, n, g, tabs, bm, out, out_count);
+}
+
+size_t scatter_lds_bytes(uint32_t log2F) {
+    const size_t F = 1u << log2F;
+    return (F * 32 + F * 5 + 128 + 4) * sizeof(uint32_t);
+}
+
+template <int SRC, int MODE, int FMT>
+static void scatter_inst(const ScatterParams& p, uint32_t grid, hipStream_t st) {
+    const size_t lds = scatter_lds_bytes(p.g.log2F);
+    (void) hipFuncSetAttribute((const void*) &k_scatter<SRC, MODE, FMT>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds);
+    k_scatter<SRC, MODE, FMT><<<grid, kScThreads, lds, st>>>(p);
+}
+
+void launch_scatter(const ScatterParams& p, int src, uint32_t grid, hipStream_t st) {
+    const Geometry& g = p.g;
+    if (src == SRC_CODES) return scatter_inst<SRC_CODES, MODE_GLOBAL, FMT_CODE>(p, grid, st);
+    switch (g.mode) {
+        case MODE_SLICE_BLOCK:
+            if (g.format == FMT_PACKED)
+                return scatter_inst<SRC_TUPLES, MODE_SLICE_BLOCK, FMT_PACKED>(p, grid, st);
+            return scatter_inst<SRC_TUPLES, MODE_SLICE_BLOCK, FMT_CODE>(p, grid, st);
+        case MODE_SLICE_BASIC:
+            return scatter_inst<SRC_TUPLES, MODE_SLICE_BASIC, FMT_CODE>(p, grid, st);
+        default: return scatter_inst<SRC_TUPLES, MODE_NOBLOOM, FMT_CODE>(p, grid, st);
+    }
+}
+
+void launch_list_fill(const uint32_t* meta, const uint32_t* wg_used, uint64_t cap, uint32_t log2F,
+                      uint32_t* list_cursor, uint32_t* list, uint32_t grid, hipStream_t st) {
+    k_list_fill<<<grid, 1024, (2u << log2F) * sizeof(uint32_t), st>>>(meta, wg_used, cap, log2F,
+                                                                      list_cursor, list);
+}
+
+void launch_plan(const uint32_t* part_chunks, const uint64_t* part_elems, uint32_t log2F,
+                 uint32_t CH, uint32_t nseg, uint32_t* list_start, uint32_t* list_cursor,
+                 uint64_t* elem_start, uint32_t* item_start, hipStream_t st) {
+    k_plan<<<1, 1024, 0, st>>>(part_chunks, part_elems, log2F, CH, nseg, list_start, list_cursor,
+                               elem_start, item_start);
+}
+
+void launch_scan_u64(const uint64_t* in, uint64_t* out, uint32_t n, hipStream_t st) {
+    k_scan_u64<<<1, 1024, 0, st>>>(in, out, n);
+}
+
+size_t slice_lds_bytes(const Geometry& g) {
+    const bool slices = g.mode == MODE_SLICE_BLOCK || g.mode == MODE_SLICE_BASIC;
+    return ((slices ? g.seg_words : 0) + 128 + 64 + 2 * 64 + 4) * sizeof(uint32_t);
+}
+
+void launch_build(const BuildParams& p, uint32_t F, hipStream_t st) {
+    const size_t lds = slice_lds_bytes(p.g);
+    (void) hipFuncSetAttribute((const void*) &k_build, hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds);
+    k_build<<<F, 1024, lds, st>>>(p);
+}
+
+void launch_probe(const ProbeParams& p, uint32_t grid, hipStream_t st) {
+    const size_t lds = slice_lds_bytes(p.g);
+    (void) hipFuncSetAttribute((const void*) &k_probe, hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds);
+    k_probe<<<grid, 1024, lds, st>>>(p);
+}
+
+void launch_surv_totals(const uint32_t* item_start, const uint32_t* surv_cnt, uint32_t log2F,
+                        uint32_t log2NSUB, uint32_t* item_off, uint64_t* qs_tot, hipStream_t st) {
+    k_surv_totals<<<1u << log2F, 64, 0, st>>>(item_start, surv_cnt, log2NSUB, item_off, qs_tot);
+}
+
+void launch_surv_scatter(const SurvParams& p, uint32_t grid, hipStream_t st) {
+    k_surv_scatter<<<grid, 256, 0, st>>>(p);
+}
+
+void launch_join(const JoinParams& p, uint32_t jobs, hipStream_t st) {
+    k_join<<<jobs, 512, 0, st>>>(p);
+}
+
+void launch_export(const uint32_t* slices, const Geometry& g, uint32_t* out, uint64_t nwords,
+                   hipStream_t st) {
+    k_export<<<2048, 256, 0, st>>>(slices, g, out, nwords);
+}
+
+}  // namespace hwbrj

@@ -1,0 +1,211 @@
+// mchashjoins.cpp -- CLI driver with the reference's flags and stdout (src/main.c:351-731),
+// running the join through libhwbrj.so's BPRO / PRO on an MI355X.
+//
+// Differences from the reference driver (DESIGN.md "CLI"):
+//   -b sectorized    selects this build's SECTORIZED filter (the reference silently runs BASIC);
+//   -a               PRO is the only algorithm behind this boundary (others print an error);
+//   -z / --non-unique / --full-range are not generated yet (error);
+//   relations are generated with the reference's key multiset and a seeded (-x / -y) Feistel
+//   shuffle instead of the time-seeded Knuth shuffle (src/generator.c:173-176).
+#include <getopt.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <climits>
+#include <cmath>
+#include <string>
+#include <thread>
+
+#include "hwbrj.h"
+
+struct Params {
+    std::string algo        = "PRO";
+    uint32_t    nthreads    = 2;
+    uint64_t    r_size      = 128000000;
+    uint64_t    s_size      = 128000000;
+    uint32_t    r_seed      = 12345;
+    uint32_t    s_seed      = 54321;
+    double      skew        = 0.0;
+    double      selectivity = 1.0;
+    const char* loadR       = nullptr;
+    const char* loadS       = nullptr;
+    bool        bloom       = false;
+    bloom_filter_args_t bf  = {BASIC, 256ull << 20, 8, 1024};  // src/main.c:389-393
+    int         gpus        = 1;
+};
+
+static void print_help(const char* prog) {
+    printf("Usage: %s [options]\n", prog);
+    printf(
+        "    Join algorithm selection, algorithms : PRO (MI355X)                         \n"
+        "       -a --algo=<name>    Run the hash join algorithm named <name> [PRO]      \n"
+        "                                                                               \n"
+        "    Other join configuration options, with default values in [] :              \n"
+        "       -n --nthreads=<N>  Number of threads to use <N> [2]                     \n"
+        "       -r --r-size=<R>    Number of tuples in build relation R <R> [128000000] \n"
+        "       -s --s-size=<S>    Number of tuples in probe relation S <S> [128000000] \n"
+        "       -x --r-seed=<x>    Seed value for generating relation R <x> [12345]     \n"
+        "       -y --s-seed=<y>    Seed value for generating relation S <y> [54321]     \n"
+        "       -q --s-sel=<q>     Selectivity for %% of S-tuples with a match in R [1.0]\n"
+        "       -R --r-file=<Rf>   The file to load build relation R from <Rf> [R.tbl]  \n"
+        "       -S --s-file=<Sf>   The file to load probe relation S from <Sf> [S.tbl]  \n"
+        "                                                                               \n"
+        "    Bloom Filter options:                                                      \n"
+        "       -b --bloom-filter=<b>     no, basic, blocked, sectorized (this build)   \n"
+        "       -k --bloom-hashes=<k>     number of bits set per tuple                  \n"
+        "       -m --bloom-size=<m>       number of filter entries in bits              \n"
+        "       -B --bloom-block-size=<B> number of bits per block (B = 2^x)            \n"
+        "       --gpus=<G>                MI355X devices (S range-sharded) [1]          \n"
+        "        -h --help         Show this message                                    \n"
+        "        --version         Show version                                         \n");
+}
+
+// src/generator.c:685-741: "key payload" or "key,payload" per line, '#' comments.
+static int load_relation(relation_t* rel, const char* path, uint64_t n) {
+    FILE* fp = fopen(path, "r");
+    if (!fp) {
+        perror(path);
+        return -1;
+    }
+    rel->tuples     = (tuple_t*) malloc(sizeof(tuple_t) * (n ? n : 1));
+    rel->num_tuples = n;
+    char     line[256];
+    uint64_t i = 0;
+    while (i < n && fgets(line, sizeof line, fp)) {
+        if (line[0] == '#') continue;
+        for (char* c = line; *c; c++)
+            if (*c == ',' || *c == '|') *c = ' ';
+        long long k, p;
+        if (sscanf(line, "%lld %lld", &k, &p) != 2) continue;
+        rel->tuples[i].key     = (int32_t) k;
+        rel->tuples[i].payload = (int32_t) p;
+        i++;
+    }
+    fclose(fp);
+    rel->num_tuples = i;
+    return 0;
+}
+
+int main(int argc, char** argv) {
+    Params         P;
+    static int     nonunique = 0, fullrange = 0, basic_numa = 0, verbose = 0;
+    static option  opts[] = {{"verbose", no_argument, &verbose, 1},
+                            {"brief", no_argument, &verbose, 0},
+                            {"non-unique", no_argument, &nonunique, 1},
+                            {"full-range", no_argument, &fullrange, 1},
+                            {"basic-numa", no_argument, &basic_numa, 1},
+                            {"help", no_argument, 0, 'h'},
+                            {"version", no_argument, 0, 'v'},
+                            {"algo", required_argument, 0, 'a'},
+                            {"nthreads", required_argument, 0, 'n'},
+                            {"perfconf", required_argument, 0, 'p'},
+                            {"r-size", required_argument, 0, 'r'},
+                            {"s-size", required_argument, 0, 's'},
+                            {"perfout", required_argument, 0, 'o'},
+                            {"r-seed", required_argument, 0, 'x'},
+                            {"s-seed", required_argument, 0, 'y'},
+                            {"s-sel", required_argument, 0, 'q'},
+                            {"skew", required_argument, 0, 'z'},
+                            {"r-file", required_argument, 0, 'R'},
+                            {"s-file", required_argument, 0, 'S'},
+                            {"bloom-filter", required_argument, 0, 'b'},
+                            {"bloom-size", required_argument, 0, 'm'},
+                            {"bloom-hashes", required_argument, 0, 'k'},
+                            {"bloom-block-size", required_argument, 0, 'B'},
+                            {"gpus", required_argument, 0, 'G'},
+                            {0, 0, 0, 0}};
+    int c, idx = 0;
+    while ((c = getopt_long(argc, argv, "a:n:p:q:r:s:o:x:y:z:R:S:b:m:k:B:Z:A:hv", opts, &idx)) != -1) {
+        switch (c) {
+            case 0: break;
+            case 'a':
+                if (strcmp(optarg, "PRO") != 0) {
+                    printf("[ERROR] Join algorithm named `%s' does not exist in this build (PRO only)!\n",
+                           optarg);
+                    print_help(argv[0]);
+                    exit(EXIT_SUCCESS);
+                }
+                P.algo = optarg;
+                break;
+            case 'h':
+            case '?': print_help(argv[0]); exit(EXIT_SUCCESS);
+            case 'v': printf("\n%s\n\n", hwbrj_version()); exit(EXIT_SUCCESS);
+            case 'n': P.nthreads = (uint32_t) atoi(optarg); break;
+            case 'q': P.selectivity = atof(optarg); break;
+            case 'r': P.r_size = (uint64_t) atol(optarg); break;
+            case 's': P.s_size = (uint64_t) atol(optarg); break;
+            case 'x': P.r_seed = (uint32_t) atoi(optarg); break;
+            case 'y': P.s_seed = (uint32_t) atoi(optarg); break;
+            case 'z': P.skew = atof(optarg); break;
+            case 'R': P.loadR = optarg; break;
+            case 'S': P.loadS = optarg; break;
+            case 'b':  // src/main.c:692-698 (+ sectorized)
+                P.bloom = strcmp(optarg, "no") != 0;
+                if (strcmp(optarg, "basic") == 0) P.bf.variant = BASIC;
+                else if (strcmp(optarg, "blocked") == 0) P.bf.variant = BLOCKED;
+                else if (strcmp(optarg, "sectorized") == 0) P.bf.variant = SECTORIZED;
+                break;
+            case 'm': P.bf.m = (uint64_t) atoll(optarg); break;
+            case 'k': P.bf.k = (uint64_t) atoi(optarg); break;
+            case 'B': P.bf.B = (uint64_t) atoi(optarg); break;
+            case 'G': P.gpus = atoi(optarg); break;
+            default: break;
+        }
+    }
+    if (P.bloom) assert_args(&P.bf);  // src/main.c:730
+    if (P.skew > 0 || nonunique || fullrange) {
+        printf("[ERROR] -z / --non-unique / --full-range generation is not available in this build\n");
+        exit(EXIT_FAILURE);
+    }
+    if (P.gpus != 1) {
+        printf("[ERROR] --gpus=%d: the CLI drives one device; use bench.py for N>1\n", P.gpus);
+        exit(EXIT_FAILURE);
+    }
+    if (P.nthreads == 0) P.nthreads = 1;
+    const int hthreads = (int) std::thread::hardware_concurrency();
+
+    relation_t relR, relS;
+    fprintf(stdout, "[INFO ] %s relation R with size = %.3lf MiB, #tuples = %llu : ",
+            P.loadS ? "Loading" : "Creating", 8.0 * P.r_size / 1024.0 / 1024.0,
+            (unsigned long long) P.r_size);
+    fflush(stdout);
+    if (P.loadR) {
+        if (load_relation(&relR, P.loadR, P.r_size)) exit(EXIT_FAILURE);
+    } else {
+        relR.num_tuples = P.r_size;
+        relR.tuples     = (tuple_t*) malloc(sizeof(tuple_t) * (P.r_size ? P.r_size : 1));
+        if (!relR.tuples ||
+            hwbrj_generate_host(relR.tuples, P.r_size, P.nthreads, P.r_size, P.r_size, 1.0,
+                                P.r_seed, hthreads)) {
+            printf("[ERROR] generating R: %s\n", hwbrj_last_error());
+            exit(EXIT_FAILURE);
+        }
+    }
+    printf("OK \n");
+    fprintf(stdout, "[INFO ] %s relation S with size = %.3lf MiB, #tuples = %lld : ",
+            P.loadS ? "Loading" : "Creating", 8.0 * P.s_size / 1024.0 / 1024.0,
+            (long long) P.s_size);
+    fflush(stdout);
+    if (P.loadS) {
+        if (load_relation(&relS, P.loadS, P.s_size)) exit(EXIT_FAILURE);
+    } else {
+        relS.num_tuples = P.s_size;
+        relS.tuples     = (tuple_t*) malloc(sizeof(tuple_t) * (P.s_size ? P.s_size : 1));
+        if (!relS.tuples ||
+            hwbrj_generate_host(relS.tuples, P.s_size, P.nthreads, INT_MAX, P.r_size, P.selectivity,
+                                P.s_seed, hthreads)) {
+            printf("[ERROR] generating S: %s\n", hwbrj_last_error());
+            exit(EXIT_FAILURE);
+        }
+    }
+    printf("OK \n");
+    printf("[INFO ] Running join algorithm %s ...\n", P.algo.c_str());
+    result_t* res = P.bloom ? BPRO(&relR, &relS, (int) P.nthreads, &P.bf)
+                            : PRO(&relR, &relS, (int) P.nthreads);
+    printf("[INFO ] Results = %llu. DONE.\n", (unsigned long long) res->totalresults);
+    free(relR.tuples);
+    free(relS.tuples);
+    free(res);
+    return 0;
+}

@@ -1,0 +1,123 @@
+/*
+ * hwbrj.h -- C-ABI of libhwbrj.so, the MI355X drop-in for the reference's bloom radix join.
+ *
+ * Reference interfaces replaced (paths relative to the Briimbo/HwBloomRadixJoin root):
+ *   tuple_t, relation_t, threadresult_t, result_t   src/types.h:37-63 (KEY_8B off: 8-byte tuples)
+ *   bloom_filter_variant_t, bloom_filter_args_t     src/bloom_filter.h:10, :50-55
+ *   BPRO                                            src/parallel_radix_join_bloom.h:34-36
+ *                                                   (impl. src/parallel_radix_join_bloom.c:1781-1787)
+ *   PRO                                             src/parallel_radix_join.h:33-34 (impl. :1697-1700)
+ *   assert_args                                     src/bloom_filter.h:80-81 (impl. bloom_filter.c:25-34)
+ *
+ * BPRO/PRO keep the reference's contract: caller-owned host relations, a malloc'd result_t the
+ * caller frees, the reference's stdout lines ("S-tuples after filter", the timing block), and
+ * print + exit(EXIT_FAILURE) on fatal errors. Inputs are copied to HBM (hipMemcpy) outside the
+ * timed region, like the reference allocates its tmp buffers before its timer starts.
+ *
+ * The hwbrj_* entry points are this build's additions: the same join on device-resident data,
+ * generators, and test hooks. They return 0 on success and a nonzero code otherwise
+ * (message in hwbrj_last_error()).
+ */
+#ifndef HWBRJ_H
+#define HWBRJ_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- reference-compatible types (layouts identical to src/types.h, src/bloom_filter.h) ---- */
+typedef int32_t intkey_t;
+typedef int32_t value_t;
+
+typedef struct tuple_t {
+    intkey_t key;
+    value_t  payload;
+} tuple_t;
+
+typedef struct relation_t {
+    tuple_t * tuples;
+    uint64_t  num_tuples;
+} relation_t;
+
+typedef struct threadresult_t {
+    int64_t  nresults;
+    void *   results;
+    uint32_t threadid;
+} threadresult_t;
+
+typedef struct result_t {
+    int64_t          totalresults;
+    threadresult_t * resultlist; /* NULL: results are counted, not materialized (reference default) */
+    int              nthreads;
+} result_t;
+
+/* BASIC = 0 and BLOCKED = 1 as in the reference. SECTORIZED is this build's extension
+ * (DESIGN.md "Filter variants"); the reference has no such variant. */
+typedef enum { BASIC = 0, BLOCKED = 1, SECTORIZED = 2 } bloom_filter_variant_t;
+
+typedef struct bloom_filter_args_t {
+    bloom_filter_variant_t variant;
+    uint64_t               m; /* filter size in bits (power of 2, <= 2^32) */
+    uint64_t               k; /* hashes per key */
+    uint64_t               B; /* block size in bits (power of 2, divides m) */
+} bloom_filter_args_t;
+
+/* ---- drop-in operator boundary ---- */
+result_t * BPRO(relation_t * relR, relation_t * relS, int nthreads,
+                bloom_filter_args_t * bloom_filter_args);
+result_t * PRO(relation_t * relR, relation_t * relS, int nthreads);
+void       assert_args(bloom_filter_args_t * args);
+
+/* ---- device-resident entry points (this build) ---- */
+typedef struct hwbrj_stats_t {
+    uint64_t filtered;      /* "S-tuples after filter" (= |S| without a filter) */
+    int64_t  matches;       /* "Results" */
+    int      mode;          /* 0 nobloom, 1 slice-blocked, 2 slice-basic, 3 global fallback */
+    int      format;        /* 0 code words, 1 packed words */
+    uint32_t partitions;    /* F */
+    uint32_t subparts;      /* join sub-partitions per partition */
+    uint32_t slice_segments;
+    /* device time (ms, HIP events on the join stream) */
+    double   ms_total;
+    double   ms_r_scatter;  /* R -> partitions */
+    double   ms_r_index;
+    double   ms_build;      /* filter slices + R sub-partitioning (or global build) */
+    double   ms_s_scatter;  /* S -> partitions (the dominant, HBM-bound kernel) */
+    double   ms_s_index;
+    double   ms_probe;      /* filter probe + survivor compaction */
+    double   ms_surv;       /* survivor sub-partitioning */
+    double   ms_join;
+} hwbrj_stats_t;
+
+/* Join device-resident tuple arrays (tuple_t layout). args == NULL runs PRO (no filter).
+ * stream: a hipStream_t (NULL = the library's own stream). The call is synchronous. */
+int hwbrj_join_device(const tuple_t * d_R, uint64_t nR, const tuple_t * d_S, uint64_t nS,
+                      const bloom_filter_args_t * args, void * stream, hwbrj_stats_t * stats);
+
+/* Fill d_out / out with the reference generator's key multiset (src/generator.c:304-415 with
+ * `nthreads` generator threads) in a seeded permuted order; payload = row index. */
+int hwbrj_generate_device(tuple_t * d_out, uint64_t n, uint32_t nthreads, uint64_t maxid,
+                          uint64_t threshold, double selectivity, uint64_t seed, void * stream);
+int hwbrj_generate_host(tuple_t * out, uint64_t n, uint32_t nthreads, uint64_t maxid,
+                        uint64_t threshold, double selectivity, uint64_t seed, int host_threads);
+
+/* The filter built by the last join, in the reference's byte layout (src/bloom_filter.c:143-171:
+ * m/8 bytes, bit h of a block at byte h>>3, bit h&7). nbytes must be m/8. */
+int hwbrj_export_filter(uint8_t * host_out, uint64_t nbytes);
+
+/* Scalar hashes on the host (test hooks): crc32c(seed,key) and CrapWow(seed,key). */
+uint32_t hwbrj_hash_crc(uint32_t seed, int32_t key);
+uint32_t hwbrj_hash_crapwow(uint32_t seed, int32_t key);
+
+int          hwbrj_device_count(void);
+int          hwbrj_set_device(int device);
+void         hwbrj_release(void); /* free all device buffers */
+const char * hwbrj_last_error(void);
+const char * hwbrj_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HWBRJ_H */

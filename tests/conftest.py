@@ -1,0 +1,36 @@
+"""Shared test setup: the `gpu` marker, import paths, and the oracle build."""
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP kernels)")
+
+
+@pytest.fixture(scope="session")
+def orc():
+    from oracle import pyoracle
+    if not os.path.exists(pyoracle.LIB):
+        pyoracle.build()
+    return pyoracle
+
+
+@pytest.fixture(scope="session")
+def hw():
+    import hwbloomradixjoin_amd as hw
+    hw.lib()  # raises if libhwbrj.so is missing: no silent fallback
+    return hw
+
+
+@pytest.fixture(scope="session")
+def cuda():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch
