@@ -1,0 +1,224 @@
+#!/usr/bin/env python3
+"""bench.py -- headline benchmark of the MI355X bloom radix join (BASELINE.json metric).
+
+One step = one full BPRO join (filter build + probe + both partition passes + join + count) over
+HBM-resident synthetic relations with the reference generator's key multiset
+(src/generator.c:304-415): |R| = 128M, |S| = 1024M, q = 0.01, -b blocked, m = 2^30, k = 1,
+B = 1024 (the reference default, src/main.c:393). value = probe tuples (|S|) per second over the
+whole job.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (N > 1)
+
+N > 1: one rank per GPU (RCCL backend). S is range-sharded over the ranks (total |S| fixed:
+strong scaling, --scaling weak gives every rank a full |S|); R is replicated and every rank
+builds the filter from it, so the data path has no collective. Counts are summed with one
+all_reduce after the timed region.
+
+Prints ONE JSON line (rank 0) with roofline (dominant kernel, HIP-event timed) and cpu_baseline
+(the oracle's multithreaded restatement of the reference, "port", on a bounded sample).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "probe-tuples/sec, |R|=128M |S|=1024M q=0.01, 1/2/4/8 MI355X; %HBM roofline"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+# golden counts of the reference binary at this exact config
+GOLDEN = {(128000000, 1024000000, 0.01, "blocked", 1 << 30, 1, 1024): (124236515, 10240000)}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("-r", "--r-size", type=int, default=128000000)
+    ap.add_argument("-s", "--s-size", type=int, default=1024000000)
+    ap.add_argument("-q", "--s-sel", type=float, default=0.01)
+    ap.add_argument("-b", "--bloom-filter", default="blocked")
+    ap.add_argument("-m", "--bloom-size", type=int, default=1 << 30)
+    ap.add_argument("-k", "--bloom-hashes", type=int, default=1)
+    ap.add_argument("-B", "--bloom-block-size", type=int, default=1024)
+    ap.add_argument("-n", "--nthreads", type=int, default=2, help="generator threads (multiset)")
+    ap.add_argument("--scaling", choices=("strong", "weak"), default="strong")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample", type=int, default=256000000, help="S tuples in the CPU sample")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r01_pmc_traffic.json"))
+    return ap.parse_args()
+
+
+def phase_bytes(ph: str, nR: int, nS: int, filtered: int, m: int) -> float:
+    """Algorithmic bytes per launch of each pipeline phase (DESIGN.md "Roofline"): every input
+    tuple read once (8 B), every partitioned 4-byte word written once and read once."""
+    return {
+        "r_scatter": 8.0 * nR + 4.0 * nR,
+        "build": 4.0 * nR + m / 8.0 + 4.0 * nR,
+        "s_scatter": 8.0 * nS + 4.0 * nS,
+        "probe": 4.0 * nS + 4.0 * filtered,
+        "surv": 8.0 * filtered,
+        "join": 4.0 * nR + 4.0 * filtered,
+    }.get(ph, 0.0)
+
+
+def main():
+    a = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import torch
+    import hwbloomradixjoin_amd as hw
+
+    torch.cuda.set_device(local)
+    hw.lib().hwbrj_set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    nR, nS_total = a.r_size, a.s_size
+    if a.scaling == "strong":
+        lo, hi = hw.shard_range(nS_total, rank, world)
+        total_units = nS_total
+    else:
+        lo, hi = 0, nS_total
+        total_units = nS_total * world
+    nS = hi - lo
+    dR = torch.empty((nR, 2), dtype=torch.int32, device="cuda")
+    dS = torch.empty((nS, 2), dtype=torch.int32, device="cuda")
+    hw.generate_device(dR, a.nthreads, nR, nR, 1.0, 12345)  # src/main.c:410-431 (-x 12345)
+    hw.generate_device_range(dS, nS_total, lo, a.nthreads, 2**31 - 1, nR, a.s_sel,
+                             54321 + (rank if a.scaling == "weak" else 0))  # :443-466 (-y 54321)
+    torch.cuda.synchronize()
+    args = hw.BloomFilterArgs.from_flag(a.bloom_filter, a.bloom_size, a.bloom_hashes,
+                                        a.bloom_block_size)
+
+    # one untimed parity run (counts reduced over ranks)
+    st = hw.join_device(dR, dS, args)
+    counts = torch.tensor([st.filtered, st.matches], dtype=torch.int64, device="cuda")
+    if dist:
+        dist.all_reduce(counts)
+    filtered, matches = (int(x) for x in counts.tolist())
+    for _ in range(a.warmup):
+        hw.join_device(dR, dS, args)
+
+    sums = {}
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        st = hw.join_device(dR, dS, args)
+        for f in ("ms_total", "ms_r_scatter", "ms_r_index", "ms_build", "ms_s_scatter",
+                  "ms_s_index", "ms_probe", "ms_surv", "ms_join"):
+            sums[f] = sums.get(f, 0.0) + getattr(st, f)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    if rank != 0:
+        if dist:
+            dist.destroy_process_group()
+        return
+
+    K = max(a.steps, 1)
+    mean = {k: v / K for k, v in sums.items()}
+    phases = ["r_scatter", "build", "s_scatter", "probe", "surv", "join"]
+    dom = max(phases, key=lambda p: mean["ms_" + p])
+    local_filtered = st.filtered
+    bytes_dom = phase_bytes(dom, nR, nS, local_filtered, a.bloom_size if args else 0)
+    achieved = bytes_dom / (mean["ms_" + dom] * 1e-3) / 1e9
+    traffic = None
+    if os.path.exists(a.pmc_json):
+        try:
+            pm = json.load(open(a.pmc_json))
+            if pm.get("config_key") == [nR, nS, a.s_sel, a.bloom_filter, a.bloom_size,
+                                        a.bloom_hashes, a.bloom_block_size]:
+                traffic = pm.get("phases", {}).get(dom, {}).get("hbm_bytes")
+        except (OSError, ValueError):
+            traffic = None
+    roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "kernel": dom, "algorithmic_bytes": bytes_dom,
+                "kernel_ms": round(mean["ms_" + dom], 4)}
+
+    cpu = None
+    if world == 1 and not a.no_cpu_baseline:
+        cpu = cpu_baseline(a, hw)
+
+    key = (nR, nS_total, a.s_sel, a.bloom_filter, a.bloom_size, a.bloom_hashes, a.bloom_block_size)
+    gold = GOLDEN.get(key)
+    value = total_units * a.steps / elapsed
+    out = {
+        "metric": METRIC,
+        "value": round(value, 1),
+        "unit": "probe-tuples/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(elapsed / K * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": a.scaling,
+        "vs_baseline": None,
+        "dtype": "int32",
+        "data": "synthetic: reference generator key multiset, seeded permutation, in HBM",
+        "config": {"workload": f"PRO + -b {a.bloom_filter}, |R|={nR} |S|={nS_total} q={a.s_sel}, "
+                               f"m={a.bloom_size} k={a.bloom_hashes} B={a.bloom_block_size}",
+                   "r_size": nR, "s_size": nS_total, "selectivity": a.s_sel,
+                   "bloom": a.bloom_filter, "m": a.bloom_size, "k": a.bloom_hashes,
+                   "B": a.bloom_block_size, "parallelism": f"S range-sharded x{world}, R replicated"},
+        "roofline": roofline,
+        "cpu_baseline": cpu,
+        "parity": {"filtered": filtered, "matches": matches,
+                   "golden": list(gold) if gold else None,
+                   "ok": (gold == (filtered, matches)) if gold else None},
+        "phase_ms": {k[3:]: round(v, 4) for k, v in mean.items()},
+        "published_ref": {"value": 3.98e8, "config": "blocked B=512 k=1 m=2^30, 2x Xeon Gold 6226 "
+                          "48 threads (thesis data, BASELINE.md)"},
+    }
+    print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(a, hw):
+    """The oracle's pthreads restatement of BPRO (oracle/oracle.c), full R and full filter size,
+    on the first --cpu-sample tuples of S; probe-tuples/s over its TOTAL-TIME region."""
+    try:
+        from oracle import pyoracle as orc
+        sample = min(a.cpu_sample, a.s_size)
+        R = hw.generate_host(a.r_size, a.nthreads, a.r_size, a.r_size, 1.0, 12345, a.cpu_threads)
+        # a |S|=sample relation of the same generator (same q, same key ranges)
+        S = hw.generate_host(sample, a.nthreads, 2**31 - 1, a.r_size, a.s_sel, 54321,
+                             a.cpu_threads)
+        variant = {"basic": 0, "blocked": 1, "sectorized": 2}.get(a.bloom_filter, 0)
+        use = a.bloom_filter != "no"
+        res, filt, tm = orc.bpro(R, S, a.cpu_threads, variant, a.bloom_size, a.bloom_hashes,
+                                 a.bloom_block_size, use)
+        secs = tm["total"] / 1e6
+        return {"value": round(sample / secs, 1), "unit": "probe-tuples/s",
+                "cores": a.cpu_threads, "kind": "port",
+                "sample": f"|R|={a.r_size} (full), |S| sample={sample} tuples of the same "
+                          f"generator (q={a.s_sel}), m={a.bloom_size}; oracle orc_bpro "
+                          f"TOTAL-TIME {secs:.3f} s, filtered={filt} matches={res}"}
+    except Exception as e:  # the baseline is reported, never required for the GPU line
+        return {"value": None, "unit": "probe-tuples/s", "cores": a.cpu_threads, "kind": "port",
+                "sample": f"failed: {e}"}
+
+
+if __name__ == "__main__":
+    main()

@@ -17,8 +17,9 @@ import numpy as np
 
 __all__ = [
     "BASIC", "BLOCKED", "SECTORIZED", "BloomFilterArgs", "Relation", "Result", "Stats",
-    "BPRO", "PRO", "assert_args", "join_device", "generate_device", "generate_host",
-    "export_filter", "hash_crc", "hash_crapwow", "lib", "LIB_PATH",
+    "BPRO", "PRO", "assert_args", "join_device", "generate_device", "generate_device_range",
+    "generate_host",
+    "export_filter", "hash_crc", "hash_crapwow", "lib", "LIB_PATH", "shard_range",
 ]
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
@@ -83,6 +84,11 @@ def lib() -> ctypes.CDLL:
         L.hwbrj_generate_device.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
                                             ctypes.c_uint64, ctypes.c_uint64, ctypes.c_double,
                                             ctypes.c_uint64, ctypes.c_void_p]
+        L.hwbrj_generate_device_range.restype = ctypes.c_int
+        L.hwbrj_generate_device_range.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
+                                                  ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64,
+                                                  ctypes.c_uint64, ctypes.c_double, ctypes.c_uint64,
+                                                  ctypes.c_void_p]
         L.hwbrj_generate_host.restype = ctypes.c_int
         L.hwbrj_generate_host.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
                                           ctypes.c_uint64, ctypes.c_uint64, ctypes.c_double,
@@ -226,6 +232,15 @@ def generate_device(out, nthreads: int, maxid: int, threshold: int, selectivity:
                                      selectivity, seed, sp), "hwbrj_generate_device")
 
 
+def generate_device_range(out, n: int, offset: int, nthreads: int, maxid: int, threshold: int,
+                          selectivity: float, seed: int, stream=None) -> None:
+    """Rows [offset, offset + out.shape[0]) of the n-row relation generate_device would build."""
+    sp = ctypes.c_void_p(stream.cuda_stream) if stream is not None else None
+    _err(lib().hwbrj_generate_device_range(_ptr(out), n, offset, out.shape[0], nthreads, maxid,
+                                           threshold, selectivity, seed, sp),
+         "hwbrj_generate_device_range")
+
+
 def generate_host(n: int, nthreads: int, maxid: int, threshold: int, selectivity: float,
                   seed: int, host_threads: int = 0) -> np.ndarray:
     """The same relation as generate_device, on the host: (n, 2) int32."""
@@ -240,6 +255,13 @@ def export_filter(m_bits: int) -> np.ndarray:
     out = np.empty(m_bits // 8, dtype=np.uint8)
     _err(lib().hwbrj_export_filter(out.ctypes.data, out.nbytes), "hwbrj_export_filter")
     return out
+
+
+def shard_range(n: int, rank: int, world: int) -> tuple[int, int]:
+    """Rows [lo, hi) of an n-row relation owned by `rank` of `world` (range sharding of S, the
+    multi-GPU analogue of the reference's per-thread chunking,
+    src/parallel_radix_join_bloom.c:1646-1670: equal chunks, the remainder spread evenly)."""
+    return rank * n // world, (rank + 1) * n // world
 
 
 def hash_crc(seed: int, key: int) -> int:

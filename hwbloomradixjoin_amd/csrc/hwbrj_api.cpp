@@ -66,8 +66,20 @@ int hwbrj_generate_device(tuple_t* d_out, uint64_t n, uint32_t nthreads, uint64_
         set_last_error("no HIP device");
         return 10;
     }
-    return e->generate((uint2*) d_out, n, nthreads, maxid, threshold, selectivity, seed,
+    return e->generate((uint2*) d_out, n, 0, n, nthreads, maxid, threshold, selectivity, seed,
                        (hipStream_t) stream);
+}
+
+int hwbrj_generate_device_range(tuple_t* d_out, uint64_t n, uint64_t offset, uint64_t count,
+                                uint32_t nthreads, uint64_t maxid, uint64_t threshold,
+                                double selectivity, uint64_t seed, void* stream) {
+    Engine* e = engine_for_current_device();
+    if (!e) {
+        set_last_error("no HIP device");
+        return 10;
+    }
+    return e->generate((uint2*) d_out, n, offset, count, nthreads, maxid, threshold, selectivity,
+                       seed, (hipStream_t) stream);
 }
 
 int hwbrj_generate_host(tuple_t* out, uint64_t n, uint32_t nthreads, uint64_t maxid,

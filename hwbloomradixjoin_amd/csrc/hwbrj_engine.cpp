@@ -461,8 +461,9 @@ int Engine::export_filter(uint8_t* host_out, uint64_t nbytes) {
     return 0;
 }
 
-int Engine::generate(uint2* d_out, uint64_t n, uint32_t nthreads, uint64_t maxid,
-                     uint64_t threshold, double selectivity, uint64_t seed, hipStream_t stream) {
+int Engine::generate(uint2* d_out, uint64_t n, uint64_t offset, uint64_t count, uint32_t nthreads,
+                     uint64_t maxid, uint64_t threshold, double selectivity, uint64_t seed,
+                     hipStream_t stream) {
     HWBRJ_CHECK(hipSetDevice(device_));
     std::vector<GenPlan> plan(1);
     if (make_gen_plan(&plan[0], n, nthreads, maxid, threshold, selectivity)) {
@@ -471,7 +472,11 @@ int Engine::generate(uint2* d_out, uint64_t n, uint32_t nthreads, uint64_t maxid
     }
     if (!stream) stream = own_stream_;
     HWBRJ_CHECK(hipMemcpyAsync(d_plan_, plan.data(), sizeof(GenPlan), hipMemcpyHostToDevice, stream));
-    launch_gen(d_out, n, d_plan_, make_perm(n, seed), stream);
+    if (offset > n || count > n - offset) {
+        set_last_error("generator range outside the relation");
+        return 2;
+    }
+    launch_gen(d_out, offset, count, d_plan_, make_perm(n, seed), stream);
     HWBRJ_CHECK(hipGetLastError());
     HWBRJ_CHECK(hipStreamSynchronize(stream));
     return 0;

@@ -32,8 +32,9 @@ class Engine {
     int  run(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
              const bloom_filter_args_t* args, hipStream_t stream, hwbrj_stats_t* st);
     int  export_filter(uint8_t* host_out, uint64_t nbytes);
-    int  generate(uint2* d_out, uint64_t n, uint32_t nthreads, uint64_t maxid, uint64_t threshold,
-                  double selectivity, uint64_t seed, hipStream_t stream);
+    int  generate(uint2* d_out, uint64_t n, uint64_t offset, uint64_t count, uint32_t nthreads,
+                  uint64_t maxid, uint64_t threshold, double selectivity, uint64_t seed,
+                  hipStream_t stream);
     void release();
     int  device() const { return device_; }
 

@@ -75,7 +75,8 @@ struct JoinParams {
     uint64_t*       result;
 };
 
-void   launch_gen(uint2* out, uint64_t n, const GenPlan* d_plan, const Perm& perm, hipStream_t st);
+void   launch_gen(uint2* out, uint64_t offset, uint64_t count, const GenPlan* d_plan, const Perm& perm,
+                  hipStream_t st);
 void   launch_build_global(const uint2* R, uint64_t n, const Geometry& g, const CrcTables* tabs,
                            uint32_t* bm, hipStream_t st);
 void   launch_probe_global(const uint2* S, uint64_t n, const Geometry& g, const CrcTables* tabs,

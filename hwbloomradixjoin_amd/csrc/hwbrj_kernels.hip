@@ -120,12 +120,13 @@ __device__ __forceinline__ bool apply_bits(const Loc& L, const Geometry& g, uint
 }
 
 // ========================================================================= K0: generator
-__global__ void k_gen(uint2* out, uint64_t n, const GenPlan* plan, Perm perm) {
+__global__ void k_gen(uint2* out, uint64_t offset, uint64_t count, const GenPlan* plan, Perm perm) {
     uint64_t       i      = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x;
     const uint64_t stride = (uint64_t) gridDim.x * blockDim.x;
-    for (; i < n; i += stride) {
-        const uint64_t g = perm_apply(perm, i);
-        out[i]           = make_uint2((uint32_t) gen_key_at(*plan, g), (uint32_t) i);
+    for (; i < count; i += stride) {
+        const uint64_t row = offset + i;
+        const uint64_t g   = perm_apply(perm, row);
+        out[i]             = make_uint2((uint32_t) gen_key_at(*plan, g), (uint32_t) row);
     }
 }
 
@@ -803,8 +804,9 @@ __global__ void k_export(const uint32_t* slices, Geometry g, uint32_t* out, uint
 }
 
 // ===================================================================== launch wrappers
-void launch_gen(uint2* out, uint64_t n, const GenPlan* d_plan, const Perm& perm, hipStream_t st) {
-    k_gen<<<4096, 256, 0, st>>>(out, n, d_plan, perm);
+void launch_gen(uint2* out, uint64_t offset, uint64_t count, const GenPlan* d_plan, const Perm& perm,
+                hipStream_t st) {
+    k_gen<<<4096, 256, 0, st>>>(out, offset, count, d_plan, perm);
 }
 
 void launch_build_global(const uint2* R, uint64_t n, const Geometry& g, const CrcTables* tabs,

@@ -100,6 +100,10 @@ int hwbrj_join_device(const tuple_t * d_R, uint64_t nR, const tuple_t * d_S, uin
  * `nthreads` generator threads) in a seeded permuted order; payload = row index. */
 int hwbrj_generate_device(tuple_t * d_out, uint64_t n, uint32_t nthreads, uint64_t maxid,
                           uint64_t threshold, double selectivity, uint64_t seed, void * stream);
+/* Rows [offset, offset + count) of the same n-row relation (for range-sharding S over ranks). */
+int hwbrj_generate_device_range(tuple_t * d_out, uint64_t n, uint64_t offset, uint64_t count,
+                                uint32_t nthreads, uint64_t maxid, uint64_t threshold,
+                                double selectivity, uint64_t seed, void * stream);
 int hwbrj_generate_host(tuple_t * out, uint64_t n, uint32_t nthreads, uint64_t maxid,
                         uint64_t threshold, double selectivity, uint64_t seed, int host_threads);
 

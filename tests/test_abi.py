@@ -1,0 +1,110 @@
+"""CPU tests of the drop-in boundary: libhwbrj.so loads and exports every symbol include/hwbrj.h
+declares, the host-side pieces (hashes, generator, argument checks, CLI parsing) agree with the
+oracle. No GPU compute here."""
+import json
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+GOLD = json.load(open(os.path.join(HERE, "golden", "survey_counts.json")))
+KATS = json.load(open(os.path.join(HERE, "golden", "ref_kats.json")))
+INT_MAX = 2**31 - 1
+
+
+def declared_functions():
+    src = open(os.path.join(ROOT, "include", "hwbrj.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    names = re.findall(r"\b([A-Za-z_][A-Za-z0-9_]*)\s*\([^;{]*\)\s*;", src)
+    return sorted(set(n for n in names if n not in ("if", "while", "for", "sizeof")))
+
+
+def test_library_exports_every_declared_symbol(hw):
+    names = declared_functions()
+    assert {"BPRO", "PRO", "assert_args", "hwbrj_join_device"} <= set(names)
+    out = subprocess.run(["nm", "-D", "--defined-only", hw.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    exported = {line.split()[-1] for line in out.splitlines() if " T " in line}
+    missing = [n for n in names if n not in exported]
+    assert not missing, missing
+
+
+def test_struct_layouts_match_reference(hw):
+    import ctypes
+    # src/types.h:37-63, src/bloom_filter.h:50-55 on x86-64
+    assert ctypes.sizeof(hw._Tuple) == 8
+    assert ctypes.sizeof(hw._Relation) == 16
+    assert ctypes.sizeof(hw._Result) == 24
+    assert ctypes.sizeof(hw._BloomArgs) == 32
+    assert hw.BASIC == 0 and hw.BLOCKED == 1
+
+
+def test_host_hashes_match_reference_kats(hw):
+    for row in KATS["kats"]:
+        assert hw.hash_crc(42, row["key"]) == row["crc32c"]
+        assert hw.hash_crapwow(42, row["key"]) == row["crapwow"]
+        assert hw.hash_crc(7, row["key"]) == row["crc32c_seed7"]
+
+
+@pytest.mark.parametrize("n,nthr,maxid,thr,q", [
+    (1000000, 2, 1000000, 1000000, 1.0),
+    (16000000, 2, INT_MAX, 1000000, 0.01),
+    (2000000, 3, INT_MAX, 250000, 0.001),
+    (1000, 7, INT_MAX, 100, 0.5),
+    (4095, 1, INT_MAX, 4095, 0.0),
+    (100, 16, 100, 100, 1.0),
+    (50000, 5, INT_MAX, 333, 1.0),
+])
+def test_host_generator_is_reference_multiset(hw, orc, n, nthr, maxid, thr, q):
+    t = hw.generate_host(n, nthr, maxid, thr, q, 99, 4)
+    assert np.array_equal(t[:, 1], np.arange(n, dtype=np.int64).astype(np.int32))
+    want = np.sort(orc.gen_keys(n, nthr, maxid, thr, q))
+    assert np.array_equal(np.sort(t[:, 0]), want)
+
+
+def test_host_generator_seeds_permute(hw):
+    a = hw.generate_host(100000, 2, 100000, 100000, 1.0, 1, 2)
+    b = hw.generate_host(100000, 2, 100000, 100000, 1.0, 2, 2)
+    assert not np.array_equal(a[:, 0], b[:, 0])
+    assert np.array_equal(np.sort(a[:, 0]), np.sort(b[:, 0]))
+
+
+@pytest.mark.parametrize("variant,m,B", [(1, 1 << 20, 512), (1, 3 << 20, 512), (1, 1 << 20, 48),
+                                         (1, 1 << 10, 2048), (0, 1 << 20, 48), (0, 7, 1),
+                                         (2, 1 << 20, 64), (1, 1 << 20, 0)])
+def test_assert_args_matches_reference_rules(hw, orc, variant, m, B):
+    ref_invalid = bool(orc.lib().orc_bloom_args_invalid(min(variant, 1), m, B))
+    assert hw.assert_args(hw.BloomFilterArgs(variant, m, 1, B)) == (not ref_invalid)
+
+
+def test_from_flag_mirrors_cli_parsing(hw):
+    assert hw.BloomFilterArgs.from_flag("no", 1, 1) is None
+    assert hw.BloomFilterArgs.from_flag("blocked", 1 << 20, 2).variant == hw.BLOCKED
+    assert hw.BloomFilterArgs.from_flag("basic", 1 << 20, 2).variant == hw.BASIC
+    assert hw.BloomFilterArgs.from_flag("whatever", 1 << 20, 2).variant == hw.BASIC  # main.c:692
+    assert hw.BloomFilterArgs.from_flag("sectorized", 1 << 20, 2).variant == hw.SECTORIZED
+
+
+def test_cli_help_and_errors(hw):
+    cli = hw.CLI_PATH
+    out = subprocess.run([cli, "-h"], capture_output=True, text=True, timeout=60)
+    assert out.returncode == 0 and "--bloom-filter" in out.stdout
+    out = subprocess.run([cli, "-a", "NPO"], capture_output=True, text=True, timeout=60)
+    assert "does not exist" in out.stdout
+    # src/bloom_filter.c:25-34: invalid filter arguments print and exit(1)
+    out = subprocess.run([cli, "-b", "blocked", "-m", "1000", "-r", "10", "-s", "10"],
+                         capture_output=True, text=True, timeout=60)
+    assert out.returncode == 1 and "m must be a power of 2" in out.stdout
+
+
+def test_package_refuses_without_library(tmp_path):
+    # the product path must fail loudly when the HIP library is missing (no CPU fallback)
+    code = ("import sys, os; sys.path.insert(0, %r); import hwbloomradixjoin_amd as hw; "
+            "hw.LIB_PATH = os.path.join(%r, 'nope.so'); hw._LIB = None\n"
+            "try:\n    hw.lib()\nexcept ImportError as e:\n    print('RAISED', e)\n") % (ROOT, str(tmp_path))
+    out = subprocess.run(["python3", "-c", code], capture_output=True, text=True, timeout=120)
+    assert "RAISED" in out.stdout

@@ -1,0 +1,231 @@
+"""GPU parity tests: the HIP path (through the C-ABI) against the reference's counts and the oracle.
+
+Bar: bit-exact. `filtered` ("S-tuples after filter", src/parallel_radix_join_bloom.c:1253) and
+`Results` (src/main.c:480) must equal the golden counts / the oracle on the same inputs, and the
+exported filter must be byte-identical to the reference's bloom_filter.c bitmap.
+"""
+import hashlib
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLD = json.load(open(os.path.join(HERE, "golden", "survey_counts.json")))
+FILT = json.load(open(os.path.join(HERE, "golden", "ref_filters.json")))
+INT_MAX = 2**31 - 1
+VAR = {"basic": 0, "blocked": 1}
+
+
+def dev_rel(hw, cuda, n, maxid, thr, q, seed, nthr=2):
+    t = cuda.empty((n, 2), dtype=cuda.int32, device="cuda")
+    if n:
+        hw.generate_device(t, nthr, maxid, thr, q, seed)
+    return t
+
+
+def to_dev(cuda, a):
+    return cuda.from_numpy(np.ascontiguousarray(a, dtype=np.int32)).cuda()
+
+
+@pytest.fixture(scope="module")
+def f3(hw, cuda):
+    g = GOLD["F3_grid"]
+    return (dev_rel(hw, cuda, g["r"], g["r"], g["r"], 1.0, 11),
+            dev_rel(hw, cuda, g["s"], INT_MAX, g["r"], g["q"], 22))
+
+
+@pytest.mark.parametrize("Bname", ["32", "64", "128", "256", "512", "1024", "basic"])
+def test_f3_grid(hw, f3, Bname):
+    g = GOLD["F3_grid"]
+    R, S = f3
+    for k, want in zip(g["k"], g["rows"][Bname]):
+        v, B = (hw.BASIC, 1024) if Bname == "basic" else (hw.BLOCKED, int(Bname))
+        st = hw.join_device(R, S, hw.BloomFilterArgs(v, g["m"], k, B))
+        assert (st.filtered, st.matches) == (want, g["results"]), (Bname, k, st)
+
+
+def test_f3_extra_and_pro(hw, cuda, f3):
+    g = GOLD["F3_grid"]
+    R, S = f3
+    for row in g["extra"]:
+        st = hw.join_device(R, S, hw.BloomFilterArgs(VAR[row["variant"]], g["m"], row["k"], row["B"]))
+        assert (st.filtered, st.matches) == (row["filtered"], g["results"])
+    S1 = dev_rel(hw, cuda, g["s"], INT_MAX, g["r"], 1.0, 5)  # BASELINE config 1 (-b no, q=1.0)
+    st = hw.join_device(R, S1, None)
+    assert st.matches == st.filtered == g["nobloom_q1_results"]
+
+
+@pytest.mark.parametrize("row", GOLD["F1_fast"] + GOLD["F1_mid"],
+                         ids=lambda r: f"{r['variant']}-r{r['r']}-m{r['m']}-k{r['k']}-s{r['s']}")
+def test_f1_rows(hw, cuda, row):
+    R = dev_rel(hw, cuda, row["r"], row["r"], row["r"], 1.0, 3)
+    S = dev_rel(hw, cuda, row["s"], INT_MAX, row["r"], row["q"], 4)
+    st = hw.join_device(R, S, hw.BloomFilterArgs(VAR[row["variant"]], row["m"], row["k"], row["B"]))
+    assert (st.filtered, st.matches) == (row["filtered"], row["results"])
+
+
+@pytest.fixture(scope="module")
+def full_scale(hw, cuda):
+    """The north-star relations: |R| = 128M, |S| = 1024M (S regenerated per q)."""
+    nR = 128000000
+    R = dev_rel(hw, cuda, nR, nR, nR, 1.0, 12345)
+    cache = {}
+
+    def S_for(q):
+        if q not in cache:
+            cache.clear()
+            cuda.cuda.empty_cache()
+            cache[q] = dev_rel(hw, cuda, 1024000000, INT_MAX, nR, q, 54321)
+        return cache[q]
+    return R, S_for
+
+
+def test_northstar_golden(hw, full_scale):
+    g = GOLD["F4_northstar"]
+    R, S_for = full_scale
+    S = S_for(g["q"])
+    st = hw.join_device(R, S, hw.BloomFilterArgs(hw.BLOCKED, g["m"], 1, g["B"]))
+    assert (st.filtered, st.matches) == (g["k1_filtered"], g["results"])
+    st = hw.join_device(R, S, hw.BloomFilterArgs(hw.BLOCKED, g["m"], 2, g["B"]))
+    assert (st.filtered, st.matches) == (g["k2_filtered"], g["results"])
+    # the full-size filter popcount (F2) through the export path
+    for row in [r for r in GOLD["F2_popcount"] if r["r"] == 128000000]:
+        hw.join_device(R, S, hw.BloomFilterArgs(VAR[row["variant"]], row["m"], row["k"], row["B"]))
+        bm = hw.export_filter(row["m"])
+        assert int(np.unpackbits(bm).sum()) == row["popcount"]
+
+
+@pytest.mark.parametrize("row", GOLD["F1_published"],
+                         ids=lambda r: f"{r['variant']}-q{r['q']}-m{r['m']}-k{r['k']}-B{r['B']}")
+def test_published_thesis_rows(hw, full_scale, row):
+    R, S_for = full_scale
+    st = hw.join_device(R, S_for(row["q"]),
+                        hw.BloomFilterArgs(VAR[row["variant"]], row["m"], row["k"], row["B"]))
+    assert (st.filtered, st.matches) == (row["filtered"], row["results"])
+
+
+@pytest.mark.parametrize("case", FILT["cases"], ids=lambda c: f"v{c['variant']}-m{c['m']}-k{c['k']}-B{c['B']}")
+def test_filter_bytes_identical_to_reference(hw, cuda, orc, case):
+    R = orc.gen_keys(FILT["r"], FILT["nthreads"], FILT["r"], FILT["r"], 1.0, 7)
+    S = orc.gen_keys(FILT["s"], FILT["nthreads"], INT_MAX, FILT["r"], FILT["q"], 8)
+    dR = to_dev(cuda, np.stack([R, np.arange(R.size, dtype=np.int32)], 1))
+    dS = to_dev(cuda, np.stack([S, np.arange(S.size, dtype=np.int32)], 1))
+    st = hw.join_device(dR, dS, hw.BloomFilterArgs(case["variant"], case["m"], case["k"], case["B"]))
+    assert st.filtered == case["filtered"]
+    bm = hw.export_filter(case["m"])
+    assert hashlib.sha256(bm.tobytes()).hexdigest() == case["sha256"]
+
+
+def oracle_check(hw, cuda, orc, Rk, Sk, args, nthr=4):
+    R = np.stack([Rk.astype(np.int32), np.arange(Rk.size, dtype=np.int32)], 1)
+    S = np.stack([Sk.astype(np.int32), np.arange(Sk.size, dtype=np.int32)], 1)
+    st = hw.join_device(to_dev(cuda, R.reshape(-1, 2)), to_dev(cuda, S.reshape(-1, 2)), args)
+    if args is None:
+        res, filt, _ = orc.bpro(R, S, nthr, 0, 0, 0, 0, use_bloom=False)
+    else:
+        res, filt, _ = orc.bpro(R, S, nthr, args.variant, args.m, args.k, args.B)
+    assert (st.filtered, st.matches) == (filt, res), (st, filt, res)
+    return st
+
+
+ARGS = [None, ("blocked", 1 << 20, 1, 1024), ("blocked", 1 << 22, 3, 512), ("basic", 1 << 20, 1, 0),
+        ("basic", 1 << 20, 3, 0), ("sectorized", 1 << 20, 1, 1024), ("sectorized", 1 << 22, 4, 512),
+        ("blocked", 1 << 16, 2, 4), ("blocked", 1 << 31, 2, 512), ("blocked", 64, 1, 32)]
+
+
+def mk(hw, a):
+    return None if a is None else hw.BloomFilterArgs.from_flag(a[0], a[1], a[2], a[3] or 1024)
+
+
+@pytest.mark.parametrize("a", ARGS, ids=str)
+def test_edge_sizes(hw, cuda, orc, a):
+    args = mk(hw, a)
+    rng = np.random.default_rng(3)
+    for nR, nS in [(0, 1000), (1000, 0), (1, 1), (1, 5000), (7, 33), (4097, 4099), (100003, 400009)]:
+        Rk = rng.permutation(nR).astype(np.int64) + 1
+        Sk = rng.integers(0, 2 * max(nR, 1) + 2, size=nS)
+        oracle_check(hw, cuda, orc, Rk, Sk, args)
+
+
+@pytest.mark.parametrize("a", ARGS[:6], ids=str)
+def test_duplicates_negatives_and_extremes(hw, cuda, orc, a):
+    args = mk(hw, a)
+    rng = np.random.default_rng(4)
+    Rk = np.concatenate([rng.integers(-3000, 3000, size=60000),
+                         np.array([INT_MAX, -INT_MAX - 1, 0, -1, 42] * 3)])
+    Sk = np.concatenate([rng.integers(-4000, 4000, size=500000),
+                         np.array([INT_MAX, -INT_MAX - 1, 0, -1, 42, 43] * 7)])
+    oracle_check(hw, cuda, orc, Rk, Sk, args)
+
+
+@pytest.mark.parametrize("a", ARGS[:4], ids=str)
+def test_skewed_probe_side(hw, cuda, orc, a):
+    """Zipf-like skew: a few hot keys carry most of S (one partition gets most of the work)."""
+    args = mk(hw, a)
+    rng = np.random.default_rng(5)
+    nR = 200000
+    Rk = rng.permutation(nR) + 1
+    ranks = rng.zipf(1.3, size=3000000)
+    Sk = np.where(ranks <= nR, ranks, rng.integers(nR + 1, 10 * nR, size=ranks.size))
+    oracle_check(hw, cuda, orc, Rk, Sk, args)
+    Sk1 = np.full(1000000, 77)  # every S tuple on one key
+    st = oracle_check(hw, cuda, orc, Rk, Sk1, args)
+    assert st.matches == Sk1.size
+
+
+def test_hot_build_key_chunked_join(hw, cuda, orc):
+    """One key repeated in R beyond the LDS table capacity: the join processes R in pieces."""
+    Rk = np.concatenate([np.full(20000, 5), np.arange(100, 50000)])
+    Sk = np.concatenate([np.full(3000, 5), np.arange(0, 60000)])
+    st = oracle_check(hw, cuda, orc, Rk, Sk, mk(hw, ("blocked", 1 << 20, 1, 1024)))
+    assert st.matches == 20000 * 3001 + (50000 - 100)
+
+
+def test_repeatable_and_buffer_reuse(hw, cuda, f3):
+    R, S = f3
+    a = hw.BloomFilterArgs(hw.BLOCKED, 1 << 24, 1, 1024)
+    first = hw.join_device(R, S, a)
+    small = hw.join_device(R[:1000], S[:5000], a)  # shrink, then grow again
+    again = hw.join_device(R, S, a)
+    assert (first.filtered, first.matches) == (again.filtered, again.matches)
+    assert small.matches <= 5000
+
+
+def test_generate_device_matches_host(hw, cuda):
+    for (n, nthr, maxid, thr, q) in [(1000000, 2, 1000000, 1000000, 1.0), (3000001, 3, INT_MAX, 100000, 0.01)]:
+        d = dev_rel(hw, cuda, n, maxid, thr, q, 9, nthr).cpu().numpy()
+        h = hw.generate_host(n, nthr, maxid, thr, q, 9, 8)
+        assert np.array_equal(d, h)
+        part = cuda.empty((n // 3, 2), dtype=cuda.int32, device="cuda")
+        hw.generate_device_range(part, n, n // 2, nthr, maxid, thr, q, 9)
+        assert np.array_equal(part.cpu().numpy(), h[n // 2: n // 2 + n // 3])
+
+
+def test_bpro_host_boundary_stdout(hw, capfd):
+    """BPRO over host relation_t (H2D inside), stdout lines of the reference (run.py regexes)."""
+    g = GOLD["F3_grid"]
+    R = hw.Relation(hw.generate_host(g["r"], 2, g["r"], g["r"], 1.0, 1))
+    S = hw.Relation(hw.generate_host(g["s"], 2, INT_MAX, g["r"], g["q"], 2))
+    res = hw.BPRO(R, S, 4, hw.BloomFilterArgs(hw.BLOCKED, g["m"], 1, 1024))
+    out = capfd.readouterr().out
+    assert res.totalresults == g["results"] and res.nthreads == 4
+    assert f"S-tuples after filter: {g['rows']['1024'][0]}" in out
+    assert "TOTAL-TIME-USECS, TOTAL-TUPLES, NSEC-PER-TUPLE:" in out
+    assert "PARTITION-TIME-USECS, PROBE-TIME-USECS, JOIN-TIME-USECS:" in out
+    res = hw.PRO(R, S, 2)
+    assert res.totalresults == g["results"]
+
+
+def test_cli_end_to_end(hw):
+    g = GOLD["F3_grid"]
+    out = subprocess.run([hw.CLI_PATH, "-a", "PRO", "-r", str(g["r"]), "-s", str(g["s"]), "-q", "0.01",
+                          "-b", "blocked", "-m", str(g["m"]), "-k", "1", "-n", "2"],
+                         capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert f"S-tuples after filter: {g['rows']['1024'][0]}" in out.stdout
+    assert f"[INFO ] Results = {g['results']}. DONE." in out.stdout

@@ -1,0 +1,96 @@
+"""Summarise rocprofv3 outputs of bench.py into per-phase numbers (committed under profiles/).
+
+    python tools/prof_summary.py <trace_dir> <pmc_fetch_dir> <pmc_write_dir> <out.json> [config...]
+
+Kernel-trace: per-dispatch durations of the last join of the run. PMC: FETCH_SIZE and WRITE_SIZE
+(KiB per dispatch) from two separate --pmc passes; on gfx950 FETCH_SIZE reports half the bytes of
+wide coalesced reads (MI355X_MICROARCH.md, HBM), so hbm_bytes = (2*FETCH_SIZE + WRITE_SIZE)*1024.
+Infinity-Cache hits are included in these counters.
+"""
+import csv
+import glob
+import json
+import sys
+from collections import defaultdict
+
+# dispatch order of one join (hwbrj_engine.cpp Engine::run) -> phase
+PHASE_OF = {"k_build_global": "build", "k_build": "build", "k_probe_global": "probe",
+            "k_probe": "probe", "k_surv_totals": "surv", "k_scan_u64": "surv",
+            "k_surv_scatter": "surv", "k_join": "join", "k_plan": "index", "k_list_fill": "index"}
+
+
+def one(path_glob):
+    f = glob.glob(path_glob, recursive=True)
+    if not f:
+        raise SystemExit(f"missing {path_glob}")
+    return f[0]
+
+
+def last_join(names):
+    """Indices of the dispatches of the last join (from the last R scatter on)."""
+    sc = [i for i, n in enumerate(names) if n == "k_scatter"]
+    if len(sc) < 2:
+        return list(range(len(names)))
+    start = sc[-2]
+    return list(range(start, len(names)))
+
+
+def label(names, idx):
+    out, nsc = [], 0
+    for i in idx:
+        n = names[i]
+        if n == "k_scatter":
+            out.append("r_scatter" if nsc == 0 else "s_scatter")
+            nsc += 1
+        elif n in ("k_plan", "k_list_fill"):
+            out.append("r_index" if nsc <= 1 else "s_index")
+        else:
+            out.append(PHASE_OF.get(n, "other"))
+    return out
+
+
+def main():
+    tdir, fdir, wdir, out = sys.argv[1:5]
+    tr = list(csv.DictReader(open(one(f"{tdir}/**/*kernel_trace.csv"))))
+    tr.sort(key=lambda r: int(r["Start_Timestamp"]))
+    names = [r["Kernel_Name"] for r in tr]
+    idx = last_join(names)
+    labs = label(names, idx)
+    phases = defaultdict(lambda: {"ms": 0.0, "kernels": []})
+    for i, lab in zip(idx, labs):
+        r = tr[i]
+        ms = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
+        phases[lab]["ms"] += ms
+        phases[lab]["kernels"].append({"name": names[i], "ms": round(ms, 4)})
+
+    def counters(d, cname):
+        rows = list(csv.DictReader(open(one(f"{d}/**/*counter_collection.csv"))))
+        rows = [r for r in rows if r["Counter_Name"] == cname]
+        rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+        nm = [r["Kernel_Name"] for r in rows]
+        ix = last_join(nm)
+        return list(zip(label(nm, ix), (float(rows[i]["Counter_Value"]) for i in ix)))
+
+    fetch, write = defaultdict(float), defaultdict(float)
+    for lab, v in counters(fdir, "FETCH_SIZE"):
+        fetch[lab] += v
+    for lab, v in counters(wdir, "WRITE_SIZE"):
+        write[lab] += v
+    res = {"config_key": None, "phases": {}}
+    if len(sys.argv) > 5:
+        res["config_key"] = json.loads(sys.argv[5])
+    for lab, p in phases.items():
+        res["phases"][lab] = {
+            "ms": round(p["ms"], 4), "kernels": p["kernels"],
+            "fetch_kib": round(fetch.get(lab, 0.0), 1), "write_kib": round(write.get(lab, 0.0), 1),
+            "hbm_bytes": round((2 * fetch.get(lab, 0.0) + write.get(lab, 0.0)) * 1024),
+        }
+    json.dump(res, open(out, "w"), indent=1)
+    for lab, p in res["phases"].items():
+        gbs = p["hbm_bytes"] / (p["ms"] * 1e-3) / 1e9 if p["ms"] else 0
+        print(f"{lab:10s} {p['ms']:8.4f} ms  fetch {p['fetch_kib']/1e6:7.3f} GiB*  write "
+              f"{p['write_kib']/1e6:7.3f} GiB  -> {p['hbm_bytes']/1e9:7.3f} GB  {gbs:8.1f} GB/s")
+
+
+if __name__ == "__main__":
+    main()
