@@ -227,4 +227,13 @@ result_t* PRO(relation_t* relR, relation_t* relS, int nthreads) {
     return run_host_join(relR, relS, nthreads, nullptr);
 }
 
+result_t* hwbrj_BPRO(relation_t* relR, relation_t* relS, int nthreads,
+                     bloom_filter_args_t* bloom_filter_args) {
+    return run_host_join(relR, relS, nthreads, bloom_filter_args);
+}
+
+result_t* hwbrj_PRO(relation_t* relR, relation_t* relS, int nthreads) {
+    return run_host_join(relR, relS, nthreads, nullptr);
+}
+
 }  // extern "C"

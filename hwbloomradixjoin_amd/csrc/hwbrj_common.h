@@ -102,6 +102,20 @@ struct Geometry {
     uint32_t seg_bits;     // bits per LDS-resident slice segment (<= kSliceMaxBits)
     uint32_t seg_words;    // 32-bit words per stored segment (>= seg_bits/32, multiple of 4)
     uint32_t nseg;         // slice_bits / seg_bits
+    // derived constants (no per-element loops or divisions on the device)
+    uint32_t log2B;        // blocked family
+    uint32_t log2seg;      // log2(seg_bits)
+    uint32_t lbmask;       // (nblocks >> log2F) - 1: slice-local block index mask
+    uint32_t log2secw;     // sectorized: log2(min(B, 64))
+    uint32_t nsecmask;     // sectorized: B / secw - 1
+};
+
+// Consumer-kernel specializations (selected on the host from Geometry).
+enum Kind : int {
+    KIND_PASS        = 0,  // no filter test (PRO, or the global-bitmap fallback already filtered)
+    KIND_BLOCK_PK1   = 1,  // blocked/sectorized, k = 1, packed words
+    KIND_BLOCK       = 2,  // blocked/sectorized, code words, any k
+    KIND_BASIC_K1    = 3,  // basic, k = 1
 };
 
 constexpr uint32_t kMaxLog2F     = 10;

@@ -177,13 +177,21 @@ bool plan_geometry(const bloom_filter_args_t* a, uint64_t nR, Geometry* g, std::
             g->seg_words  = std::max<uint32_t>(4, g->seg_bits / 32);
         }
         if (g->mode == MODE_SLICE_BLOCK && k == 1 && ilog2u(B) <= g->log2F) g->format = FMT_PACKED;
+        if (g->mode == MODE_SLICE_BLOCK || g->mode == MODE_SLICE_BASIC) g->log2seg = ilog2u(g->seg_bits);
+        if (a->variant != BASIC) {
+            g->log2B    = ilog2u(B);
+            g->log2secw = std::min<uint32_t>(g->log2B, 6);
+            g->nsecmask = (uint32_t) (B >> g->log2secw) - 1u;
+            if (g->mode == MODE_SLICE_BLOCK) g->lbmask = (g->nblocks >> g->log2F) - 1u;
+        }
     }
     const uint64_t F    = 1ull << g->log2F;
     const uint64_t rper = (nR + F - 1) / F;
     uint32_t       l2s  = 0;
     while (l2s < 6 && (rper >> l2s) > 8192) l2s++;
-    g->log2NSUB   = l2s;
     g->sub_shift  = (g->mode == MODE_SLICE_BASIC) ? 0 : g->log2F;
+    if (g->sub_shift + l2s == 0) l2s = 1;  // k_join stores code >> hash_shift with an empty sentinel
+    g->log2NSUB   = l2s;
     g->hash_shift = g->sub_shift + g->log2NSUB;
     return true;
 }
@@ -251,13 +259,13 @@ int Engine::run(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     const uint32_t F = 1u << g.log2F, NSUB = 1u << g.log2NSUB, NJ = F * NSUB;
     const bool     slice_mode = g.mode == MODE_SLICE_BLOCK || g.mode == MODE_SLICE_BASIC;
     const uint32_t nseg       = slice_mode ? g.nseg : 1;
-    const uint32_t CH         = 1024;  // chunks per probe item
+    const uint32_t CH         = 1024;  // chunks per probe item (= one k_probe sweep)
     const size_t   sc_lds     = scatter_lds_bytes(g.log2F);
     const uint32_t G          = (uint32_t) cus_ * (uint32_t) std::max<size_t>(1, std::min<size_t>(2, 163840 / sc_lds));
     const uint64_t capR = region_cap(nR, G, F), capS = region_cap(nS, G, F);
     const uint64_t LR = (uint64_t) G * capR, LS = (uint64_t) G * capS;  // max chunks
     const uint64_t items_max = (LS / CH + F + 1) * nseg;
-    if (LS > 0xFFFFFFFFull || LR > 0xFFFFFFFFull) {
+    if (LS > 0xFFFFFFFFull || LR > 0xFFFFFFFFull || capS >= (1u << 22) || capR >= (1u << 22)) {
         set_last_error("relation too large for 32-bit chunk ids");
         return 3;
     }

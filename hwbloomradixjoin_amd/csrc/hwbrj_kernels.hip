@@ -17,6 +17,7 @@
 // Keys travel as 32-bit "codes" = crc32c(42, key): a bijection of the key, so code equality is key
 // equality and the code's low bits ARE the bloom block index.
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 
 #include "hwbrj_common.h"
 #include "hwbrj_kernels.h"
@@ -44,57 +45,47 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
     return v;
 }
 
-// Element word -> code (see Format in hwbrj_common.h).
-__device__ __forceinline__ uint32_t decode_code(uint32_t w, uint32_t q, const Geometry& g) {
-    if (g.format == FMT_PACKED) {
-        const uint32_t lowbits = 32u - g.log2F;  // log2F >= 3 for PACKED
-        return ((w & ((1u << lowbits) - 1u)) << g.log2F) | q;
-    }
-    return w;
-}
-
-// Where an element's filter bits live inside its partition slice.
+// Where an element's filter bits live inside its partition slice (KIND != KIND_PASS).
 struct Loc {
     uint32_t seg;   // slice segment
     uint32_t base;  // bit offset of the block (or the single bit, basic) inside the segment
     uint32_t h, y;  // enhanced double hashing state (block-relative)
 };
 
-__device__ __forceinline__ Loc locate(uint32_t w, uint32_t q, const Geometry& g,
-                                      const uint32_t* inv) {
+template <int KIND>
+__device__ __forceinline__ Loc locate(uint32_t w, const Geometry& g, const uint32_t* inv) {
     Loc L;
-    const uint32_t log2seg = ilog2u(g.seg_bits);
-    if (g.mode == MODE_SLICE_BASIC) {
+    if (KIND == KIND_BASIC_K1) {
         const uint32_t key = code_key(inv, w);
-        const uint32_t b   = mod_m(crapwow(kSeed, key), (uint32_t) g.m);  // add_basic k = 1
+        const uint32_t b   = mod_m(crapwow(kSeed, key), (uint32_t) g.m);  // add_basic, k = 1
         const uint32_t lb  = b >> g.log2F;
-        L.seg  = lb >> log2seg;
+        L.seg  = lb >> g.log2seg;
         L.base = lb & (g.seg_bits - 1u);
         L.h = L.y = 0;
         return L;
     }
     uint32_t lb;
-    if (g.format == FMT_PACKED) {
-        const uint32_t lowbits = 32u - g.log2F;
-        lb  = w & ((g.nblocks >> g.log2F) - 1u);
-        L.h = w >> lowbits;
+    if (KIND == KIND_BLOCK_PK1) {
+        lb  = w & g.lbmask;           // (code >> log2F) & (nblocks/F - 1)
+        L.h = w >> (32u - g.log2F);   // crapwow(key) & (B-1), stored by the scatter
         L.y = 0;
     } else {
         const uint32_t key = code_key(inv, w);
-        lb  = (w & (g.nblocks - 1u)) >> g.log2F;
+        lb  = (w >> g.log2F) & g.lbmask;
         L.h = crapwow(kSeed, key) & (g.B - 1u);
         L.y = (key + kSeed) & (g.B - 1u);
     }
-    const uint32_t sbit = lb * g.B;
-    L.seg  = sbit >> log2seg;
+    const uint32_t sbit = lb << g.log2B;
+    L.seg  = sbit >> g.log2seg;
     L.base = sbit & (g.seg_bits - 1u);
     return L;
 }
 
-template <bool SET>
+// SET: add the key's bits (ds_or); otherwise test them (src/bloom_filter.c:73-111 per variant).
+template <int KIND, bool SET>
 __device__ __forceinline__ bool apply_bits(const Loc& L, const Geometry& g, uint32_t* slice) {
-    if (g.mode == MODE_SLICE_BASIC) {
-        const uint32_t b = L.base;
+    if (KIND == KIND_BASIC_K1 || KIND == KIND_BLOCK_PK1) {
+        const uint32_t b = L.base + L.h;
         if (SET) {
             atomicOr(slice + (b >> 5), 1u << (b & 31u));
             return true;
@@ -103,10 +94,12 @@ __device__ __forceinline__ bool apply_bits(const Loc& L, const Geometry& g, uint
     }
     uint32_t       h    = L.h, y = L.y;
     const uint32_t mask = g.B - 1u;
-    const uint32_t secw = g.B < 64u ? g.B : 64u;
-    const uint32_t s0   = h / secw;
+    const uint32_t s0   = h >> g.log2secw;
+    const bool     sect = g.variant == VAR_SECTORIZED;
     for (uint32_t i = 0; i < g.k; i++) {
-        const uint32_t pos = (g.variant == VAR_SECTORIZED) ? sectorize(h, s0, i, g.B) : h;
+        // SECTORIZED: bit i lands in 64-bit sector (s0 + i) mod nsec (hwbrj_common.h sectorize)
+        const uint32_t pos = sect ? (((s0 + i) & g.nsecmask) << g.log2secw) | (h & ((1u << g.log2secw) - 1u))
+                                  : h;
         const uint32_t b   = L.base + pos;
         if (SET) {
             atomicOr(slice + (b >> 5), 1u << (b & 31u));
@@ -117,6 +110,12 @@ __device__ __forceinline__ bool apply_bits(const Loc& L, const Geometry& g, uint
         y = (y + i + 1u) & mask;
     }
     return true;
+}
+
+template <int KIND>
+__device__ __forceinline__ uint32_t decode_k(uint32_t w, uint32_t q, uint32_t log2F) {
+    if (KIND == KIND_BLOCK_PK1) return (w << log2F) | q;  // log2F >= 3: (w << log2F) drops the h bits
+    return w;
 }
 
 // ========================================================================= K0: generator
@@ -236,7 +235,9 @@ __global__ __launch_bounds__(1024) void k_probe_global(const uint2* S, uint64_t 
 // 32 elements is flushed as one 128-byte chunk into the workgroup's private chunk region (no
 // cross-workgroup coordination); a round that overfills a partition (skew) writes its extra whole
 // chunks directly. Chunk metadata = partition | count << 16.
-constexpr int kScThreads = 1024;
+constexpr int      kScThreads = 1024;
+constexpr uint32_t kCbBits    = 22;                       // ncb: chunk base | nchunks << 22
+constexpr uint32_t kCbMask    = (1u << kCbBits) - 1u;
 
 template <int SRC, int MODE, int FMT>
 __device__ __forceinline__ void sc_word(uint32_t x, const Geometry& g, const uint32_t* fwd,
@@ -261,13 +262,14 @@ __device__ __forceinline__ void sc_word(uint32_t x, const Geometry& g, const uin
     }
 }
 
-template <int SRC, int MODE, int FMT>
+template <int SRC, int MODE, int FMT, int kScE>
 __global__ __launch_bounds__(kScThreads) void k_scatter(ScatterParams P) {
+    constexpr uint32_t kScRound = kScThreads * kScE;  // elements per workgroup round
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const uint32_t F     = 1u << P.g.log2F;
     uint32_t*      stage = lds;            // F * 32
     uint32_t*      fill  = stage + F * 32; // F
-    uint32_t*      ncb   = fill + F;       // F: chunk base | nchunks << 24 (this round)
+    uint32_t*      ncb   = fill + F;       // F: chunk base | nchunks << kCbBits (this round)
     uint32_t*      tch   = ncb + F;        // F: chunks of q (this workgroup)
     uint32_t*      tel   = tch + F;        // F: elements of q (this workgroup)
     uint32_t*      flq   = tel + F;        // F: flush queue
@@ -296,60 +298,71 @@ __global__ __launch_bounds__(kScThreads) void k_scatter(ScatterParams P) {
     const uint64_t region = wg * P.cap;
     uint32_t* __restrict__ pool = P.pool;
 
-    // Raw round data is prefetched one round ahead so the loads overlap the barriers below.
-    uint4 pre0 = make_uint4(0, 0, 0, 0), pre1 = make_uint4(0, 0, 0, 0);
-    auto fetch = [&](uint64_t base, uint4& r0, uint4& r1) {
-        if (SRC == SRC_TUPLES) {
-            const uint2* src = (const uint2*) P.src;
-            const uint64_t i0 = base + 2 * tid, i1 = base + 2048 + 2 * tid;
-            if (i0 + 1 < e1) r0 = *(const uint4*) (src + i0);
-            else if (i0 < e1) r0 = make_uint4(src[i0].x, 0, 0, 0);
-            if (i1 + 1 < e1) r1 = *(const uint4*) (src + i1);
-            else if (i1 < e1) r1 = make_uint4(src[i1].x, 0, 0, 0);
-        } else {
-            const uint32_t* src = (const uint32_t*) P.src;
-            const uint64_t  i   = base + 4 * (uint64_t) tid;
-            if (i + 3 < e1) {
-                r0 = *(const uint4*) (src + i);
+    // Raw round data is prefetched one round ahead so the loads overlap the LDS phases below.
+    constexpr int NR = (SRC == SRC_TUPLES) ? kScE / 2 : kScE / 4;  // uint4 loads per round
+    constexpr uint32_t RSTRIDE = (SRC == SRC_TUPLES) ? 2 * kScThreads : 4 * kScThreads;
+    uint4 pre[NR];
+    auto fetch = [&](uint64_t base) {
+#pragma unroll
+        for (int h = 0; h < NR; h++) {
+            if (SRC == SRC_TUPLES) {
+                const uint2*   src = (const uint2*) P.src;
+                const uint64_t i   = base + (uint64_t) h * RSTRIDE + 2 * tid;
+                if (i + 1 < e1) pre[h] = *(const uint4*) (src + i);
+                else if (i < e1) pre[h] = make_uint4(src[i].x, 0, 0, 0);
             } else {
-                r0.x = i < e1 ? src[i] : 0u;
-                r0.y = i + 1 < e1 ? src[i + 1] : 0u;
-                r0.z = i + 2 < e1 ? src[i + 2] : 0u;
-                r0.w = 0u;
+                const uint32_t* src = (const uint32_t*) P.src;
+                const uint64_t  i   = base + (uint64_t) h * RSTRIDE + 4 * tid;
+                if (i + 3 < e1) {
+                    pre[h] = *(const uint4*) (src + i);
+                } else {
+                    pre[h].x = i < e1 ? src[i] : 0u;
+                    pre[h].y = i + 1 < e1 ? src[i + 1] : 0u;
+                    pre[h].z = i + 2 < e1 ? src[i + 2] : 0u;
+                    pre[h].w = 0u;
+                }
             }
         }
     };
-    if (e0 < e1) fetch(e0, pre0, pre1);
-    for (uint64_t base = e0; base < e1; base += 4096) {
-        uint32_t x[4];
-        bool     v[4];
-        if (SRC == SRC_TUPLES) {
-            const uint64_t i0 = base + 2 * tid, i1 = base + 2048 + 2 * tid;
-            x[0] = pre0.x; x[1] = pre0.z; x[2] = pre1.x; x[3] = pre1.z;
-            v[0] = i0 < e1; v[1] = i0 + 1 < e1; v[2] = i1 < e1; v[3] = i1 + 1 < e1;
-        } else {
-            const uint64_t i = base + 4 * (uint64_t) tid;
-            x[0] = pre0.x; x[1] = pre0.y; x[2] = pre0.z; x[3] = pre0.w;
+    if (e0 < e1) fetch(e0);
+    for (uint64_t base = e0; base < e1; base += kScRound) {
+        uint32_t x[kScE];
+        bool     v[kScE];
 #pragma unroll
-            for (int j = 0; j < 4; j++) v[j] = i + j < e1;
+        for (int h = 0; h < NR; h++) {
+            if (SRC == SRC_TUPLES) {
+                const uint64_t i = base + (uint64_t) h * RSTRIDE + 2 * tid;
+                x[2 * h]         = pre[h].x;
+                x[2 * h + 1]     = pre[h].z;
+                v[2 * h]         = i < e1;
+                v[2 * h + 1]     = i + 1 < e1;
+            } else {
+                const uint64_t i = base + (uint64_t) h * RSTRIDE + 4 * tid;
+                x[4 * h]         = pre[h].x;
+                x[4 * h + 1]     = pre[h].y;
+                x[4 * h + 2]     = pre[h].z;
+                x[4 * h + 3]     = pre[h].w;
+#pragma unroll
+                for (int j = 0; j < 4; j++) v[4 * h + j] = i + j < e1;
+            }
         }
-        if (base + 4096 < e1) fetch(base + 4096, pre0, pre1);
-        uint32_t wv[4], q[4], e[4];
+        if (base + kScRound < e1) fetch(base + kScRound);
+        uint32_t wv[kScE], q[kScE], e[kScE];
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
+        for (int j = 0; j < kScE; j++) {
             sc_word<SRC, MODE, FMT>(x[j], P.g, fwd, wv[j], q[j]);
             e[j] = v[j] ? atomicAdd(&fill[q[j]], 1u) : 0u;
         }
         __syncthreads();
 #pragma unroll
-        for (int j = 0; j < 4; j++)
+        for (int j = 0; j < kScE; j++)
             if (v[j] && e[j] < 32) stage[q[j] * 32 + e[j]] = wv[j];
         for (uint32_t qq = tid; qq < F; qq += kScThreads) {
             const uint32_t f = fill[qq];
             if (f >= 32) {
                 const uint32_t c  = f >> 5;
                 const uint32_t cb = atomicAdd(&misc[1], c);
-                ncb[qq]           = cb | (c << 24);
+                ncb[qq]           = cb | (c << kCbBits);
                 tch[qq] += c;
                 tel[qq] += c * 32;
                 fill[qq]          = f & 31u;
@@ -363,17 +376,17 @@ __global__ __launch_bounds__(kScThreads) void k_scatter(ScatterParams P) {
             const uint32_t qq = flq[i];
             const uint32_t l8 = tid & 7;
             const uint4    vv = *(const uint4*) &stage[qq * 32 + l8 * 4];
-            *(uint4*) &pool[(region + (ncb[qq] & 0xFFFFFFu)) * 32 + l8 * 4] = vv;
+            *(uint4*) &pool[(region + (ncb[qq] & kCbMask)) * 32 + l8 * 4] = vv;
         }
         __syncthreads();
         if (tid == 0) misc[0] = 0;
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
+        for (int j = 0; j < kScE; j++) {
             if (v[j] && e[j] >= 32) {
                 const uint32_t qq = q[j], ch = e[j] >> 5, s = e[j] & 31u;
                 const uint32_t cb = ncb[qq];
-                if (ch < (cb >> 24))
-                    pool[(region + (cb & 0xFFFFFFu) + ch) * 32 + s] = wv[j];
+                if (ch < (cb >> kCbBits))
+                    pool[(region + (cb & kCbMask) + ch) * 32 + s] = wv[j];
                 else
                     stage[qq * 32 + s] = wv[j];
             }
@@ -500,28 +513,60 @@ __global__ __launch_bounds__(1024) void k_scan_u64(const uint64_t* in, uint64_t*
     if (t == 1023) out[n] = part[1023];
 }
 
-// ======================================================== chunk-walking helper (8 lanes)
-// Threads cooperate 8 per chunk: lane8 loads 4 words (16 B). Returns the number of valid words.
-__device__ __forceinline__ uint32_t load_chunk_quad(const uint32_t* pool, const uint32_t* meta,
-                                                    uint32_t cid, uint32_t l8, uint32_t (&w)[4]) {
-    const uint32_t cnt = meta[cid] >> 16;
-    const uint4    v   = *(const uint4*) &pool[(uint64_t) cid * 32 + l8 * 4];
-    w[0] = v.x;
-    w[1] = v.y;
-    w[2] = v.z;
-    w[3] = v.w;
-    const uint32_t first = l8 * 4;
-    return cnt > first ? min(cnt - first, 4u) : 0u;
+// ======================================================== chunk-walking helpers (8 lanes)
+// A sweep covers kSweep = 128 * kPQ chunks of a chunk list: 8 threads share a chunk (16 B each) and
+// every thread issues kPQ independent list loads, then kPQ independent meta + chunk loads, so a
+// workgroup keeps kPQ * 16 KiB in flight per round trip instead of one dependent load chain.
+constexpr int      kPQ    = 8;
+constexpr uint32_t kSweep = 128u * kPQ;
+
+struct Sweep {
+    uint4    v[kPQ];
+    uint32_t n[kPQ];  // valid words of this thread's quad (0..4)
+};
+
+__device__ __forceinline__ void load_sweep(const uint32_t* __restrict__ list,
+                                           const uint32_t* __restrict__ pool,
+                                           const uint32_t* __restrict__ meta, uint32_t lb,
+                                           uint32_t le, Sweep& S) {
+    const uint32_t l8 = threadIdx.x & 7, cslot = threadIdx.x >> 3;
+    uint32_t       cid[kPQ];
+#pragma unroll
+    for (int j = 0; j < kPQ; j++) {
+        const uint32_t l = lb + cslot + (uint32_t) j * 128u;
+        cid[j]           = l < le ? list[l] : 0xFFFFFFFFu;
+    }
+    uint32_t cnt[kPQ];
+#pragma unroll
+    for (int j = 0; j < kPQ; j++) {
+        if (cid[j] != 0xFFFFFFFFu) {
+            cnt[j]  = meta[cid[j]] >> 16;
+            S.v[j]  = *(const uint4*) &pool[(uint64_t) cid[j] * 32 + l8 * 4];
+        } else {
+            cnt[j] = 0;
+            S.v[j] = make_uint4(0, 0, 0, 0);
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < kPQ; j++) {
+        const uint32_t first = l8 * 4;
+        S.n[j]               = cnt[j] > first ? min(cnt[j] - first, 4u) : 0u;
+    }
+}
+
+__device__ __forceinline__ uint32_t sweep_word(const Sweep& S, int j, int t) {
+    return t == 0 ? S.v[j].x : t == 1 ? S.v[j].y : t == 2 ? S.v[j].z : S.v[j].w;
 }
 
 // ======================================================================== K6: R build
 // One workgroup per partition q. Filter bits of R go into an LDS slice segment (ds_or), the slice
 // is written once (coalesced); then R codes are written grouped by sub-partition.
+template <int KIND>
 __global__ __launch_bounds__(1024) void k_build(BuildParams P) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const Geometry& g      = P.g;
     const uint32_t  NSUB   = 1u << g.log2NSUB;
-    const bool      slices = g.mode == MODE_SLICE_BLOCK || g.mode == MODE_SLICE_BASIC;
+    constexpr bool  slices = KIND != KIND_PASS;
     const uint32_t  segw   = slices ? g.seg_words : 0;  // multiple of 4
     uint32_t*       slice  = lds;
     uint32_t*       inv    = slice + segw;
@@ -531,23 +576,28 @@ __global__ __launch_bounds__(1024) void k_build(BuildParams P) {
     load_tab(inv, &P.tabs->inv[0][0]);
     for (uint32_t i = threadIdx.x; i < NSUB; i += blockDim.x) subh[i] = 0;
     const uint32_t l0 = P.list_start[q], l1 = P.list_start[q + 1];
-    const uint32_t l8 = threadIdx.x & 7, cslot = threadIdx.x >> 3;  // 128 chunks per sweep
     const uint32_t nseg = slices ? g.nseg : 1;
     for (uint32_t seg = 0; seg < nseg; seg++) {
         for (uint32_t i = threadIdx.x; i < segw; i += blockDim.x) slice[i] = 0;
         __syncthreads();
         const bool last = seg + 1 == nseg;
-        for (uint32_t l = l0 + cslot; l < l1; l += 128) {
-            uint32_t       w[4];
-            const uint32_t nv = load_chunk_quad(P.pool, P.meta, P.list[l], l8, w);
-            for (uint32_t j = 0; j < nv; j++) {
-                if (slices) {
-                    const Loc L = locate(w[j], q, g, inv);
-                    if (L.seg == seg) apply_bits<true>(L, g, slice);
-                }
-                if (last) {
-                    const uint32_t c = decode_code(w[j], q, g);
-                    atomicAdd(&subh[(c >> g.sub_shift) & (NSUB - 1u)], 1u);
+        for (uint32_t lb = l0; lb < l1; lb += kSweep) {
+            Sweep S;
+            load_sweep(P.list, P.pool, P.meta, lb, l1, S);
+#pragma unroll
+            for (int j = 0; j < kPQ; j++) {
+#pragma unroll
+                for (int t = 0; t < 4; t++) {
+                    if ((uint32_t) t >= S.n[j]) continue;
+                    const uint32_t w = sweep_word(S, j, t);
+                    if (slices) {
+                        const Loc L = locate<KIND>(w, g, inv);
+                        if (L.seg == seg) apply_bits<KIND, true>(L, g, slice);
+                    }
+                    if (last) {
+                        const uint32_t c = decode_k<KIND>(w, q, g.log2F);
+                        atomicAdd(&subh[(c >> g.sub_shift) & (NSUB - 1u)], 1u);
+                    }
                 }
             }
         }
@@ -569,14 +619,19 @@ __global__ __launch_bounds__(1024) void k_build(BuildParams P) {
         if (q == gridDim.x - 1) P.qs_off[(uint64_t) gridDim.x * NSUB] = run;
     }
     __syncthreads();
-    for (uint32_t l = l0 + cslot; l < l1; l += 128) {
-        uint32_t       w[4];
-        const uint32_t nv = load_chunk_quad(P.pool, P.meta, P.list[l], l8, w);
-        for (uint32_t j = 0; j < nv; j++) {
-            const uint32_t c   = decode_code(w[j], q, g);
-            const uint32_t s   = (c >> g.sub_shift) & (NSUB - 1u);
-            const uint64_t pos = atomicAdd((unsigned long long*) &subc[s], 1ull);
-            P.out_codes[pos]   = c;
+    for (uint32_t lb = l0; lb < l1; lb += kSweep) {
+        Sweep S;
+        load_sweep(P.list, P.pool, P.meta, lb, l1, S);
+#pragma unroll
+        for (int j = 0; j < kPQ; j++) {
+#pragma unroll
+            for (int t = 0; t < 4; t++) {
+                if ((uint32_t) t >= S.n[j]) continue;
+                const uint32_t c   = decode_k<KIND>(sweep_word(S, j, t), q, g.log2F);
+                const uint32_t s   = (c >> g.sub_shift) & (NSUB - 1u);
+                const uint64_t pos = atomicAdd((unsigned long long*) &subc[s], 1ull);
+                P.out_codes[pos]   = c;
+            }
         }
     }
 }
@@ -593,75 +648,88 @@ __device__ __forceinline__ uint32_t find_q(const uint32_t* item_start, uint32_t 
     return lo;
 }
 
+template <int KIND>
 __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const Geometry& g      = P.g;
     const uint32_t  F      = 1u << g.log2F;
     const uint32_t  NSUB   = 1u << g.log2NSUB;
-    const bool      slices = g.mode == MODE_SLICE_BLOCK || g.mode == MODE_SLICE_BASIC;
+    constexpr bool  slices = KIND != KIND_PASS;
     const uint32_t  segw   = slices ? g.seg_words : 0;  // multiple of 4
     uint32_t*       slice  = lds;
     uint32_t*       inv    = slice + segw;
     uint32_t*       subc   = inv + 128;  // NSUB
-    uint32_t*       misc   = subc + 64;  // [0] survivor cursor, [1] loaded (q,seg) tag
+    uint32_t*       misc   = subc + 64;  // [0] survivor cursor
     load_tab(inv, &P.tabs->inv[0][0]);
     for (uint32_t i = threadIdx.x; i < NSUB; i += blockDim.x) subc[i] = 0;
-    if (threadIdx.x == 0) {
-        misc[0] = 0;
-        misc[1] = 0xFFFFFFFFu;
-    }
+    if (threadIdx.x == 0) misc[0] = 0;
     __syncthreads();
     const uint32_t I   = P.item_start[F];
     const uint32_t it0 = (uint32_t) ((uint64_t) blockIdx.x * I / gridDim.x);
     const uint32_t it1 = (uint32_t) ((uint64_t) (blockIdx.x + 1) * I / gridDim.x);
     const uint32_t nseg = slices ? g.nseg : 1;
-    const uint32_t l8 = threadIdx.x & 7, cslot = threadIdx.x >> 3;
     const int      lane = threadIdx.x & 63;
+    if (it0 >= it1) return;
+    // walk partitions sequentially from the first item's (one binary search per workgroup)
+    uint32_t q      = find_q(P.item_start, F, it0);
+    uint32_t q_it0  = P.item_start[q], q_it1 = P.item_start[q + 1];
+    uint32_t lq0    = P.list_start[q], lq1 = P.list_start[q + 1];
+    uint32_t loaded = 0xFFFFFFFFu;
     for (uint32_t it = it0; it < it1; it++) {
-        const uint32_t q     = find_q(P.item_start, F, it);
-        const uint32_t local = it - P.item_start[q];
+        while (it >= q_it1) {  // uniform
+            q++;
+            q_it0 = q_it1;
+            q_it1 = P.item_start[q + 1];
+            lq0   = lq1;
+            lq1   = P.list_start[q + 1];
+        }
+        const uint32_t local = it - q_it0;
         const uint32_t seg   = local % nseg;
         const uint32_t piece = local / nseg;
-        const uint32_t lq0 = P.list_start[q], lq1 = P.list_start[q + 1];
-        const uint32_t lb  = lq0 + piece * P.CH;
-        const uint32_t le  = min(lq1, lb + P.CH);
+        const uint32_t lb    = lq0 + piece * P.CH;
+        const uint32_t le    = min(lq1, lb + P.CH);
         if (slices) {
             const uint32_t tag = q * nseg + seg;
-            if (misc[1] != tag) {  // uniform: every thread reads the same LDS word
+            if (loaded != tag) {
                 const uint4* src = (const uint4*) (P.slices + (uint64_t) tag * segw);
                 uint4*       dst = (uint4*) slice;
                 for (uint32_t i = threadIdx.x; i < segw / 4; i += blockDim.x) dst[i] = src[i];
+                loaded = tag;
                 __syncthreads();
-                if (threadIdx.x == 0) misc[1] = tag;
             }
         }
-        __syncthreads();
         uint32_t* __restrict__ out = P.surv + (uint64_t) seg * P.surv_seg_stride + (uint64_t) lb * 32;
-        for (uint32_t l0 = lb; l0 < le; l0 += 128) {
-            const uint32_t l  = l0 + cslot;
-            uint32_t       w[4];
-            uint32_t       nv = 0;
-            if (l < le) nv = load_chunk_quad(P.pool, P.meta, P.list[l], l8, w);
-            uint32_t keep[4];
-            uint32_t ns = 0;
-            for (uint32_t j = 0; j < nv; j++) {
-                bool pass = true;
-                if (slices) {
-                    const Loc L = locate(w[j], q, g, inv);
-                    pass = (L.seg == seg) && apply_bits<false>(L, g, slice);
+        for (uint32_t l0 = lb; l0 < le; l0 += kSweep) {
+            Sweep S;
+            load_sweep(P.list, P.pool, P.meta, l0, le, S);
+#pragma unroll
+            for (int j = 0; j < kPQ; j++) {
+                uint32_t cw[4];
+                uint32_t pm = 0;  // pass mask of this thread's (up to) 4 words
+#pragma unroll
+                for (int t = 0; t < 4; t++) {
+                    const uint32_t w    = sweep_word(S, j, t);
+                    bool           pass = (uint32_t) t < S.n[j];
+                    if (slices && pass) {
+                        const Loc L = locate<KIND>(w, g, inv);
+                        pass        = (nseg == 1 || L.seg == seg) && apply_bits<KIND, false>(L, g, slice);
+                    }
+                    cw[t] = decode_k<KIND>(w, q, g.log2F);
+                    if (pass) {
+                        pm |= 1u << t;
+                        atomicAdd(&subc[(cw[t] >> g.sub_shift) & (NSUB - 1u)], 1u);
+                    }
                 }
-                if (pass) {
-                    const uint32_t c = decode_code(w[j], q, g);
-                    keep[ns++]       = c;
-                    atomicAdd(&subc[(c >> g.sub_shift) & (NSUB - 1u)], 1u);
-                }
+                const uint32_t ns   = __popc(pm);
+                const uint32_t incl = wave_incl_scan(ns);
+                uint32_t       wb   = 0;
+                if (lane == 63 && incl) wb = atomicAdd(&misc[0], incl);
+                wb = __shfl(wb, 63, 64);
+                const uint32_t o = wb + incl - ns;
+#pragma unroll
+                for (int t = 0; t < 4; t++)
+                    if (pm & (1u << t)) out[o + __popc(pm & ((1u << t) - 1u))] = cw[t];
             }
-            const uint32_t incl = wave_incl_scan(ns);
-            uint32_t       wb   = 0;
-            if (lane == 63 && incl) wb = atomicAdd(&misc[0], incl);
-            wb = __shfl(wb, 63, 64);
-            const uint32_t o = wb + incl - ns;
-            for (uint32_t j = 0; j < ns; j++) out[o + j] = keep[j];
         }
         __syncthreads();
         for (uint32_t s = threadIdx.x; s < NSUB; s += blockDim.x) {
@@ -708,11 +776,20 @@ __global__ __launch_bounds__(256) void k_surv_scatter(SurvParams P) {
             cur[s] = P.qs_off[(uint64_t) q * NSUB + s] + P.item_off[(uint64_t) it * NSUB + s];
         __syncthreads();
         const uint32_t* src = P.surv + (uint64_t) seg * P.surv_seg_stride + (uint64_t) lb * 32;
-        for (uint32_t i = threadIdx.x; i < total; i += blockDim.x) {
-            const uint32_t c   = src[i];
-            const uint32_t s   = (c >> P.sub_shift) & (NSUB - 1u);
-            const uint64_t pos = atomicAdd((unsigned long long*) &cur[s], 1ull);
-            P.out[pos]         = c;
+        for (uint32_t i0 = threadIdx.x; i0 < total; i0 += blockDim.x * 8) {
+            uint32_t c[8];
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                const uint32_t i = i0 + j * blockDim.x;
+                c[j]             = i < total ? src[i] : 0u;
+            }
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                if (i0 + j * blockDim.x >= total) continue;
+                const uint32_t s   = (c[j] >> P.sub_shift) & (NSUB - 1u);
+                const uint64_t pos = atomicAdd((unsigned long long*) &cur[s], 1ull);
+                P.out[pos]         = c[j];
+            }
         }
     }
 }
@@ -724,44 +801,60 @@ __global__ __launch_bounds__(256) void k_surv_scatter(SurvParams P) {
 constexpr uint32_t kJoinLog2T  = 14;
 constexpr uint32_t kJoinT      = 1u << kJoinLog2T;
 constexpr uint32_t kJoinPiece  = kJoinT / 2;
+constexpr int      kJoinB      = 16;           // independent loads per thread per batch
+constexpr uint32_t kEmpty      = 0xFFFFFFFFu;  // codes of one job share their low hash_shift >= 1
+                                               // bits, so (code >> hash_shift) never equals it
 
-__device__ __forceinline__ uint32_t join_slot(uint32_t c, uint32_t shift) {
-    return ((c >> shift) * 0x9E3779B1u) >> (32 - kJoinLog2T);
+__device__ __forceinline__ uint32_t join_slot(uint32_t v) {
+    return (v * 0x9E3779B1u) >> (32 - kJoinLog2T);
 }
 
 __global__ __launch_bounds__(512) void k_join(JoinParams P) {
     __shared__ uint32_t keys[kJoinT];
-    __shared__ uint32_t occ[kJoinT / 32];
     __shared__ uint64_t wsum[8];
     const uint32_t job = blockIdx.x;
     const uint64_t r0 = P.r_off[job], r1 = P.r_off[job + 1];
     const uint64_t s0 = P.s_off[job], s1 = P.s_off[job + 1];
     if (r1 == r0 || s1 == s0) return;
-    uint64_t cnt = 0;
+    const uint32_t sh  = P.hash_shift;
+    uint64_t       cnt = 0;
     for (uint64_t rb = r0; rb < r1; rb += kJoinPiece) {
         const uint64_t re = min(r1, rb + kJoinPiece);
-        for (uint32_t i = threadIdx.x; i < kJoinT / 32; i += blockDim.x) occ[i] = 0;
+        for (uint32_t i = threadIdx.x; i < kJoinT / 4; i += blockDim.x)
+            ((uint4*) keys)[i] = make_uint4(kEmpty, kEmpty, kEmpty, kEmpty);
         __syncthreads();
-        for (uint64_t i = rb + threadIdx.x; i < re; i += blockDim.x) {
-            const uint32_t c = P.r_codes[i];
-            uint32_t       h = join_slot(c, P.hash_shift);
-            while (true) {
-                const uint32_t bit = 1u << (h & 31u);
-                const uint32_t old = atomicOr(&occ[h >> 5], bit);
-                if (!(old & bit)) {
-                    keys[h] = c;
-                    break;
-                }
-                h = (h + 1u) & (kJoinT - 1u);
+        for (uint64_t i0 = rb + threadIdx.x; i0 < re; i0 += (uint64_t) blockDim.x * kJoinB) {
+            uint32_t c[kJoinB];
+#pragma unroll
+            for (int j = 0; j < kJoinB; j++) {
+                const uint64_t i = i0 + (uint64_t) j * blockDim.x;
+                c[j]             = i < re ? P.r_codes[i] : 0u;
+            }
+#pragma unroll
+            for (int j = 0; j < kJoinB; j++) {
+                if (i0 + (uint64_t) j * blockDim.x >= re) continue;
+                const uint32_t v = c[j] >> sh;
+                uint32_t       h = join_slot(v);
+                while (atomicCAS(&keys[h], kEmpty, v) != kEmpty) h = (h + 1u) & (kJoinT - 1u);
             }
         }
         __syncthreads();
-        for (uint64_t i = s0 + threadIdx.x; i < s1; i += blockDim.x) {
-            const uint32_t c = P.s_codes[i];
-            uint32_t       h = join_slot(c, P.hash_shift);
-            while ((occ[h >> 5] >> (h & 31u)) & 1u) {
-                cnt += keys[h] == c;
-                h = (h + 1u) & (kJoinT - 1u);
+        for (uint64_t i0 = s0 + threadIdx.x; i0 < s1; i0 += (uint64_t) blockDim.x * kJoinB) {
+            uint32_t c[kJoinB];
+#pragma unroll
+            for (int j = 0; j < kJoinB; j++) {
+                const uint64_t i = i0 + (uint64_t) j * blockDim.x;
+                c[j]             = i < s1 ? P.s_codes[i] : 0u;
+            }
+#pragma unroll
+            for (int j = 0; j < kJoinB; j++) {
+                if (i0 + (uint64_t) j * blockDim.x >= s1) continue;
+                const uint32_t v = c[j] >> sh;
+                uint32_t       h = join_slot(v);
+                for (uint32_t k = keys[h]; k != kEmpty; k = keys[h]) {
+                    cnt += k == v;
+                    h = (h + 1u) & (kJoinT - 1u);
+                }
             }
         }
         __syncthreads();
@@ -824,12 +917,23 @@ size_t scatter_lds_bytes(uint32_t log2F) {
     return (F * 32 + F * 5 + 128 + 4) * sizeof(uint32_t);
 }
 
+static int scatter_elems() {  // dev knob for A/B runs: HWBRJ_SCE=4|8 elements per thread/round
+    const char* v = getenv("HWBRJ_SCE");
+    return (v && atoi(v) == 8) ? 8 : 4;
+}
+
 template <int SRC, int MODE, int FMT>
 static void scatter_inst(const ScatterParams& p, uint32_t grid, hipStream_t st) {
     const size_t lds = scatter_lds_bytes(p.g.log2F);
-    (void) hipFuncSetAttribute((const void*) &k_scatter<SRC, MODE, FMT>,
-                               hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds);
-    k_scatter<SRC, MODE, FMT><<<grid, kScThreads, lds, st>>>(p);
+    if (scatter_elems() == 8) {
+        (void) hipFuncSetAttribute((const void*) &k_scatter<SRC, MODE, FMT, 8>,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds);
+        k_scatter<SRC, MODE, FMT, 8><<<grid, kScThreads, lds, st>>>(p);
+    } else {
+        (void) hipFuncSetAttribute((const void*) &k_scatter<SRC, MODE, FMT, 4>,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds);
+        k_scatter<SRC, MODE, FMT, 4><<<grid, kScThreads, lds, st>>>(p);
+    }
 }
 
 void launch_scatter(const ScatterParams& p, int src, uint32_t grid, hipStream_t st) {
@@ -868,16 +972,42 @@ size_t slice_lds_bytes(const Geometry& g) {
     return ((slices ? g.seg_words : 0) + 128 + 64 + 2 * 64 + 4) * sizeof(uint32_t);
 }
 
+int consumer_kind(const Geometry& g) {
+    if (g.mode == MODE_SLICE_BASIC) return KIND_BASIC_K1;
+    if (g.mode == MODE_SLICE_BLOCK) return g.format == FMT_PACKED ? KIND_BLOCK_PK1 : KIND_BLOCK;
+    return KIND_PASS;
+}
+
+template <int KIND>
+static void build_inst(const BuildParams& p, uint32_t F, size_t lds, hipStream_t st) {
+    (void) hipFuncSetAttribute((const void*) &k_build<KIND>, hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds);
+    k_build<KIND><<<F, 1024, lds, st>>>(p);
+}
+
+template <int KIND>
+static void probe_inst(const ProbeParams& p, uint32_t grid, size_t lds, hipStream_t st) {
+    (void) hipFuncSetAttribute((const void*) &k_probe<KIND>, hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds);
+    k_probe<KIND><<<grid, 1024, lds, st>>>(p);
+}
+
 void launch_build(const BuildParams& p, uint32_t F, hipStream_t st) {
     const size_t lds = slice_lds_bytes(p.g);
-    (void) hipFuncSetAttribute((const void*) &k_build, hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds);
-    k_build<<<F, 1024, lds, st>>>(p);
+    switch (consumer_kind(p.g)) {
+        case KIND_BLOCK_PK1: return build_inst<KIND_BLOCK_PK1>(p, F, lds, st);
+        case KIND_BLOCK: return build_inst<KIND_BLOCK>(p, F, lds, st);
+        case KIND_BASIC_K1: return build_inst<KIND_BASIC_K1>(p, F, lds, st);
+        default: return build_inst<KIND_PASS>(p, F, lds, st);
+    }
 }
 
 void launch_probe(const ProbeParams& p, uint32_t grid, hipStream_t st) {
     const size_t lds = slice_lds_bytes(p.g);
-    (void) hipFuncSetAttribute((const void*) &k_probe, hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds);
-    k_probe<<<grid, 1024, lds, st>>>(p);
+    switch (consumer_kind(p.g)) {
+        case KIND_BLOCK_PK1: return probe_inst<KIND_BLOCK_PK1>(p, grid, lds, st);
+        case KIND_BLOCK: return probe_inst<KIND_BLOCK>(p, grid, lds, st);
+        case KIND_BASIC_K1: return probe_inst<KIND_BASIC_K1>(p, grid, lds, st);
+        default: return probe_inst<KIND_PASS>(p, grid, lds, st);
+    }
 }
 
 void launch_surv_totals(const uint32_t* item_start, const uint32_t* surv_cnt, uint32_t log2F,

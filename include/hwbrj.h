@@ -69,6 +69,11 @@ result_t * BPRO(relation_t * relR, relation_t * relS, int nthreads,
                 bloom_filter_args_t * bloom_filter_args);
 result_t * PRO(relation_t * relR, relation_t * relS, int nthreads);
 void       assert_args(bloom_filter_args_t * args);
+/* The same two operators under prefixed names, for linking next to the reference's own
+ * parallel_radix_join*.o (which also define BPRO/PRO): see INTEGRATION.md. */
+result_t * hwbrj_BPRO(relation_t * relR, relation_t * relS, int nthreads,
+                      bloom_filter_args_t * bloom_filter_args);
+result_t * hwbrj_PRO(relation_t * relR, relation_t * relS, int nthreads);
 
 /* ---- device-resident entry points (this build) ---- */
 typedef struct hwbrj_stats_t {

@@ -35,6 +35,8 @@ dS = torch.empty((nS, 2), dtype=torch.int32, device="cuda")
 hw.generate_device(dR, 2, nR, nR, 1.0, 12345)
 hw.generate_device(dS, 2, 2**31 - 1, nR, 0.01, 54321)
 args = hw.BloomFilterArgs(hw.BLOCKED, 2**30, 1, 1024)
-for i in range(3):
+for i in range(6):
+    os.environ["HWBRJ_SCE"] = "8" if i % 2 else "4"
     st = hw.join_device(dR, dS, args)
+    print("SCE", os.environ["HWBRJ_SCE"], end=" ")
     print(f"NS run {i}: filtered={st.filtered} (want 124236515) matches={st.matches} (want 10240000) total={st.ms_total:.3f} ms | r_sc {st.ms_r_scatter:.3f} r_ix {st.ms_r_index:.3f} build {st.ms_build:.3f} s_sc {st.ms_s_scatter:.3f} s_ix {st.ms_s_index:.3f} probe {st.ms_probe:.3f} surv {st.ms_surv:.3f} join {st.ms_join:.3f}", flush=True)
