@@ -24,6 +24,7 @@ struct ScatterParams {
     uint64_t         cap;          // chunk capacity of one workgroup region
     Geometry         g;
     const CrcTables* tabs;
+    uint32_t         ablate;       // dev-only timing ablation (HWBRJ_SC_ABLATE); results invalid if != 0
 };
 
 struct BuildParams {

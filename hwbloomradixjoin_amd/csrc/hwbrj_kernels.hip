@@ -265,16 +265,18 @@ __device__ __forceinline__ void sc_word(uint32_t x, const Geometry& g, const uin
 template <int SRC, int MODE, int FMT, int kScE>
 __global__ __launch_bounds__(kScThreads) void k_scatter(ScatterParams P) {
     constexpr uint32_t kScRound = kScThreads * kScE;  // elements per workgroup round
+    constexpr uint32_t kNone    = 0xFFFFFFFFu;        // no pending word
+    constexpr uint32_t kDirect  = 0x80000000u;        // pending word goes to the pool, not the stage
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const uint32_t F     = 1u << P.g.log2F;
     uint32_t*      stage = lds;            // F * 32
-    uint32_t*      fill  = stage + F * 32; // F
+    uint32_t*      fill  = stage + F * 32; // F: words in the stage (incl. pending ones)
     uint32_t*      ncb   = fill + F;       // F: chunk base | nchunks << kCbBits (this round)
     uint32_t*      tch   = ncb + F;        // F: chunks of q (this workgroup)
     uint32_t*      tel   = tch + F;        // F: elements of q (this workgroup)
     uint32_t*      flq   = tel + F;        // F: flush queue
     uint32_t*      fwd   = flq + F;        // 128
-    uint32_t*      misc  = fwd + 128;      // [0] nflush, [1] chunks used
+    uint32_t*      misc  = fwd + 128;      // [0],[1] flush counts by round parity, [2] chunks used
 
     const int tid = threadIdx.x;
     for (uint32_t i = tid; i < F; i += kScThreads) {
@@ -283,10 +285,7 @@ __global__ __launch_bounds__(kScThreads) void k_scatter(ScatterParams P) {
         tel[i]  = 0;
     }
     load_tab(fwd, &P.tabs->fwd[0][0]);
-    if (tid == 0) {
-        misc[0] = 0;
-        misc[1] = 0;
-    }
+    if (tid < 4) misc[tid] = 0;
     __syncthreads();
 
     const uint64_t n     = P.n_dev ? *P.n_dev : P.n;
@@ -295,116 +294,171 @@ __global__ __launch_bounds__(kScThreads) void k_scatter(ScatterParams P) {
     const uint64_t e0    = 4 * (wg * units / G);
     const uint64_t e1r   = 4 * ((wg + 1) * units / G);
     const uint64_t e1    = e1r < n ? e1r : n;
-    const uint64_t region = wg * P.cap;
-    uint32_t* __restrict__ pool = P.pool;
+    const uint32_t len   = e1 > e0 ? (uint32_t) (e1 - e0) : 0u;  // < 2^32 per workgroup
+    uint32_t* __restrict__ pool = P.pool + wg * P.cap * 32;
+    uint32_t* __restrict__ meta = P.meta + wg * P.cap;
 
     // Raw round data is prefetched one round ahead so the loads overlap the LDS phases below.
-    constexpr int NR = (SRC == SRC_TUPLES) ? kScE / 2 : kScE / 4;  // uint4 loads per round
+    constexpr int      NR      = (SRC == SRC_TUPLES) ? kScE / 2 : kScE / 4;  // uint4 per round
     constexpr uint32_t RSTRIDE = (SRC == SRC_TUPLES) ? 2 * kScThreads : 4 * kScThreads;
+    const uint2*    tsrc = (const uint2*) P.src + e0;
+    const uint32_t* csrc = (const uint32_t*) P.src + e0;
     uint4 pre[NR];
-    auto fetch = [&](uint64_t base) {
+    auto fetch = [&](uint32_t base) {
 #pragma unroll
         for (int h = 0; h < NR; h++) {
             if (SRC == SRC_TUPLES) {
-                const uint2*   src = (const uint2*) P.src;
-                const uint64_t i   = base + (uint64_t) h * RSTRIDE + 2 * tid;
-                if (i + 1 < e1) pre[h] = *(const uint4*) (src + i);
-                else if (i < e1) pre[h] = make_uint4(src[i].x, 0, 0, 0);
+                const uint32_t i = base + (uint32_t) h * RSTRIDE + 2 * tid;
+                if (i + 1 < len) pre[h] = *(const uint4*) (tsrc + i);
+                else if (i < len) pre[h] = make_uint4(tsrc[i].x, 0, 0, 0);
             } else {
-                const uint32_t* src = (const uint32_t*) P.src;
-                const uint64_t  i   = base + (uint64_t) h * RSTRIDE + 4 * tid;
-                if (i + 3 < e1) {
-                    pre[h] = *(const uint4*) (src + i);
+                const uint32_t i = base + (uint32_t) h * RSTRIDE + 4 * tid;
+                if (i + 3 < len) {
+                    pre[h] = *(const uint4*) (csrc + i);
                 } else {
-                    pre[h].x = i < e1 ? src[i] : 0u;
-                    pre[h].y = i + 1 < e1 ? src[i + 1] : 0u;
-                    pre[h].z = i + 2 < e1 ? src[i + 2] : 0u;
+                    pre[h].x = i < len ? csrc[i] : 0u;
+                    pre[h].y = i + 1 < len ? csrc[i + 1] : 0u;
+                    pre[h].z = i + 2 < len ? csrc[i + 2] : 0u;
                     pre[h].w = 0u;
                 }
             }
         }
     };
-    if (e0 < e1) fetch(e0);
-    for (uint64_t base = e0; base < e1; base += kScRound) {
+    uint32_t pend[kScE], pendw[kScE];  // overflow words of the previous round
+#pragma unroll
+    for (int j = 0; j < kScE; j++) pend[j] = kNone;
+    uint32_t wv[kScE], q[kScE], e[kScE];
+    bool     v[kScE];
+#pragma unroll
+    for (int j = 0; j < kScE; j++) v[j] = false;
+    // Overflow words of the previous round are parked in registers (read ncb before it changes).
+    auto capture_pending = [&]() {
+#pragma unroll
+        for (int j = 0; j < kScE; j++) {
+            pend[j] = kNone;
+            if (v[j] && e[j] >= 32) {  // whole extra chunks go to the pool, the rest start the stage
+                const uint32_t qq = q[j], ch = e[j] >> 5, sl = e[j] & 31u;
+                const uint32_t cb = ncb[qq];
+                pend[j]  = ch < (cb >> kCbBits) ? (kDirect | (((cb & kCbMask) + ch) * 32 + sl))
+                                                : qq * 32 + sl;
+                pendw[j] = wv[j];
+            }
+        }
+    };
+    // D: flush every full stage of the previous round as one 128-byte line (8 lanes x 16 B).
+    // Issued after this round's prefetched words are consumed and before the next prefetch, so the
+    // stores are acknowledged during the round's compute (vmcnt also counts stores on CDNA).
+    auto flush_prev = [&](uint32_t pp) {
+        const uint32_t nfl = misc[pp];
+        for (uint32_t i = tid >> 3; i < nfl; i += kScThreads / 8) {
+            const uint32_t qq = flq[i];
+            const uint32_t l8 = tid & 7;
+            const uint32_t cb = ncb[qq];
+            const uint4    vv = *(const uint4*) &stage[qq * 32 + l8 * 4];
+            if (P.ablate & 2u) {
+                asm volatile("" ::"v"(vv.x), "v"(vv.y), "v"(vv.z), "v"(vv.w));
+            } else {
+                *(uint4*) &pool[(cb & kCbMask) * 32 + l8 * 4] = vv;
+                if (!(P.ablate & 1u))  // metas of this flush's chunks
+                    for (uint32_t c = l8; c < (cb >> kCbBits); c += 8)
+                        meta[(cb & kCbMask) + c] = qq | (32u << 16);
+            }
+        }
+    };
+    if (len) fetch(0);
+    uint32_t par = 0;  // round parity (selects the flush counter)
+    for (uint32_t base = 0; base < len; base += kScRound, par ^= 1u) {
+        capture_pending();
         uint32_t x[kScE];
-        bool     v[kScE];
 #pragma unroll
         for (int h = 0; h < NR; h++) {
             if (SRC == SRC_TUPLES) {
-                const uint64_t i = base + (uint64_t) h * RSTRIDE + 2 * tid;
+                const uint32_t i = base + (uint32_t) h * RSTRIDE + 2 * tid;
                 x[2 * h]         = pre[h].x;
                 x[2 * h + 1]     = pre[h].z;
-                v[2 * h]         = i < e1;
-                v[2 * h + 1]     = i + 1 < e1;
+                v[2 * h]         = i < len;
+                v[2 * h + 1]     = i + 1 < len;
             } else {
-                const uint64_t i = base + (uint64_t) h * RSTRIDE + 4 * tid;
+                const uint32_t i = base + (uint32_t) h * RSTRIDE + 4 * tid;
                 x[4 * h]         = pre[h].x;
                 x[4 * h + 1]     = pre[h].y;
                 x[4 * h + 2]     = pre[h].z;
                 x[4 * h + 3]     = pre[h].w;
 #pragma unroll
-                for (int j = 0; j < 4; j++) v[4 * h + j] = i + j < e1;
+                for (int j = 0; j < 4; j++) v[4 * h + j] = i + j < len;
             }
         }
-        if (base + kScRound < e1) fetch(base + kScRound);
-        uint32_t wv[kScE], q[kScE], e[kScE];
+        // ---- A1: hash this round's words (consumes the prefetched registers)
 #pragma unroll
         for (int j = 0; j < kScE; j++) {
-            sc_word<SRC, MODE, FMT>(x[j], P.g, fwd, wv[j], q[j]);
-            e[j] = v[j] ? atomicAdd(&fill[q[j]], 1u) : 0u;
+            if (P.ablate & 4u) {
+                wv[j] = x[j];
+                q[j]  = x[j] & (F - 1u);
+            } else {
+                sc_word<SRC, MODE, FMT>(x[j], P.g, fwd, wv[j], q[j]);
+            }
+        }
+        flush_prev(par ^ 1u);
+        if (base + kScRound < len) fetch(base + kScRound);
+        // ---- A2: rank every word in its partition's stage
+#pragma unroll
+        for (int j = 0; j < kScE; j++) {
+            if (P.ablate & 8u) {
+                e[j] = 0;
+                asm volatile("" ::"v"(wv[j]), "v"(q[j]));
+                v[j] = false;
+            } else {
+                e[j] = v[j] ? atomicAdd(&fill[q[j]], 1u) : 0u;
+            }
         }
         __syncthreads();
+        // ---- B: previous round's overflow words, this round's in-stage words; C: flush plan
+        if (tid == 0) misc[par ^ 1u] = 0;
 #pragma unroll
-        for (int j = 0; j < kScE; j++)
+        for (int j = 0; j < kScE; j++) {
+            if (pend[j] != kNone) {
+                if (pend[j] & kDirect) pool[pend[j] & ~kDirect] = pendw[j];
+                else stage[pend[j]] = pendw[j];
+            }
             if (v[j] && e[j] < 32) stage[q[j] * 32 + e[j]] = wv[j];
+        }
         for (uint32_t qq = tid; qq < F; qq += kScThreads) {
             const uint32_t f = fill[qq];
             if (f >= 32) {
                 const uint32_t c  = f >> 5;
-                const uint32_t cb = atomicAdd(&misc[1], c);
+                const uint32_t cb = atomicAdd(&misc[2], c);
                 ncb[qq]           = cb | (c << kCbBits);
                 tch[qq] += c;
                 tel[qq] += c * 32;
                 fill[qq]          = f & 31u;
-                flq[atomicAdd(&misc[0], 1u)] = qq;
-                for (uint32_t j = 0; j < c; j++) P.meta[region + cb + j] = qq | (32u << 16);
+                flq[atomicAdd(&misc[par], 1u)] = qq;
             }
         }
         __syncthreads();
-        const uint32_t nfl = misc[0];
-        for (uint32_t i = tid >> 3; i < nfl; i += kScThreads / 8) {
-            const uint32_t qq = flq[i];
-            const uint32_t l8 = tid & 7;
-            const uint4    vv = *(const uint4*) &stage[qq * 32 + l8 * 4];
-            *(uint4*) &pool[(region + (ncb[qq] & kCbMask)) * 32 + l8 * 4] = vv;
-        }
-        __syncthreads();
-        if (tid == 0) misc[0] = 0;
+    }
+    capture_pending();
+    flush_prev(par ^ 1u);
+    __syncthreads();
 #pragma unroll
-        for (int j = 0; j < kScE; j++) {
-            if (v[j] && e[j] >= 32) {
-                const uint32_t qq = q[j], ch = e[j] >> 5, s = e[j] & 31u;
-                const uint32_t cb = ncb[qq];
-                if (ch < (cb >> kCbBits))
-                    pool[(region + (cb & kCbMask) + ch) * 32 + s] = wv[j];
-                else
-                    stage[qq * 32 + s] = wv[j];
-            }
+    for (int j = 0; j < kScE; j++) {
+        if (pend[j] != kNone) {
+            if (pend[j] & kDirect) pool[pend[j] & ~kDirect] = pendw[j];
+            else stage[pend[j]] = pendw[j];
         }
     }
     __syncthreads();
     for (uint32_t qq = tid; qq < F; qq += kScThreads) {
         const uint32_t f = fill[qq];
         if (f > 0) {
-            const uint32_t cb         = atomicAdd(&misc[1], 1u);
-            P.meta[region + cb]       = qq | (f << 16);
-            for (uint32_t s = 0; s < f; s++) pool[(region + cb) * 32 + s] = stage[qq * 32 + s];
+            const uint32_t cb = atomicAdd(&misc[2], 1u);
+            meta[cb]          = qq | (f << 16);
+            for (uint32_t s2 = 0; s2 < f; s2++) pool[cb * 32 + s2] = stage[qq * 32 + s2];
             tch[qq] += 1;
             tel[qq] += f;
         }
     }
     __syncthreads();
-    if (tid == 0) P.wg_used[wg] = misc[1];
+    if (tid == 0) P.wg_used[wg] = misc[2];
     for (uint32_t qq = tid; qq < F; qq += kScThreads) {
         if (tch[qq]) {
             atomicAdd(&P.part_chunks[qq], tch[qq]);
@@ -914,7 +968,7 @@ void launch_probe_global(const uint2* S, uint64_t n, const Geometry& g, const Cr
 
 size_t scatter_lds_bytes(uint32_t log2F) {
     const size_t F = 1u << log2F;
-    return (F * 32 + F * 5 + 128 + 4) * sizeof(uint32_t);
+    return (F * 32 + F * 5 + 128 + 4) * sizeof(uint32_t);  // stage, 5 arrays, table, misc
 }
 
 static int scatter_elems() {  // dev knob for A/B runs: HWBRJ_SCE=4|8 elements per thread/round
@@ -936,7 +990,10 @@ static void scatter_inst(const ScatterParams& p, uint32_t grid, hipStream_t st) 
     }
 }
 
-void launch_scatter(const ScatterParams& p, int src, uint32_t grid, hipStream_t st) {
+void launch_scatter(const ScatterParams& p0, int src, uint32_t grid, hipStream_t st) {
+    ScatterParams p = p0;
+    const char*   ab = getenv("HWBRJ_SC_ABLATE");
+    p.ablate         = ab ? (uint32_t) atoi(ab) : 0u;
     const Geometry& g = p.g;
     if (src == SRC_CODES) return scatter_inst<SRC_CODES, MODE_GLOBAL, FMT_CODE>(p, grid, st);
     switch (g.mode) {
