@@ -185,11 +185,19 @@ bool plan_geometry(const bloom_filter_args_t* a, uint64_t nR, Geometry* g, std::
             if (g->mode == MODE_SLICE_BLOCK) g->lbmask = (g->nblocks >> g->log2F) - 1u;
         }
     }
+    // Join sub-partitions (k_join): codes of a job share their low hash_shift bits. Where the
+    // partition digit is a code digit (sub_shift = log2F), 2^(14 - log2F) subs make the job keys
+    // v = code >> hash_shift fit the 2^18-bit LDS bitmap; otherwise (or when that needs > 64 subs)
+    // the hash table path needs <= ~4096 R keys per job.
     const uint64_t F    = 1ull << g->log2F;
     const uint64_t rper = (nR + F - 1) / F;
     uint32_t       l2s  = 0;
-    while (l2s < 6 && (rper >> l2s) > 8192) l2s++;
     g->sub_shift  = (g->mode == MODE_SLICE_BASIC) ? 0 : g->log2F;
+    if (g->sub_shift > 0 && g->log2F + 6 >= 14) {
+        l2s = g->log2F >= 14 ? 0 : 14 - g->log2F;
+    } else {
+        while (l2s < 6 && (rper >> l2s) > 4096) l2s++;
+    }
     if (g->sub_shift + l2s == 0) l2s = 1;  // k_join stores code >> hash_shift with an empty sentinel
     g->log2NSUB   = l2s;
     g->hash_shift = g->sub_shift + g->log2NSUB;
@@ -232,10 +240,10 @@ Engine::Engine(int device) : device_(device) {
 Engine::~Engine() { release(); }
 
 void Engine::release() {
-    for (DevBuf* b : {&poolR, &metaR, &usedR, &pchR, &pelR, &lstartR, &lcurR, &estartR, &istartR,
-                      &listR, &poolS, &metaS, &usedS, &pchS, &pelS, &lstartS, &lcurS, &estartS,
-                      &istartS, &listS, &slices, &bitmap, &rjoin, &rqs, &surv, &survcnt, &itemoff,
-                      &qstot, &sqs, &sjoin, &dense, &small})
+    for (DevBuf* b : {&poolR, &metaR, &usedR, &wgqcR, &wgqeR, &wgqoR, &lstartR, &estartR, &istartR,
+                      &listR, &poolS, &metaS, &usedS, &wgqcS, &wgqeS, &wgqoS, &lstartS, &estartS,
+                      &istartS, &listS, &slices, &bitmap, &rjoin, &rqs, &surv, &survcnt, &survoff,
+                      &dense, &small})
         b->release();
     have_filter_ = false;
 }
@@ -259,27 +267,28 @@ int Engine::run(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     const uint32_t F = 1u << g.log2F, NSUB = 1u << g.log2NSUB, NJ = F * NSUB;
     const bool     slice_mode = g.mode == MODE_SLICE_BLOCK || g.mode == MODE_SLICE_BASIC;
     const uint32_t nseg       = slice_mode ? g.nseg : 1;
-    const uint32_t CH         = 1024;  // chunks per probe item (= one k_probe sweep)
+    const uint32_t CH         = probe_chunks_per_item();  // chunks per probe item
     const size_t   sc_lds     = scatter_lds_bytes(g.log2F);
     const uint32_t G          = (uint32_t) cus_ * (uint32_t) std::max<size_t>(1, std::min<size_t>(2, 163840 / sc_lds));
     const uint64_t capR = region_cap(nR, G, F), capS = region_cap(nS, G, F);
     const uint64_t LR = (uint64_t) G * capR, LS = (uint64_t) G * capS;  // max chunks
     const uint64_t items_max = (LS / CH + F + 1) * nseg;
-    if (LS > 0xFFFFFFFFull || LR > 0xFFFFFFFFull || capS >= (1u << 22) || capR >= (1u << 22)) {
-        set_last_error("relation too large for 32-bit chunk ids");
+    // list entries hold a 27-bit chunk id (hwbrj_kernels.hip, K4); metas a 22-bit region offset
+    if (LS > (1ull << 27) || LR > (1ull << 27) || capS >= (1u << 22) || capR >= (1u << 22)) {
+        set_last_error("relation too large for 27-bit chunk ids (|S| or |R| > ~4.2e9 tuples per GPU)");
         return 3;
     }
+    const uint64_t GF = (uint64_t) G * F;
     bool ok = true;
     ok &= poolR.ensure(LR * 128) && metaR.ensure(LR * 4) && listR.ensure(LR * 4);
-    ok &= usedR.ensure(G * 4) && pchR.ensure(F * 4) && pelR.ensure(F * 8) && lcurR.ensure(F * 4);
+    ok &= usedR.ensure(G * 4) && wgqcR.ensure(GF * 4) && wgqeR.ensure(GF * 4) && wgqoR.ensure(GF * 4);
     ok &= lstartR.ensure((F + 1) * 4) && estartR.ensure((F + 1) * 8) && istartR.ensure((F + 1) * 4);
     ok &= poolS.ensure(LS * 128) && metaS.ensure(LS * 4) && listS.ensure(LS * 4);
-    ok &= usedS.ensure(G * 4) && pchS.ensure(F * 4) && pelS.ensure(F * 8) && lcurS.ensure(F * 4);
+    ok &= usedS.ensure(G * 4) && wgqcS.ensure(GF * 4) && wgqeS.ensure(GF * 4) && wgqoS.ensure(GF * 4);
     ok &= lstartS.ensure((F + 1) * 4) && estartS.ensure((F + 1) * 8) && istartS.ensure((F + 1) * 4);
     ok &= rjoin.ensure(nR * 4) && rqs.ensure((NJ + 1) * 8ull);
     ok &= surv.ensure(nseg * LS * 128) && survcnt.ensure(items_max * NSUB * 4) &&
-          itemoff.ensure(items_max * NSUB * 4);
-    ok &= qstot.ensure(NJ * 8ull) && sqs.ensure((NJ + 1) * 8ull) && sjoin.ensure(nS * 4);
+          survoff.ensure(items_max * NSUB * 4);
     ok &= small.ensure(64);
     if (slice_mode) ok &= slices.ensure((uint64_t) F * nseg * g.seg_words * 4);
     if (g.mode == MODE_GLOBAL) ok &= bitmap.ensure(((g.m + 31) / 32) * 4) && dense.ensure(nS * 4);
@@ -287,14 +296,11 @@ int Engine::run(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
         set_last_error("hipMalloc failed (device memory)");
         return 4;
     }
-    uint64_t* d_result = small.as<uint64_t>();      // [0] matches
-    uint64_t* d_dcount = small.as<uint64_t>() + 1;  // [1] dense survivor count (global mode)
+    uint64_t* d_result   = small.as<uint64_t>();      // [0] matches
+    uint64_t* d_dcount   = small.as<uint64_t>() + 1;  // [1] dense survivor count (global mode)
+    uint64_t* d_filtered = small.as<uint64_t>() + 2;  // [2] S-tuples after filter
 
     // zeroing outside the timed region (the reference callocs before its timer, :1583, :1601)
-    HWBRJ_CHECK(hipMemsetAsync(pchR.p, 0, F * 4, stream));
-    HWBRJ_CHECK(hipMemsetAsync(pelR.p, 0, F * 8, stream));
-    HWBRJ_CHECK(hipMemsetAsync(pchS.p, 0, F * 4, stream));
-    HWBRJ_CHECK(hipMemsetAsync(pelS.p, 0, F * 8, stream));
     HWBRJ_CHECK(hipMemsetAsync(small.p, 0, 64, stream));
     if (g.mode == MODE_GLOBAL) HWBRJ_CHECK(hipMemsetAsync(bitmap.p, 0, bitmap.bytes, stream));
 
@@ -306,27 +312,26 @@ int Engine::run(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     // ---------------------------------------------------------------- R: pass-1 (+ filter)
     if (g.mode == MODE_GLOBAL)
         launch_build_global(dR, nR, g, d_tabs_, bitmap.as<uint32_t>(), stream);
-    sp.src = dR;
-    sp.n = nR;
-    sp.n_dev = nullptr;
-    sp.pool = poolR.as<uint32_t>();
-    sp.meta = metaR.as<uint32_t>();
-    sp.wg_used = usedR.as<uint32_t>();
-    sp.part_chunks = pchR.as<uint32_t>();
-    sp.part_elems = pelR.as<uint64_t>();
-    sp.cap = capR;
+    sp.src        = dR;
+    sp.n          = nR;
+    sp.n_dev      = nullptr;
+    sp.pool       = poolR.as<uint32_t>();
+    sp.meta       = metaR.as<uint32_t>();
+    sp.wg_used    = usedR.as<uint32_t>();
+    sp.wgq_chunks = wgqcR.as<uint32_t>();
+    sp.wgq_elems  = wgqeR.as<uint32_t>();
+    sp.cap        = capR;
     launch_scatter(sp, SRC_TUPLES, G, stream);
     HWBRJ_CHECK(hipEventRecord(ev_[1], stream));
-    launch_plan(pchR.as<uint32_t>(), pelR.as<uint64_t>(), g.log2F, CH, 1, lstartR.as<uint32_t>(),
-                lcurR.as<uint32_t>(), estartR.as<uint64_t>(), istartR.as<uint32_t>(), stream);
-    launch_list_fill(metaR.as<uint32_t>(), usedR.as<uint32_t>(), capR, g.log2F,
-                     lcurR.as<uint32_t>(), listR.as<uint32_t>(), G, stream);
+    launch_plan(wgqcR.as<uint32_t>(), wgqeR.as<uint32_t>(), G, g.log2F, CH, 1, wgqoR.as<uint32_t>(),
+                lstartR.as<uint32_t>(), estartR.as<uint64_t>(), istartR.as<uint32_t>(), stream);
+    launch_list_fill(metaR.as<uint32_t>(), usedR.as<uint32_t>(), capR, g.log2F, wgqoR.as<uint32_t>(),
+                     lstartR.as<uint32_t>(), listR.as<uint32_t>(), G, stream);
     HWBRJ_CHECK(hipEventRecord(ev_[2], stream));
     BuildParams bp{};
     bp.g          = g;
     bp.tabs       = d_tabs_;
     bp.pool       = poolR.as<uint32_t>();
-    bp.meta       = metaR.as<uint32_t>();
     bp.list       = listR.as<uint32_t>();
     bp.list_start = lstartR.as<uint32_t>();
     bp.elem_start = estartR.as<uint64_t>();
@@ -347,25 +352,23 @@ int Engine::run(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
         sp.n     = nS;
         sp.n_dev = nullptr;
     }
-    sp.pool = poolS.as<uint32_t>();
-    sp.meta = metaS.as<uint32_t>();
-    sp.wg_used = usedS.as<uint32_t>();
-    sp.part_chunks = pchS.as<uint32_t>();
-    sp.part_elems = pelS.as<uint64_t>();
-    sp.cap = capS;
+    sp.pool       = poolS.as<uint32_t>();
+    sp.meta       = metaS.as<uint32_t>();
+    sp.wg_used    = usedS.as<uint32_t>();
+    sp.wgq_chunks = wgqcS.as<uint32_t>();
+    sp.wgq_elems  = wgqeS.as<uint32_t>();
+    sp.cap        = capS;
     launch_scatter(sp, g.mode == MODE_GLOBAL ? SRC_CODES : SRC_TUPLES, G, stream);
     HWBRJ_CHECK(hipEventRecord(ev_[4], stream));
-    launch_plan(pchS.as<uint32_t>(), pelS.as<uint64_t>(), g.log2F, CH, nseg,
-                lstartS.as<uint32_t>(), lcurS.as<uint32_t>(), estartS.as<uint64_t>(),
-                istartS.as<uint32_t>(), stream);
-    launch_list_fill(metaS.as<uint32_t>(), usedS.as<uint32_t>(), capS, g.log2F,
-                     lcurS.as<uint32_t>(), listS.as<uint32_t>(), G, stream);
+    launch_plan(wgqcS.as<uint32_t>(), wgqeS.as<uint32_t>(), G, g.log2F, CH, nseg, wgqoS.as<uint32_t>(),
+                lstartS.as<uint32_t>(), estartS.as<uint64_t>(), istartS.as<uint32_t>(), stream);
+    launch_list_fill(metaS.as<uint32_t>(), usedS.as<uint32_t>(), capS, g.log2F, wgqoS.as<uint32_t>(),
+                     lstartS.as<uint32_t>(), listS.as<uint32_t>(), G, stream);
     HWBRJ_CHECK(hipEventRecord(ev_[5], stream));
     ProbeParams pp{};
     pp.g               = g;
     pp.tabs            = d_tabs_;
     pp.pool            = poolS.as<uint32_t>();
-    pp.meta            = metaS.as<uint32_t>();
     pp.list            = listS.as<uint32_t>();
     pp.list_start      = lstartS.as<uint32_t>();
     pp.item_start      = istartS.as<uint32_t>();
@@ -373,47 +376,57 @@ int Engine::run(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     pp.surv            = surv.as<uint32_t>();
     pp.surv_seg_stride = LS * 32;
     pp.surv_cnt        = survcnt.as<uint32_t>();
-    pp.CH              = CH;
-    const size_t   pl_lds = slice_lds_bytes(g);
+    pp.surv_off        = survoff.as<uint32_t>();
+    pp.filtered        = d_filtered;
+    const size_t   pl_lds = probe_lds_bytes(g, nullptr);
     const uint32_t PG = (uint32_t) cus_ * (uint32_t) std::max<size_t>(1, std::min<size_t>(2, 163840 / pl_lds));
+    const bool dbg_on = getenv("HWBRJ_DBG") != nullptr;  // dev-only phase stamps
+    if (dbg_on) {
+        ok &= dbgP.ensure((size_t) std::max<uint32_t>(PG, F) * 64) && dbgJ.ensure((size_t) F * 64);
+        HWBRJ_CHECK(hipMemsetAsync(dbgP.p, 0, dbgP.bytes, stream));
+        HWBRJ_CHECK(hipMemsetAsync(dbgJ.p, 0, dbgJ.bytes, stream));
+        pp.dbg = dbgP.as<uint64_t>();
+    }
     launch_probe(pp, PG, stream);
     HWBRJ_CHECK(hipEventRecord(ev_[6], stream));
-    // ------------------------------------------------------- S: pass-2 of the survivors
-    launch_surv_totals(istartS.as<uint32_t>(), survcnt.as<uint32_t>(), g.log2F, g.log2NSUB,
-                       itemoff.as<uint32_t>(), qstot.as<uint64_t>(), stream);
-    launch_scan_u64(qstot.as<uint64_t>(), sqs.as<uint64_t>(), NJ, stream);
-    SurvParams sv{};
-    sv.log2F           = g.log2F;
-    sv.log2NSUB        = g.log2NSUB;
-    sv.sub_shift       = g.sub_shift;
-    sv.nseg            = nseg;
-    sv.CH              = CH;
-    sv.item_start      = istartS.as<uint32_t>();
-    sv.list_start      = lstartS.as<uint32_t>();
-    sv.surv            = surv.as<uint32_t>();
-    sv.surv_seg_stride = LS * 32;
-    sv.surv_cnt        = survcnt.as<uint32_t>();
-    sv.item_off        = itemoff.as<uint32_t>();
-    sv.qs_off          = sqs.as<uint64_t>();
-    sv.out             = sjoin.as<uint32_t>();
-    launch_surv_scatter(sv, (uint32_t) cus_ * 8, stream);
-    HWBRJ_CHECK(hipEventRecord(ev_[7], stream));
+    HWBRJ_CHECK(hipEventRecord(ev_[7], stream));  // (survivor sub-partitioning is fused into k_probe)
     // -------------------------------------------------------------------------- join
     JoinParams jp{};
-    jp.r_codes    = rjoin.as<uint32_t>();
-    jp.r_off      = rqs.as<uint64_t>();
-    jp.s_codes    = sjoin.as<uint32_t>();
-    jp.s_off      = sqs.as<uint64_t>();
-    jp.hash_shift = g.hash_shift;
-    jp.result     = d_result;
+    jp.r_codes         = rjoin.as<uint32_t>();
+    jp.r_off           = rqs.as<uint64_t>();
+    jp.surv            = surv.as<uint32_t>();
+    jp.surv_cnt        = survcnt.as<uint32_t>();
+    jp.surv_off        = survoff.as<uint32_t>();
+    jp.item_start      = istartS.as<uint32_t>();
+    jp.list_start      = lstartS.as<uint32_t>();
+    jp.surv_seg_stride = LS * 32;
+    jp.nseg            = nseg;
+    jp.CH              = CH;
+    jp.log2NSUB        = g.log2NSUB;
+    jp.hash_shift      = g.hash_shift;
+    jp.bitmap          = (g.sub_shift > 0 && 32 - g.hash_shift <= 18) ? 1u : 0u;
+    jp.result          = d_result;
+    jp.dbg             = dbg_on ? dbgJ.as<uint64_t>() : nullptr;
     launch_join(jp, NJ, stream);
     HWBRJ_CHECK(hipEventRecord(ev_[8], stream));
     HWBRJ_CHECK(hipGetLastError());
     HWBRJ_CHECK(hipEventSynchronize(ev_[8]));
 
+    if (dbg_on) {
+        std::vector<uint64_t> hp(PG * 8), hj(F * 8);
+        HWBRJ_CHECK(hipMemcpy(hp.data(), dbgP.p, hp.size() * 8, hipMemcpyDeviceToHost));
+        HWBRJ_CHECK(hipMemcpy(hj.data(), dbgJ.p, hj.size() * 8, hipMemcpyDeviceToHost));
+        double sp_[6] = {0}, sj[6] = {0};
+        for (uint32_t b = 0; b < PG; b++)
+            for (int k = 0; k < 6; k++) sp_[k] += (double) hp[b * 8 + k] / PG;
+        for (uint32_t b = 0; b < F; b++)
+            for (int k = 0; k < 6; k++) sj[k] += (double) hj[b * 8 + k] / F;
+        fprintf(stderr, "[dbg] probe cyc/WG: top %.0f test %.0f b1 %.0f scan+b2 %.0f write %.0f b3+copy %.0f\n",
+                sp_[0], sp_[1], sp_[2], sp_[3], sp_[4], sp_[5]);
+    }
     uint64_t matches = 0, filtered = 0;
     HWBRJ_CHECK(hipMemcpy(&matches, d_result, 8, hipMemcpyDeviceToHost));
-    HWBRJ_CHECK(hipMemcpy(&filtered, sqs.as<uint64_t>() + NJ, 8, hipMemcpyDeviceToHost));
+    HWBRJ_CHECK(hipMemcpy(&filtered, d_filtered, 8, hipMemcpyDeviceToHost));
     have_filter_ = args != nullptr;
     last_g_      = g;
     if (st) {

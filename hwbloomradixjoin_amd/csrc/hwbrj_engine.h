@@ -48,10 +48,10 @@ class Engine {
     CrcTables*   d_tabs_ = nullptr;
     GenPlan*     d_plan_ = nullptr;
     // R side
-    DevBuf poolR, metaR, usedR, pchR, pelR, lstartR, lcurR, estartR, istartR, listR;
+    DevBuf poolR, metaR, usedR, wgqcR, wgqeR, wgqoR, lstartR, estartR, istartR, listR;
     // S side
-    DevBuf poolS, metaS, usedS, pchS, pelS, lstartS, lcurS, estartS, istartS, listS;
-    DevBuf slices, bitmap, rjoin, rqs, surv, survcnt, itemoff, qstot, sqs, sjoin, dense, small;
+    DevBuf poolS, metaS, usedS, wgqcS, wgqeS, wgqoS, lstartS, estartS, istartS, listS;
+    DevBuf slices, bitmap, rjoin, rqs, surv, survcnt, survoff, dense, small, dbgP, dbgJ;
 };
 
 Engine* engine_for_current_device();

@@ -19,8 +19,8 @@ struct ScatterParams {
     uint32_t*        pool;         // [G * cap][32] chunk words
     uint32_t*        meta;         // [G * cap]: partition | count << 16
     uint32_t*        wg_used;      // [G] chunks used by each workgroup
-    uint32_t*        part_chunks;  // [F] (atomic)
-    uint64_t*        part_elems;   // [F] (atomic)
+    uint32_t*        wgq_chunks;   // [G][F] chunks of partition q in workgroup wg's region
+    uint32_t*        wgq_elems;    // [G][F] elements of partition q in workgroup wg's region
     uint64_t         cap;          // chunk capacity of one workgroup region
     Geometry         g;
     const CrcTables* tabs;
@@ -31,8 +31,7 @@ struct BuildParams {
     Geometry         g;
     const CrcTables* tabs;
     const uint32_t*  pool;
-    const uint32_t*  meta;
-    const uint32_t*  list;
+    const uint32_t*  list;        // chunk lists (entry = chunk id | count << 27)
     const uint32_t*  list_start;  // [F + 1]
     const uint64_t*  elem_start;  // [F + 1]
     uint32_t*        slices;      // [F][nseg][seg_words]
@@ -44,36 +43,32 @@ struct ProbeParams {
     Geometry         g;
     const CrcTables* tabs;
     const uint32_t*  pool;
-    const uint32_t*  meta;
-    const uint32_t*  list;
+    const uint32_t*  list;        // chunk lists (entry = chunk id | count << 27)
     const uint32_t*  list_start;  // [F + 1]
     const uint32_t*  item_start;  // [F + 1]
     const uint32_t*  slices;
-    uint32_t*        surv;        // per item: survivors at (seg * surv_seg_stride + list_pos * 32)
+    uint32_t*        surv;        // item region at (seg * surv_seg_stride + list_pos * 32), by sub
     uint64_t         surv_seg_stride;
-    uint32_t*        surv_cnt;    // [items][NSUB]
-    uint32_t         CH;          // chunks per item
-};
-
-struct SurvParams {
-    uint32_t        log2F, log2NSUB, sub_shift, nseg, CH;
-    const uint32_t* item_start;
-    const uint32_t* list_start;
-    const uint32_t* surv;
-    uint64_t        surv_seg_stride;
-    const uint32_t* surv_cnt;
-    const uint32_t* item_off;
-    const uint64_t* qs_off;
-    uint32_t*       out;
+    uint32_t*        surv_cnt;    // [items][NSUB] survivors of each (item, sub) run
+    uint32_t*        surv_off;    // [items][NSUB] run offset inside the item region
+    uint64_t*        filtered;    // += survivors ("S-tuples after filter")
+    uint32_t         stage_cap;   // survivor stage words (set by launch_probe)
+    uint64_t*        dbg;         // dev-only: per-workgroup phase cycles (HWBRJ_DBG), or nullptr
 };
 
 struct JoinParams {
-    const uint32_t* r_codes;
-    const uint64_t* r_off;  // [jobs + 1]
-    const uint32_t* s_codes;
-    const uint64_t* s_off;  // [jobs + 1]
-    uint32_t        hash_shift;
+    const uint32_t* r_codes;      // R codes grouped by (q, sub)
+    const uint64_t* r_off;        // [F * NSUB + 1]
+    const uint32_t* surv;         // survivor runs written by k_probe
+    const uint32_t* surv_cnt;
+    const uint32_t* surv_off;
+    const uint32_t* item_start;   // S items [F + 1]
+    const uint32_t* list_start;   // S lists [F + 1]
+    uint64_t        surv_seg_stride;
+    uint32_t        nseg, CH, log2NSUB, hash_shift;
+    uint32_t        bitmap;       // 1: keys fit the direct-address bitmap (32 - hash_shift <= 18)
     uint64_t*       result;
+    uint64_t*       dbg;          // dev-only: per-workgroup phase cycles (HWBRJ_DBG), or nullptr
 };
 
 void   launch_gen(uint2* out, uint64_t offset, uint64_t count, const GenPlan* d_plan, const Perm& perm,
@@ -85,18 +80,17 @@ void   launch_probe_global(const uint2* S, uint64_t n, const Geometry& g, const 
 size_t scatter_lds_bytes(uint32_t log2F);
 void   launch_scatter(const ScatterParams& p, int src, uint32_t grid, hipStream_t st);
 void   launch_list_fill(const uint32_t* meta, const uint32_t* wg_used, uint64_t cap,
-                        uint32_t log2F, uint32_t* list_cursor, uint32_t* list, uint32_t grid,
-                        hipStream_t st);
-void   launch_plan(const uint32_t* part_chunks, const uint64_t* part_elems, uint32_t log2F,
-                   uint32_t CH, uint32_t nseg, uint32_t* list_start, uint32_t* list_cursor,
-                   uint64_t* elem_start, uint32_t* item_start, hipStream_t st);
-void   launch_scan_u64(const uint64_t* in, uint64_t* out, uint32_t n, hipStream_t st);
+                        uint32_t log2F, const uint32_t* wgq_off, const uint32_t* list_start,
+                        uint32_t* list, uint32_t grid, hipStream_t st);
+void   launch_plan(const uint32_t* wgq_chunks, const uint32_t* wgq_elems, uint32_t G,
+                   uint32_t log2F, uint32_t CH, uint32_t nseg, uint32_t* wgq_off,
+                   uint32_t* list_start, uint64_t* elem_start, uint32_t* item_start,
+                   hipStream_t st);
+uint32_t probe_chunks_per_item();
+size_t   probe_lds_bytes(const Geometry& g, uint32_t* stage_cap);
 size_t slice_lds_bytes(const Geometry& g);
 void   launch_build(const BuildParams& p, uint32_t F, hipStream_t st);
 void   launch_probe(const ProbeParams& p, uint32_t grid, hipStream_t st);
-void   launch_surv_totals(const uint32_t* item_start, const uint32_t* surv_cnt, uint32_t log2F,
-                          uint32_t log2NSUB, uint32_t* item_off, uint64_t* qs_tot, hipStream_t st);
-void   launch_surv_scatter(const SurvParams& p, uint32_t grid, hipStream_t st);
 void   launch_join(const JoinParams& p, uint32_t jobs, hipStream_t st);
 void   launch_export(const uint32_t* slices, const Geometry& g, uint32_t* out, uint64_t nwords,
                      hipStream_t st);

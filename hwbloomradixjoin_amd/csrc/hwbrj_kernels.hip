@@ -19,6 +19,8 @@
 #include <hip/hip_runtime.h>
 #include <stdlib.h>
 
+#include <algorithm>
+
 #include "hwbrj_common.h"
 #include "hwbrj_kernels.h"
 
@@ -43,6 +45,13 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
     return v;
+}
+
+// Raw buffer access: out-of-range stores are dropped and loads return 0, so a fixed number of
+// instructions can be issued unconditionally (static vmcnt bookkeeping in pipelined loops).
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int) bytes, 0x00020000);
 }
 
 // Where an element's filter bits live inside its partition slice (KIND != KIND_PASS).
@@ -459,47 +468,31 @@ __global__ __launch_bounds__(kScThreads) void k_scatter(ScatterParams P) {
     }
     __syncthreads();
     if (tid == 0) P.wg_used[wg] = misc[2];
+    // this workgroup's row of the (workgroup x partition) chunk / element matrices (k_plan scans
+    // them column-wise: no global atomics)
     for (uint32_t qq = tid; qq < F; qq += kScThreads) {
-        if (tch[qq]) {
-            atomicAdd(&P.part_chunks[qq], tch[qq]);
-            atomicAdd((unsigned long long*) &P.part_elems[qq], (unsigned long long) tel[qq]);
-        }
+        P.wgq_chunks[wg * F + qq] = tch[qq];
+        P.wgq_elems[wg * F + qq]  = tel[qq];
     }
 }
 
-// =================================================================== K4: chunk lists
-__global__ __launch_bounds__(1024) void k_list_fill(const uint32_t* meta, const uint32_t* wg_used,
-                                                    uint64_t cap, uint32_t log2F,
-                                                    uint32_t* list_cursor, uint32_t* list) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    const uint32_t F   = 1u << log2F;
-    uint32_t*      cnt = lds;
-    uint32_t*      cur = lds + F;
-    for (uint32_t i = threadIdx.x; i < F; i += blockDim.x) cnt[i] = 0;
-    __syncthreads();
-    const uint64_t region = blockIdx.x * cap;
-    const uint32_t used   = wg_used[blockIdx.x];
-    for (uint32_t i = threadIdx.x; i < used; i += blockDim.x)
-        atomicAdd(&cnt[meta[region + i] & 0xFFFFu], 1u);
-    __syncthreads();
-    for (uint32_t i = threadIdx.x; i < F; i += blockDim.x)
-        if (cnt[i]) cur[i] = atomicAdd(&list_cursor[i], cnt[i]);
-    __syncthreads();
-    for (uint32_t i = threadIdx.x; i < used; i += blockDim.x) {
-        const uint32_t q   = meta[region + i] & 0xFFFFu;
-        const uint32_t pos = atomicAdd(&cur[q], 1u);
-        list[pos]          = (uint32_t) (region + i);
-    }
-}
+// ====================================================== K4: planning scan and chunk lists
+// List entries carry the chunk's element count, so consumers never read `meta`:
+//   entry = chunk_id | (count & 31) << kListIdBits   (count 32 is stored as 0)
+constexpr uint32_t kListIdBits = 27;
+constexpr uint32_t kListIdMask = (1u << kListIdBits) - 1u;
+constexpr uint32_t kNoEntry    = 0xFFFFFFFFu;
 
-// ======================================================= K5: single-block scans / planning
-// After a scatter: list_start = excl-scan(part_chunks), elem_start = excl-scan(part_elems),
-// item_start = excl-scan(ceil(chunks / CH) * nseg). Arrays have F + 1 entries.
-__global__ __launch_bounds__(1024) void k_plan(const uint32_t* part_chunks,
-                                               const uint64_t* part_elems, uint32_t log2F,
-                                               uint32_t CH, uint32_t nseg, uint32_t* list_start,
-                                               uint32_t* list_cursor, uint64_t* elem_start,
-                                               uint32_t* item_start) {
+__device__ __forceinline__ uint32_t list_count(uint32_t e) { return (((e >> kListIdBits) - 1u) & 31u) + 1u; }
+
+// One block. Column-wise exclusive scan of the scatter's (workgroup x partition) matrices gives
+// every (wg, q) its offset inside q's chunk list; then list_start = excl-scan(chunks),
+// elem_start = excl-scan(elements), item_start = excl-scan(ceil(chunks / CH) * nseg) over q.
+__global__ __launch_bounds__(1024) void k_plan(const uint32_t* __restrict__ wgq_chunks,
+                                               const uint32_t* __restrict__ wgq_elems, uint32_t G,
+                                               uint32_t log2F, uint32_t CH, uint32_t nseg,
+                                               uint32_t* __restrict__ wgq_off, uint32_t* list_start,
+                                               uint64_t* elem_start, uint32_t* item_start) {
     __shared__ uint32_t sc[1024];
     __shared__ uint32_t si[1024];
     __shared__ uint64_t se[1024];
@@ -508,8 +501,26 @@ __global__ __launch_bounds__(1024) void k_plan(const uint32_t* part_chunks,
     uint32_t c = 0, it = 0;
     uint64_t e = 0;
     if (t < F) {
-        c  = part_chunks[t];
-        e  = part_elems[t];
+        uint32_t wg = 0;
+        for (; wg + 8 <= G; wg += 8) {
+            uint32_t cc[8], ee[8];
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                cc[j] = wgq_chunks[(wg + j) * F + t];
+                ee[j] = wgq_elems[(wg + j) * F + t];
+            }
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                wgq_off[(wg + j) * F + t] = c;
+                c += cc[j];
+                e += ee[j];
+            }
+        }
+        for (; wg < G; wg++) {
+            wgq_off[wg * F + t] = c;
+            c += wgq_chunks[wg * F + t];
+            e += wgq_elems[wg * F + t];
+        }
         it = ((c + CH - 1) / CH) * nseg;
     }
     sc[t] = c;
@@ -534,7 +545,6 @@ __global__ __launch_bounds__(1024) void k_plan(const uint32_t* part_chunks,
         list_start[t + 1] = sc[t];
         item_start[t + 1] = si[t];
         elem_start[t + 1] = se[t];
-        list_cursor[t]    = sc[t] - c;
     }
     if (t == 0) {
         list_start[0] = 0;
@@ -543,74 +553,111 @@ __global__ __launch_bounds__(1024) void k_plan(const uint32_t* part_chunks,
     }
 }
 
-// Exclusive scan of n (<= 1M) u64 counts by one block: out[i] = sum_{j<i} in[j], out[n] = total.
-__global__ __launch_bounds__(1024) void k_scan_u64(const uint64_t* in, uint64_t* out, uint32_t n) {
-    __shared__ uint64_t part[1024];
-    const uint32_t t   = threadIdx.x;
-    const uint32_t per = (n + 1023) / 1024;
-    const uint32_t b   = t * per, e = min(b + per, n);
-    uint64_t       s   = 0;
-    for (uint32_t i = b; i < e; i++) s += in[i];
-    part[t] = s;
+// One block per scatter region: every chunk of the region gets its slot in its partition's list
+// (slot base = list_start[q] + wgq_off[wg][q], rank by an LDS counter). Eight meta loads per thread
+// are in flight per step.
+__global__ __launch_bounds__(1024) void k_list_fill(const uint32_t* __restrict__ meta,
+                                                    const uint32_t* __restrict__ wg_used,
+                                                    uint64_t cap, uint32_t log2F,
+                                                    const uint32_t* __restrict__ wgq_off,
+                                                    const uint32_t* __restrict__ list_start,
+                                                    uint32_t* __restrict__ list) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const uint32_t F   = 1u << log2F;
+    uint32_t*      cur = lds;
+    const uint32_t wg  = blockIdx.x;
+    for (uint32_t q = threadIdx.x; q < F; q += blockDim.x) cur[q] = list_start[q] + wgq_off[wg * F + q];
     __syncthreads();
-    for (uint32_t off = 1; off < 1024; off <<= 1) {
-        uint64_t a = t >= off ? part[t - off] : 0;
-        __syncthreads();
-        part[t] += a;
-        __syncthreads();
+    const uint64_t region = (uint64_t) wg * cap;
+    const uint32_t used   = wg_used[wg];
+    constexpr int  U      = 8;
+    for (uint32_t i0 = threadIdx.x; i0 < used; i0 += blockDim.x * U) {
+        uint32_t m[U];
+#pragma unroll
+        for (int j = 0; j < U; j++) {
+            const uint32_t i = i0 + j * blockDim.x;
+            m[j]             = i < used ? meta[region + i] : kNoEntry;
+        }
+#pragma unroll
+        for (int j = 0; j < U; j++) {
+            if (m[j] == kNoEntry) continue;
+            const uint32_t q   = m[j] & 0xFFFFu;
+            const uint32_t pos = atomicAdd(&cur[q], 1u);
+            list[pos] = (uint32_t) (region + i0 + j * blockDim.x) | (((m[j] >> 16) & 31u) << kListIdBits);
+        }
     }
-    uint64_t run = part[t] - s;
-    for (uint32_t i = b; i < e; i++) {
-        out[i] = run;
-        run += in[i];
-    }
-    if (t == 1023) out[n] = part[1023];
 }
 
 // ======================================================== chunk-walking helpers (8 lanes)
-// A sweep covers kSweep = 128 * kPQ chunks of a chunk list: 8 threads share a chunk (16 B each) and
-// every thread issues kPQ independent list loads, then kPQ independent meta + chunk loads, so a
-// workgroup keeps kPQ * 16 KiB in flight per round trip instead of one dependent load chain.
-constexpr int      kPQ    = 8;
-constexpr uint32_t kSweep = 128u * kPQ;
-
+// A sweep covers 128 * NPQ chunks of a chunk list: 8 threads share a chunk (16 B each) and every
+// thread issues NPQ independent list loads, then NPQ independent chunk loads.
+template <int NPQ>
 struct Sweep {
-    uint4    v[kPQ];
-    uint32_t n[kPQ];  // valid words of this thread's quad (0..4)
+    uint4    v[NPQ];
+    uint32_t n[NPQ];  // valid words of this thread's quad (0..4)
 };
 
-__device__ __forceinline__ void load_sweep(const uint32_t* __restrict__ list,
-                                           const uint32_t* __restrict__ pool,
-                                           const uint32_t* __restrict__ meta, uint32_t lb,
-                                           uint32_t le, Sweep& S) {
-    const uint32_t l8 = threadIdx.x & 7, cslot = threadIdx.x >> 3;
-    uint32_t       cid[kPQ];
+template <int NPQ>
+__device__ __forceinline__ void load_list(const uint32_t* __restrict__ list, uint32_t lb, uint32_t le,
+                                          uint32_t (&ent)[NPQ]) {
+    const uint32_t cslot = threadIdx.x >> 3;
 #pragma unroll
-    for (int j = 0; j < kPQ; j++) {
+    for (int j = 0; j < NPQ; j++) {
         const uint32_t l = lb + cslot + (uint32_t) j * 128u;
-        cid[j]           = l < le ? list[l] : 0xFFFFFFFFu;
+        ent[j]           = l < le ? list[l] : kNoEntry;
     }
-    uint32_t cnt[kPQ];
+}
+
+template <int NPQ>
+__device__ __forceinline__ void load_chunks(const uint32_t* __restrict__ pool, const uint32_t (&ent)[NPQ],
+                                            Sweep<NPQ>& S) {
+    const uint32_t l8 = threadIdx.x & 7;
 #pragma unroll
-    for (int j = 0; j < kPQ; j++) {
-        if (cid[j] != 0xFFFFFFFFu) {
-            cnt[j]  = meta[cid[j]] >> 16;
-            S.v[j]  = *(const uint4*) &pool[(uint64_t) cid[j] * 32 + l8 * 4];
+    for (int j = 0; j < NPQ; j++) {
+        if (ent[j] != kNoEntry) {
+            const uint32_t cnt = list_count(ent[j]);
+            const uint32_t first = l8 * 4;
+            S.n[j] = cnt > first ? min(cnt - first, 4u) : 0u;
+            S.v[j] = *(const uint4*) &pool[(uint64_t) (ent[j] & kListIdMask) * 32 + l8 * 4];
         } else {
-            cnt[j] = 0;
+            S.n[j] = 0;
             S.v[j] = make_uint4(0, 0, 0, 0);
         }
     }
+}
+
+// Branch-free variants (a fixed number of vector-memory instructions per call, so the compiler
+// can wait for exactly the loads it needs instead of vmcnt(0)). lb < le is required: slots past le
+// re-read entry le-1; load_chunks_u gives them count 0 (validity comes from lb/le, not from the
+// loaded value, so nothing forces an early wait on the list load).
+template <int NPQ>
+__device__ __forceinline__ void load_list_u(const uint32_t* __restrict__ list, uint32_t lb, uint32_t le,
+                                            uint32_t (&ent)[NPQ]) {
+    const uint32_t cslot = threadIdx.x >> 3;
 #pragma unroll
-    for (int j = 0; j < kPQ; j++) {
+    for (int j = 0; j < NPQ; j++) ent[j] = list[min(lb + cslot + (uint32_t) j * 128u, le - 1u)];
+}
+
+template <int NPQ>
+__device__ __forceinline__ void load_chunks_u(const uint32_t* __restrict__ pool, const uint32_t (&ent)[NPQ],
+                                              uint32_t lb, uint32_t le, Sweep<NPQ>& S) {
+    const uint32_t l8 = threadIdx.x & 7, cslot = threadIdx.x >> 3;
+#pragma unroll
+    for (int j = 0; j < NPQ; j++) {
+        S.v[j] = *(const uint4*) &pool[(uint64_t) (ent[j] & kListIdMask) * 32 + l8 * 4];
+        const uint32_t cnt   = lb + cslot + (uint32_t) j * 128u < le ? list_count(ent[j]) : 0u;
         const uint32_t first = l8 * 4;
-        S.n[j]               = cnt[j] > first ? min(cnt[j] - first, 4u) : 0u;
+        S.n[j] = cnt > first ? min(cnt - first, 4u) : 0u;
     }
 }
 
-__device__ __forceinline__ uint32_t sweep_word(const Sweep& S, int j, int t) {
+template <int NPQ>
+__device__ __forceinline__ uint32_t sweep_word(const Sweep<NPQ>& S, int j, int t) {
     return t == 0 ? S.v[j].x : t == 1 ? S.v[j].y : t == 2 ? S.v[j].z : S.v[j].w;
 }
+
+constexpr int      kPQ    = 8;
+constexpr uint32_t kSweep = 128u * kPQ;
 
 // ======================================================================== K6: R build
 // One workgroup per partition q. Filter bits of R go into an LDS slice segment (ds_or), the slice
@@ -636,8 +683,10 @@ __global__ __launch_bounds__(1024) void k_build(BuildParams P) {
         __syncthreads();
         const bool last = seg + 1 == nseg;
         for (uint32_t lb = l0; lb < l1; lb += kSweep) {
-            Sweep S;
-            load_sweep(P.list, P.pool, P.meta, lb, l1, S);
+            uint32_t      ent[kPQ];
+            Sweep<kPQ>    S;
+            load_list<kPQ>(P.list, lb, l1, ent);
+            load_chunks<kPQ>(P.pool, ent, S);
 #pragma unroll
             for (int j = 0; j < kPQ; j++) {
 #pragma unroll
@@ -674,8 +723,10 @@ __global__ __launch_bounds__(1024) void k_build(BuildParams P) {
     }
     __syncthreads();
     for (uint32_t lb = l0; lb < l1; lb += kSweep) {
-        Sweep S;
-        load_sweep(P.list, P.pool, P.meta, lb, l1, S);
+        uint32_t   ent[kPQ];
+        Sweep<kPQ> S;
+        load_list<kPQ>(P.list, lb, l1, ent);
+        load_chunks<kPQ>(P.pool, ent, S);
 #pragma unroll
         for (int j = 0; j < kPQ; j++) {
 #pragma unroll
@@ -691,8 +742,14 @@ __global__ __launch_bounds__(1024) void k_build(BuildParams P) {
 }
 
 // ======================================================================== K7: S probe
-// Items = (partition q, slice segment, range of <= CH chunks of q's list). Workgroups take
-// contiguous item ranges, so a slice segment is (re)loaded only when (q, seg) changes.
+// Items = (partition q, slice segment, range of <= kProbeCH chunks of q's list); workgroups take
+// contiguous item ranges, so a slice segment is (re)loaded only when (q, seg) changes. The next
+// item's list entries and chunks are loaded while the current one is tested. Survivors are
+// written into the item's own region grouped by join sub-partition (LDS counters + one scan), so
+// the join reads them in place: surv_cnt[it][sub] / surv_off[it][sub] describe the runs.
+constexpr int      kPC      = 4;              // chunk quads per thread per item
+constexpr uint32_t kProbeCH = 128u * kPC;     // chunks per probe item (1024 threads, 8 per chunk)
+
 __device__ __forceinline__ uint32_t find_q(const uint32_t* item_start, uint32_t F, uint32_t it) {
     uint32_t lo = 0, hi = F - 1;
     while (lo < hi) {
@@ -702,223 +759,368 @@ __device__ __forceinline__ uint32_t find_q(const uint32_t* item_start, uint32_t 
     return lo;
 }
 
-template <int KIND>
+// Items of partition q are numbered segment-major: local = seg * npieces + piece, where piece p
+// covers list positions [lq0 + p * CH, min(lq1, lq0 + (p + 1) * CH)). Survivors of an item are
+// written at seg * surv_seg_stride + lb * 32 (lb = first list position of the piece).
+
+template <int KIND, int ABL = 0>  // ABL: dev-only ablations (1 no ranks/writes, 2 nothing passes)
 __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    constexpr uint32_t NT  = 1024;
     const Geometry& g      = P.g;
     const uint32_t  F      = 1u << g.log2F;
     const uint32_t  NSUB   = 1u << g.log2NSUB;
     constexpr bool  slices = KIND != KIND_PASS;
+    constexpr bool  onebit = KIND == KIND_BLOCK_PK1 || KIND == KIND_BASIC_K1;
+    constexpr int   NW     = kPC * 4;   // words per thread per item
     const uint32_t  segw   = slices ? g.seg_words : 0;  // multiple of 4
     uint32_t*       slice  = lds;
     uint32_t*       inv    = slice + segw;
-    uint32_t*       subc   = inv + 128;  // NSUB
-    uint32_t*       misc   = subc + 64;  // [0] survivor cursor
+    uint32_t*       subc   = inv + 128;  // NSUB counters of the current item
+    uint32_t*       subo   = subc + 64;  // NSUB run offsets of the current item
+    uint32_t*       misc   = subo + 64;  // [0] survivors of the current item
+    uint32_t*       stage  = misc + 4;   // survivors of the current item, by sub (stage_cap words)
+    const int       tid    = threadIdx.x;
     load_tab(inv, &P.tabs->inv[0][0]);
-    for (uint32_t i = threadIdx.x; i < NSUB; i += blockDim.x) subc[i] = 0;
-    if (threadIdx.x == 0) misc[0] = 0;
-    __syncthreads();
-    const uint32_t I   = P.item_start[F];
-    const uint32_t it0 = (uint32_t) ((uint64_t) blockIdx.x * I / gridDim.x);
-    const uint32_t it1 = (uint32_t) ((uint64_t) (blockIdx.x + 1) * I / gridDim.x);
+    for (uint32_t i = tid; i < 64; i += NT) subc[i] = 0;
+    const uint32_t I    = P.item_start[F];
+    // uniform values computed on the VALU are pinned to SGPRs (readfirstlane)
+    const uint32_t it0  = __builtin_amdgcn_readfirstlane((uint32_t) ((uint64_t) blockIdx.x * I / gridDim.x));
+    const uint32_t it1  = __builtin_amdgcn_readfirstlane((uint32_t) ((uint64_t) (blockIdx.x + 1) * I / gridDim.x));
     const uint32_t nseg = slices ? g.nseg : 1;
-    const int      lane = threadIdx.x & 63;
-    if (it0 >= it1) return;
-    // walk partitions sequentially from the first item's (one binary search per workgroup)
-    uint32_t q      = find_q(P.item_start, F, it0);
-    uint32_t q_it0  = P.item_start[q], q_it1 = P.item_start[q + 1];
-    uint32_t lq0    = P.list_start[q], lq1 = P.list_start[q + 1];
-    uint32_t loaded = 0xFFFFFFFFu;
-    for (uint32_t it = it0; it < it1; it++) {
-        while (it >= q_it1) {  // uniform
-            q++;
-            q_it0 = q_it1;
-            q_it1 = P.item_start[q + 1];
-            lq0   = lq1;
-            lq1   = P.list_start[q + 1];
+    uint64_t tph[6] = {0, 0, 0, 0, 0, 0}, tlast = __builtin_amdgcn_s_memtime();
+    (void) tlast;
+    auto stamp = [&](int k) {  // dev-only phase stamps (build with -DHWBRJ_STAMPS, run with HWBRJ_DBG)
+#ifdef HWBRJ_STAMPS
+        if (P.dbg) {
+            const uint64_t t = __builtin_amdgcn_s_memtime();
+            tph[k] += t - tlast;
+            tlast = t;
         }
-        const uint32_t local = it - q_it0;
-        const uint32_t seg   = local % nseg;
-        const uint32_t piece = local / nseg;
-        const uint32_t lb    = lq0 + piece * P.CH;
-        const uint32_t le    = min(lq1, lb + P.CH);
-        if (slices) {
-            const uint32_t tag = q * nseg + seg;
-            if (loaded != tag) {
-                const uint4* src = (const uint4*) (P.slices + (uint64_t) tag * segw);
-                uint4*       dst = (uint4*) slice;
-                for (uint32_t i = threadIdx.x; i < segw / 4; i += blockDim.x) dst[i] = src[i];
-                loaded = tag;
-                __syncthreads();
-            }
+#else
+        (void) k;
+#endif
+    };
+    // Copy-out of the previous item's staged survivors and its run table. A fixed number of
+    // buffer stores whatever the counts (out-of-range ones are dropped): issued right after the
+    // next loads, so the compiler never has to wait for them (vmcnt counts stores on gfx9).
+    constexpr uint32_t kNoItem = 0x80000000u;  // copy_out has nothing to write
+    uint32_t  prev_total = 0, prev_it = kNoItem, subc_v = 0, subo_v = 0;
+    uint32_t* prev_out   = P.surv;
+    auto copy_out = [&]() {
+        const uint32_t nbytes = ((prev_total + 3u) & ~3u) * 4u;  // item region holds round_up(total, 4)
+        const auto     ro     = buf_rsrc(prev_out, nbytes);
+#pragma unroll
+        for (int k = 0; k < kPC; k++) {
+            const uint32_t i = tid + k * NT;
+            const v4u      v = ((const v4u*) stage)[i];  // LDS reads past the stage are never stored
+            __builtin_amdgcn_raw_buffer_store_b128(v, ro, i * 16, 0, 0);
         }
-        uint32_t* __restrict__ out = P.surv + (uint64_t) seg * P.surv_seg_stride + (uint64_t) lb * 32;
-        for (uint32_t l0 = lb; l0 < le; l0 += kSweep) {
-            Sweep S;
-            load_sweep(P.list, P.pool, P.meta, l0, le, S);
+        const uint32_t tb = prev_it == kNoItem ? 0u : NSUB * 4;  // run table of the previous item
+        const auto rc = buf_rsrc(P.surv_cnt + (uint64_t) (prev_it & ~kNoItem) * NSUB, tb);
+        const auto rf = buf_rsrc(P.surv_off + (uint64_t) (prev_it & ~kNoItem) * NSUB, tb);
+        __builtin_amdgcn_raw_buffer_store_b32(subc_v, rc, tid * 4, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(subo_v, rf, tid * 4, 0, 0);
+    };
+    uint64_t filtered = 0;  // thread 63: survivors of this workgroup's items
+    // Outer loop: runs of items with one (q, seg), i.e. one slice segment in LDS. Inner loop:
+    // the pieces of the run, software-pipelined (chunks of piece p+1 and list entries of p+2 are
+    // in flight while piece p is tested, ranked and written; two register buffers alternate, so
+    // no load result is ever copied; past the end the loads re-read the last piece).
+    uint32_t it = it0;
+    while (it < it1) {
+        const uint32_t q    = __builtin_amdgcn_readfirstlane(find_q(P.item_start, F, it));
+        const uint32_t qi0  = __builtin_amdgcn_readfirstlane(P.item_start[q]);
+        const uint32_t qi1  = __builtin_amdgcn_readfirstlane(P.item_start[q + 1]);
+        const uint32_t lq0  = __builtin_amdgcn_readfirstlane(P.list_start[q]);
+        const uint32_t lq1  = __builtin_amdgcn_readfirstlane(P.list_start[q + 1]);
+        const uint32_t npc  = (qi1 - qi0) / nseg;  // pieces of q
+        const uint32_t seg  = (it - qi0) / npc;
+        const uint32_t p0   = (it - qi0) - seg * npc;
+        const uint32_t rend = min(it1, qi0 + (seg + 1) * npc);  // end of this (q, seg) run
+        const uint32_t p1   = p0 + (rend - it);
+        const uint32_t rit0 = it;  // item index of piece p0
+        if (slices) {  // (every wave is past the previous item's test phase: barrier B1)
+            const uint4* src = (const uint4*) (P.slices + ((uint64_t) q * nseg + seg) * segw);
+            uint4*       dst = (uint4*) slice;
+            for (uint32_t i = tid; i < segw / 4; i += NT) dst[i] = src[i];
+            __syncthreads();
+        }
+        auto lb_of = [&](uint32_t p) { return lq0 + p * kProbeCH; };
+        auto le_of = [&](uint32_t p) { return min(lq1, lq0 + (p + 1) * kProbeCH); };
+        uint32_t   entA[kPC], entB[kPC];
+        Sweep<kPC> SA, SB;
+        {
+            const uint32_t pn = min(p0 + 1, p1 - 1);
+            load_list_u<kPC>(P.list, lb_of(p0), le_of(p0), entB);
+            load_list_u<kPC>(P.list, lb_of(pn), le_of(pn), entA);
+            load_chunks_u<kPC>(P.pool, entB, lb_of(p0), le_of(p0), SA);
+            copy_out();  // (previous run's last item, or nothing) -- the same vmcnt pattern as a step
+            prev_total = 0;
+            prev_it    = kNoItem;
+        }
+        // Sc: words of piece p (registers); en: list entries of p+1 -> Sn; enn <- list of p+2.
+        auto step = [&](uint32_t p, Sweep<kPC>& Sc, Sweep<kPC>& Sn, const uint32_t (&en)[kPC],
+                        uint32_t (&enn)[kPC]) {
+            const uint32_t p2 = min(p + 2, p1 - 1);
+            const uint32_t pn = min(p + 1, p1 - 1);
+            load_chunks_u<kPC>(P.pool, en, lb_of(pn), le_of(pn), Sn);
+            load_list_u<kPC>(P.list, lb_of(p2), le_of(p2), enn);
+            copy_out();
+            stamp(0);
+            // ---- test: all slice reads first, then pass bits, then ranks (LDS counters per sub)
+            uint32_t pass = 0;  // bit i: word i survives
+            if (onebit) {
+                uint32_t wv[NW], bb[NW];  // slice word, bit index inside the segment
 #pragma unroll
-            for (int j = 0; j < kPQ; j++) {
-                uint32_t cw[4];
-                uint32_t pm = 0;  // pass mask of this thread's (up to) 4 words
-#pragma unroll
-                for (int t = 0; t < 4; t++) {
-                    const uint32_t w    = sweep_word(S, j, t);
-                    bool           pass = (uint32_t) t < S.n[j];
-                    if (slices && pass) {
-                        const Loc L = locate<KIND>(w, g, inv);
-                        pass        = (nseg == 1 || L.seg == seg) && apply_bits<KIND, false>(L, g, slice);
-                    }
-                    cw[t] = decode_k<KIND>(w, q, g.log2F);
-                    if (pass) {
-                        pm |= 1u << t;
-                        atomicAdd(&subc[(cw[t] >> g.sub_shift) & (NSUB - 1u)], 1u);
-                    }
+                for (int i = 0; i < NW; i++) {
+                    const Loc L = locate<KIND>(sweep_word(Sc, i >> 2, i & 3), g, inv);
+                    bb[i]       = L.base + L.h;
+                    wv[i]       = slice[bb[i] >> 5];
                 }
-                const uint32_t ns   = __popc(pm);
-                const uint32_t incl = wave_incl_scan(ns);
-                uint32_t       wb   = 0;
-                if (lane == 63 && incl) wb = atomicAdd(&misc[0], incl);
-                wb = __shfl(wb, 63, 64);
-                const uint32_t o = wb + incl - ns;
 #pragma unroll
-                for (int t = 0; t < 4; t++)
-                    if (pm & (1u << t)) out[o + __popc(pm & ((1u << t) - 1u))] = cw[t];
-            }
-        }
-        __syncthreads();
-        for (uint32_t s = threadIdx.x; s < NSUB; s += blockDim.x) {
-            P.surv_cnt[(uint64_t) it * NSUB + s] = subc[s];
-            subc[s]                             = 0;
-        }
-        if (threadIdx.x == 0) misc[0] = 0;
-        __syncthreads();
-    }
-}
-
-// ============================================ K8: survivor offsets per (q, sub) and per item
-// One block per partition, one thread per sub: relative offsets of each item inside (q, sub)
-// and the (q, sub) totals.
-__global__ void k_surv_totals(const uint32_t* item_start, const uint32_t* surv_cnt,
-                              uint32_t log2NSUB, uint32_t* item_off, uint64_t* qs_tot) {
-    const uint32_t q = blockIdx.x, NSUB = 1u << log2NSUB;
-    const uint32_t i0 = item_start[q], i1 = item_start[q + 1];
-    for (uint32_t s = threadIdx.x; s < NSUB; s += blockDim.x) {
-        uint64_t run = 0;
-        for (uint32_t it = i0; it < i1; it++) {
-            item_off[(uint64_t) it * NSUB + s] = (uint32_t) run;
-            run += surv_cnt[(uint64_t) it * NSUB + s];
-        }
-        qs_tot[(uint64_t) q * NSUB + s] = run;
-    }
-}
-
-// K9: move each item's survivors into the (q, sub)-grouped join layout.
-__global__ __launch_bounds__(256) void k_surv_scatter(SurvParams P) {
-    __shared__ uint64_t cur[64];
-    const uint32_t F = 1u << P.log2F, NSUB = 1u << P.log2NSUB;
-    const uint32_t I = P.item_start[F];
-    for (uint32_t it = blockIdx.x; it < I; it += gridDim.x) {
-        const uint32_t q     = find_q(P.item_start, F, it);
-        const uint32_t local = it - P.item_start[q];
-        const uint32_t seg   = local % P.nseg;
-        const uint32_t piece = local / P.nseg;
-        const uint32_t lb    = P.list_start[q] + piece * P.CH;
-        __syncthreads();
-        uint32_t total = 0;
-        for (uint32_t s = 0; s < NSUB; s++) total += P.surv_cnt[(uint64_t) it * NSUB + s];
-        for (uint32_t s = threadIdx.x; s < NSUB; s += blockDim.x)
-            cur[s] = P.qs_off[(uint64_t) q * NSUB + s] + P.item_off[(uint64_t) it * NSUB + s];
-        __syncthreads();
-        const uint32_t* src = P.surv + (uint64_t) seg * P.surv_seg_stride + (uint64_t) lb * 32;
-        for (uint32_t i0 = threadIdx.x; i0 < total; i0 += blockDim.x * 8) {
-            uint32_t c[8];
+                for (int i = 0; i < NW; i++) {
+                    bool ok = (uint32_t) (i & 3) < Sc.n[i >> 2] && ((wv[i] >> (bb[i] & 31u)) & 1u);
+                    if (nseg > 1) ok = ok && locate<KIND>(sweep_word(Sc, i >> 2, i & 3), g, inv).seg == seg;
+                    pass |= (ok ? 1u : 0u) << i;
+                }
+            } else {
 #pragma unroll
-            for (int j = 0; j < 8; j++) {
-                const uint32_t i = i0 + j * blockDim.x;
-                c[j]             = i < total ? src[i] : 0u;
+                for (int i = 0; i < NW; i++) {
+                    bool ok = (uint32_t) (i & 3) < Sc.n[i >> 2];
+                    if (slices && ok) {
+                        const Loc L = locate<KIND>(sweep_word(Sc, i >> 2, i & 3), g, inv);
+                        ok          = (nseg == 1 || L.seg == seg) && apply_bits<KIND, false>(L, g, slice);
+                    }
+                    pass |= (ok ? 1u : 0u) << i;
+                }
             }
+            if (ABL == 2) pass = 0;
+            if (ABL == 3) {  // loads only: keep every loaded word alive, test nothing
 #pragma unroll
-            for (int j = 0; j < 8; j++) {
-                if (i0 + j * blockDim.x >= total) continue;
-                const uint32_t s   = (c[j] >> P.sub_shift) & (NSUB - 1u);
-                const uint64_t pos = atomicAdd((unsigned long long*) &cur[s], 1ull);
-                P.out[pos]         = c[j];
+                for (int j = 0; j < kPC; j++) asm volatile("" ::"v"(Sc.v[j].x), "v"(Sc.v[j].y), "v"(Sc.v[j].z), "v"(Sc.v[j].w));
+                pass = 0;
             }
+            if (ABL == 1) {
+                if (pass) atomicAdd(&subc[0], __popc(pass));
+                pass = 0;
+            }
+            uint32_t rank2[NW / 2];  // two 16-bit ranks per register (a piece holds <= 16K words)
+#pragma unroll
+            for (int i = 0; i < NW; i += 2) {
+                uint32_t r[2] = {0, 0};
+#pragma unroll
+                for (int u = 0; u < 2; u++) {
+                    const uint32_t c = decode_k<KIND>(sweep_word(Sc, (i + u) >> 2, (i + u) & 3), q, g.log2F);
+                    const uint32_t s = (c >> g.sub_shift) & (NSUB - 1u);
+                    if ((pass >> (i + u)) & 1u) r[u] = atomicAdd(&subc[s], 1u);
+                }
+                rank2[i / 2] = r[0] | (r[1] << 16);
+            }
+            stamp(1);
+            __syncthreads();  // B1
+            stamp(2);
+            if (tid < 64) {
+                const uint32_t c    = tid < NSUB ? subc[tid] : 0u;
+                const uint32_t incl = wave_incl_scan(c);
+                subc_v              = c;
+                subo_v              = incl - c;
+                if (tid < NSUB) {
+                    subo[tid] = incl - c;
+                    subc[tid] = 0;
+                }
+                if (tid == 63) {
+                    filtered += incl;
+                    misc[0] = incl;
+                }
+            }
+            __syncthreads();  // B2
+            stamp(3);
+            uint32_t* __restrict__ out = P.surv + (uint64_t) seg * P.surv_seg_stride + (uint64_t) lb_of(p) * 32;
+            const uint32_t total  = __builtin_amdgcn_readfirstlane(misc[0]);
+            const bool     staged = total <= P.stage_cap;
+            if (staged) {  // LDS stage (copied out coalesced at the next step)
+#pragma unroll
+                for (int i = 0; i < NW; i++) {
+                    const uint32_t c = decode_k<KIND>(sweep_word(Sc, i >> 2, i & 3), q, g.log2F);
+                    const uint32_t o = subo[(c >> g.sub_shift) & (NSUB - 1u)] + ((rank2[i / 2] >> (16 * (i & 1))) & 0xFFFFu);
+                    if ((pass >> i) & 1u) stage[o] = c;
+                }
+            } else {  // more survivors than the stage holds: scattered global (buffer) stores
+                const auto ro = buf_rsrc(out, total * 4);
+#pragma unroll
+                for (int i = 0; i < NW; i++) {
+                    const uint32_t c = decode_k<KIND>(sweep_word(Sc, i >> 2, i & 3), q, g.log2F);
+                    const uint32_t o = subo[(c >> g.sub_shift) & (NSUB - 1u)] + ((rank2[i / 2] >> (16 * (i & 1))) & 0xFFFFu);
+                    __builtin_amdgcn_raw_buffer_store_b32(c, ro, ((pass >> i) & 1u) ? o * 4 : 0x7FFFFFF0u, 0, 0);
+                }
+            }
+            stamp(4);
+            __syncthreads();  // B3: stage complete (copied out at the start of the next step)
+            prev_total = staged ? total : 0u;
+            prev_out   = out;
+            prev_it    = rit0 + (p - p0);
+            stamp(5);
+        };
+        for (uint32_t p = p0; p < p1; p += 2) {
+            step(p, SA, SB, entA, entB);
+            if (p + 1 < p1) step(p + 1, SB, SA, entB, entA);
         }
+        it = rend;
     }
+    copy_out();
+    if (tid == 63 && filtered) atomicAdd((unsigned long long*) P.filtered, (unsigned long long) filtered);
+    if (P.dbg && tid == 0)
+        for (int k = 0; k < 6; k++) P.dbg[blockIdx.x * 8 + k] = tph[k];
 }
 
 // ========================================================================= K10: join
-// One workgroup per (q, sub): R codes -> LDS open-addressing table (linear probing, occupancy
-// bits claimed with ds_or), then every S code walks its cluster counting equal codes. R runs
-// larger than the table are processed in pieces (S is re-streamed per piece).
-constexpr uint32_t kJoinLog2T  = 14;
-constexpr uint32_t kJoinT      = 1u << kJoinLog2T;
-constexpr uint32_t kJoinPiece  = kJoinT / 2;
-constexpr int      kJoinB      = 16;           // independent loads per thread per batch
-constexpr uint32_t kEmpty      = 0xFFFFFFFFu;  // codes of one job share their low hash_shift >= 1
-                                               // bits, so (code >> hash_shift) never equals it
+// One workgroup per (partition q, sub-partition s) job (bucket_chaining_join per task,
+// src/parallel_radix_join_bloom.c:259-329). The R codes of (q, s) are known to share their low
+// hash_shift bits, so v = code >> hash_shift identifies the key inside the job.
+//  * bitmap path (v < 2^18): every R key sets bit v of a 32 KiB LDS bitmap (ds_or_rtn); a bit
+//    that was already set means a duplicate R key, and the job falls back to the hash path
+//    (multiplicities). Each survivor then costs one LDS read.
+//  * hash path: LDS open-addressing table (linear probing, ds_cmpswap) holding pieces of <= 4096
+//    R keys; survivors count equal keys (S re-streamed per piece).
+// Survivor runs of (q, s) -- one per probe item of q, written in place by k_probe -- are taken a
+// wave per run, several runs in flight per wave.
+constexpr int      kJoinThreads = 256;
+constexpr int      kJoinWaves   = kJoinThreads / 64;
+constexpr uint32_t kJoinBmLog2  = 18;                  // bitmap path: v < 2^18
+constexpr uint32_t kJoinWords   = 1u << (kJoinBmLog2 - 5);  // 8192 LDS words (32 KiB)
+constexpr uint32_t kJoinLog2T   = 13;                  // hash path: 8192 slots in the same words
+constexpr uint32_t kJoinT       = 1u << kJoinLog2T;
+constexpr uint32_t kJoinPiece   = kJoinT / 2;
+constexpr int      kJoinRB      = 16;                  // R codes per thread per batch
+constexpr int      kJoinRuns    = 4;                   // survivor runs in flight per wave
+constexpr uint32_t kJoinDesc    = kJoinThreads;        // run descriptors per batch
+constexpr uint32_t kEmpty       = 0xFFFFFFFFu;  // codes of one job share their low hash_shift >= 1
+                                                // bits, so (code >> hash_shift) never equals it
 
 __device__ __forceinline__ uint32_t join_slot(uint32_t v) {
     return (v * 0x9E3779B1u) >> (32 - kJoinLog2T);
 }
 
-__global__ __launch_bounds__(512) void k_join(JoinParams P) {
-    __shared__ uint32_t keys[kJoinT];
-    __shared__ uint64_t wsum[8];
-    const uint32_t job = blockIdx.x;
+__device__ __forceinline__ uint32_t join_count(const uint32_t* keys, uint32_t v) {
+    uint32_t h = join_slot(v), cnt = 0;
+    for (uint32_t k = keys[h]; k != kEmpty; k = keys[h]) {
+        cnt += k == v;
+        h = (h + 1u) & (kJoinT - 1u);
+    }
+    return cnt;
+}
+
+__device__ __forceinline__ void join_insert(uint32_t* keys, uint32_t v) {
+    uint32_t h = join_slot(v);
+    while (atomicCAS(&keys[h], kEmpty, v) != kEmpty) h = (h + 1u) & (kJoinT - 1u);
+}
+
+__global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
+    __shared__ __attribute__((aligned(16))) uint32_t tab[kJoinWords];  // bitmap or hash table
+    __shared__ uint64_t dbase[kJoinDesc];  // survivor run start (words) of each item in the batch
+    __shared__ uint32_t dcnt[kJoinDesc];
+    __shared__ uint64_t wsum[kJoinWaves];
+    __shared__ uint32_t dupflag;
+    const uint32_t NSUB = 1u << P.log2NSUB;
+    const uint32_t job  = blockIdx.x, q = job >> P.log2NSUB, s = job & (NSUB - 1u);
     const uint64_t r0 = P.r_off[job], r1 = P.r_off[job + 1];
-    const uint64_t s0 = P.s_off[job], s1 = P.s_off[job + 1];
-    if (r1 == r0 || s1 == s0) return;
+    const uint32_t i0 = P.item_start[q], i1 = P.item_start[q + 1];
+    if (r1 == r0 || i1 == i0) return;
+    const uint32_t lq0 = P.list_start[q];
+    const uint32_t npc = (i1 - i0) / P.nseg;  // probe pieces of q (items are segment-major)
     const uint32_t sh  = P.hash_shift;
+    const int      tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     uint64_t       cnt = 0;
-    for (uint64_t rb = r0; rb < r1; rb += kJoinPiece) {
-        const uint64_t re = min(r1, rb + kJoinPiece);
-        for (uint32_t i = threadIdx.x; i < kJoinT / 4; i += blockDim.x)
-            ((uint4*) keys)[i] = make_uint4(kEmpty, kEmpty, kEmpty, kEmpty);
-        __syncthreads();
-        for (uint64_t i0 = rb + threadIdx.x; i0 < re; i0 += (uint64_t) blockDim.x * kJoinB) {
-            uint32_t c[kJoinB];
-#pragma unroll
-            for (int j = 0; j < kJoinB; j++) {
-                const uint64_t i = i0 + (uint64_t) j * blockDim.x;
-                c[j]             = i < re ? P.r_codes[i] : 0u;
+    // counts the survivors of (q, s) against the table: bitmap (BM) or hash table
+    auto probe_runs = [&](bool BM) {
+        for (uint32_t d0 = i0; d0 < i1; d0 += kJoinDesc) {
+            const uint32_t nd = min(kJoinDesc, i1 - d0);
+            __syncthreads();  // previous descriptors consumed
+            if ((uint32_t) tid < nd) {
+                const uint32_t it    = d0 + tid;
+                const uint32_t local = it - i0;
+                const uint32_t seg   = local / npc;
+                const uint32_t piece = local - seg * npc;
+                dcnt[tid]  = P.surv_cnt[(uint64_t) it * NSUB + s];
+                dbase[tid] = (uint64_t) seg * P.surv_seg_stride + (uint64_t) (lq0 + piece * P.CH) * 32 +
+                             P.surv_off[(uint64_t) it * NSUB + s];
             }
+            __syncthreads();
+            for (uint32_t d = wave; d < nd; d += kJoinWaves * kJoinRuns) {
+                uint32_t v[kJoinRuns][2], n[kJoinRuns];
 #pragma unroll
-            for (int j = 0; j < kJoinB; j++) {
-                if (i0 + (uint64_t) j * blockDim.x >= re) continue;
-                const uint32_t v = c[j] >> sh;
-                uint32_t       h = join_slot(v);
-                while (atomicCAS(&keys[h], kEmpty, v) != kEmpty) h = (h + 1u) & (kJoinT - 1u);
-            }
-        }
-        __syncthreads();
-        for (uint64_t i0 = s0 + threadIdx.x; i0 < s1; i0 += (uint64_t) blockDim.x * kJoinB) {
-            uint32_t c[kJoinB];
+                for (int r = 0; r < kJoinRuns; r++) {
+                    const uint32_t dd = d + r * kJoinWaves;
+                    n[r]              = dd < nd ? dcnt[dd] : 0u;
+                    const uint64_t bb = dd < nd ? dbase[dd] : 0ull;
 #pragma unroll
-            for (int j = 0; j < kJoinB; j++) {
-                const uint64_t i = i0 + (uint64_t) j * blockDim.x;
-                c[j]             = i < s1 ? P.s_codes[i] : 0u;
-            }
+                    for (int j = 0; j < 2; j++) {
+                        const uint32_t o = lane + 64u * j;
+                        v[r][j]          = o < n[r] ? P.surv[bb + o] : 0u;
+                    }
+                }
 #pragma unroll
-            for (int j = 0; j < kJoinB; j++) {
-                if (i0 + (uint64_t) j * blockDim.x >= s1) continue;
-                const uint32_t v = c[j] >> sh;
-                uint32_t       h = join_slot(v);
-                for (uint32_t k = keys[h]; k != kEmpty; k = keys[h]) {
-                    cnt += k == v;
-                    h = (h + 1u) & (kJoinT - 1u);
+                for (int r = 0; r < kJoinRuns; r++) {
+#pragma unroll
+                    for (int j = 0; j < 2; j++) {
+                        if (lane + 64u * j >= n[r]) continue;
+                        const uint32_t x = v[r][j] >> sh;
+                        cnt += BM ? (tab[x >> 5] >> (x & 31u)) & 1u : join_count(tab, x);
+                    }
+                    if (n[r] > 128) {  // long run (e.g. no filter): tail
+                        const uint64_t bb = dbase[d + r * kJoinWaves];
+                        for (uint32_t o = 128 + lane; o < n[r]; o += 64) {
+                            const uint32_t x = P.surv[bb + o] >> sh;
+                            cnt += BM ? (tab[x >> 5] >> (x & 31u)) & 1u : join_count(tab, x);
+                        }
+                    }
                 }
             }
         }
+    };
+    bool hashed = !P.bitmap;
+    if (!hashed) {
+        for (uint32_t i = tid; i < kJoinWords / 4; i += kJoinThreads) ((uint4*) tab)[i] = make_uint4(0, 0, 0, 0);
+        if (tid == 0) dupflag = 0;
         __syncthreads();
+        uint32_t dup = 0;
+        for (uint64_t b = r0 + tid; b < r1; b += (uint64_t) kJoinThreads * kJoinRB) {
+            uint32_t c[kJoinRB];
+#pragma unroll
+            for (int j = 0; j < kJoinRB; j++) {
+                const uint64_t i = b + (uint64_t) j * kJoinThreads;
+                c[j]             = i < r1 ? P.r_codes[i] : 0u;
+            }
+#pragma unroll
+            for (int j = 0; j < kJoinRB; j++) {
+                if (b + (uint64_t) j * kJoinThreads >= r1) continue;
+                const uint32_t x = c[j] >> sh, bit = 1u << (x & 31u);
+                dup |= atomicOr(&tab[x >> 5], bit) & bit;
+            }
+        }
+        if (dup) dupflag = 1;
+        __syncthreads();
+        hashed = dupflag != 0;  // uniform
+        if (!hashed) probe_runs(true);
+    }
+    if (hashed) {  // duplicate R keys (or keys too wide for the bitmap): counting hash table
+        for (uint64_t rb = r0; rb < r1; rb += kJoinPiece) {
+            const uint64_t re = min(r1, rb + kJoinPiece);
+            __syncthreads();
+            for (uint32_t i = tid; i < kJoinT / 4; i += kJoinThreads)
+                ((uint4*) tab)[i] = make_uint4(kEmpty, kEmpty, kEmpty, kEmpty);
+            __syncthreads();
+            for (uint64_t i = rb + tid; i < re; i += kJoinThreads) join_insert(tab, P.r_codes[i] >> sh);
+            probe_runs(false);  // (starts with a barrier: the table is complete)
+        }
     }
     cnt = wave_sum_u64(cnt);
-    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = cnt;
+    if (lane == 0) wsum[wave] = cnt;
     __syncthreads();
-    if (threadIdx.x == 0) {
+    if (tid == 0) {
         uint64_t t = 0;
-        for (uint32_t w = 0; w < blockDim.x / 64; w++) t += wsum[w];
+        for (int w = 0; w < kJoinWaves; w++) t += wsum[w];
         if (t) atomicAdd((unsigned long long*) P.result, (unsigned long long) t);
     }
 }
@@ -1008,20 +1210,17 @@ void launch_scatter(const ScatterParams& p0, int src, uint32_t grid, hipStream_t
 }
 
 void launch_list_fill(const uint32_t* meta, const uint32_t* wg_used, uint64_t cap, uint32_t log2F,
-                      uint32_t* list_cursor, uint32_t* list, uint32_t grid, hipStream_t st) {
-    k_list_fill<<<grid, 1024, (2u << log2F) * sizeof(uint32_t), st>>>(meta, wg_used, cap, log2F,
-                                                                      list_cursor, list);
+                      const uint32_t* wgq_off, const uint32_t* list_start, uint32_t* list,
+                      uint32_t grid, hipStream_t st) {
+    k_list_fill<<<grid, 1024, (1u << log2F) * sizeof(uint32_t), st>>>(meta, wg_used, cap, log2F,
+                                                                      wgq_off, list_start, list);
 }
 
-void launch_plan(const uint32_t* part_chunks, const uint64_t* part_elems, uint32_t log2F,
-                 uint32_t CH, uint32_t nseg, uint32_t* list_start, uint32_t* list_cursor,
+void launch_plan(const uint32_t* wgq_chunks, const uint32_t* wgq_elems, uint32_t G, uint32_t log2F,
+                 uint32_t CH, uint32_t nseg, uint32_t* wgq_off, uint32_t* list_start,
                  uint64_t* elem_start, uint32_t* item_start, hipStream_t st) {
-    k_plan<<<1, 1024, 0, st>>>(part_chunks, part_elems, log2F, CH, nseg, list_start, list_cursor,
+    k_plan<<<1, 1024, 0, st>>>(wgq_chunks, wgq_elems, G, log2F, CH, nseg, wgq_off, list_start,
                                elem_start, item_start);
-}
-
-void launch_scan_u64(const uint64_t* in, uint64_t* out, uint32_t n, hipStream_t st) {
-    k_scan_u64<<<1, 1024, 0, st>>>(in, out, n);
 }
 
 size_t slice_lds_bytes(const Geometry& g) {
@@ -1044,7 +1243,20 @@ static void build_inst(const BuildParams& p, uint32_t F, size_t lds, hipStream_t
 template <int KIND>
 static void probe_inst(const ProbeParams& p, uint32_t grid, size_t lds, hipStream_t st) {
     (void) hipFuncSetAttribute((const void*) &k_probe<KIND>, hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds);
-    k_probe<KIND><<<grid, 1024, lds, st>>>(p);
+    const char* ab = getenv("HWBRJ_PR_ABLATE");  // dev-only timing knob; results invalid if set
+    const int   a  = ab ? atoi(ab) : 0;
+    if (KIND == KIND_BLOCK_PK1 && a == 1) {
+        (void) hipFuncSetAttribute((const void*) &k_probe<KIND, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds);
+        k_probe<KIND, 1><<<grid, 1024, lds, st>>>(p);
+    } else if (KIND == KIND_BLOCK_PK1 && a == 3) {
+        (void) hipFuncSetAttribute((const void*) &k_probe<KIND, 3>, hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds);
+        k_probe<KIND, 3><<<grid, 1024, lds, st>>>(p);
+    } else if (KIND == KIND_BLOCK_PK1 && a == 2) {
+        (void) hipFuncSetAttribute((const void*) &k_probe<KIND, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds);
+        k_probe<KIND, 2><<<grid, 1024, lds, st>>>(p);
+    } else {
+        k_probe<KIND><<<grid, 1024, lds, st>>>(p);
+    }
 }
 
 void launch_build(const BuildParams& p, uint32_t F, hipStream_t st) {
@@ -1057,8 +1269,18 @@ void launch_build(const BuildParams& p, uint32_t F, hipStream_t st) {
     }
 }
 
-void launch_probe(const ProbeParams& p, uint32_t grid, hipStream_t st) {
-    const size_t lds = slice_lds_bytes(p.g);
+// Probe LDS: slice segment + tables + a survivor stage using what is left of the CU's 160 KiB.
+size_t probe_lds_bytes(const Geometry& g, uint32_t* stage_cap) {
+    const bool   slices = g.mode == MODE_SLICE_BLOCK || g.mode == MODE_SLICE_BASIC;
+    const size_t base   = ((slices ? g.seg_words : 0) + 128 + 64 + 64 + 4) * sizeof(uint32_t);
+    size_t       cap    = std::min<size_t>(kProbeCH * 32, (163840 - base) / 4) & ~(size_t) 3;
+    if (stage_cap) *stage_cap = (uint32_t) cap;
+    return base + cap * 4;
+}
+
+void launch_probe(const ProbeParams& p0, uint32_t grid, hipStream_t st) {
+    ProbeParams p = p0;
+    const size_t lds = probe_lds_bytes(p.g, &p.stage_cap);
     switch (consumer_kind(p.g)) {
         case KIND_BLOCK_PK1: return probe_inst<KIND_BLOCK_PK1>(p, grid, lds, st);
         case KIND_BLOCK: return probe_inst<KIND_BLOCK>(p, grid, lds, st);
@@ -1067,17 +1289,10 @@ void launch_probe(const ProbeParams& p, uint32_t grid, hipStream_t st) {
     }
 }
 
-void launch_surv_totals(const uint32_t* item_start, const uint32_t* surv_cnt, uint32_t log2F,
-                        uint32_t log2NSUB, uint32_t* item_off, uint64_t* qs_tot, hipStream_t st) {
-    k_surv_totals<<<1u << log2F, 64, 0, st>>>(item_start, surv_cnt, log2NSUB, item_off, qs_tot);
-}
-
-void launch_surv_scatter(const SurvParams& p, uint32_t grid, hipStream_t st) {
-    k_surv_scatter<<<grid, 256, 0, st>>>(p);
-}
+uint32_t probe_chunks_per_item() { return kProbeCH; }
 
 void launch_join(const JoinParams& p, uint32_t jobs, hipStream_t st) {
-    k_join<<<jobs, 512, 0, st>>>(p);
+    k_join<<<jobs, kJoinThreads, 0, st>>>(p);
 }
 
 void launch_export(const uint32_t* slices, const Geometry& g, uint32_t* out, uint64_t nwords,
