@@ -554,37 +554,76 @@ __global__ __launch_bounds__(1024) void k_plan(const uint32_t* __restrict__ wgq_
 }
 
 // One block per scatter region: every chunk of the region gets its slot in its partition's list
-// (slot base = list_start[q] + wgq_off[wg][q], rank by an LDS counter). Eight meta loads per thread
-// are in flight per step.
-__global__ __launch_bounds__(1024) void k_list_fill(const uint32_t* __restrict__ meta,
-                                                    const uint32_t* __restrict__ wg_used,
-                                                    uint64_t cap, uint32_t log2F,
-                                                    const uint32_t* __restrict__ wgq_off,
-                                                    const uint32_t* __restrict__ list_start,
-                                                    uint32_t* __restrict__ list) {
+// (slots of (wg, q) start at list_start[q] + wgq_off[wg][q]). The region's metas are taken in
+// batches of kLfBatch, counting-sorted by partition in LDS and written out as contiguous runs per
+// partition, so the list stores are coalesced.
+constexpr uint32_t kLfThreads = 1024;
+constexpr uint32_t kLfPer     = 16;
+constexpr uint32_t kLfBatch   = kLfThreads * kLfPer;
+
+__global__ __launch_bounds__(kLfThreads) void k_list_fill(const uint32_t* __restrict__ meta,
+                                                          const uint32_t* __restrict__ wg_used,
+                                                          uint64_t cap, uint32_t log2F,
+                                                          const uint32_t* __restrict__ wgq_off,
+                                                          const uint32_t* __restrict__ list_start,
+                                                          uint32_t* __restrict__ list) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    const uint32_t F   = 1u << log2F;
-    uint32_t*      cur = lds;
-    const uint32_t wg  = blockIdx.x;
-    for (uint32_t q = threadIdx.x; q < F; q += blockDim.x) cur[q] = list_start[q] + wgq_off[wg * F + q];
+    const uint32_t F    = 1u << log2F;
+    uint32_t*      ids  = lds;                // [kLfBatch] sorted entries
+    uint16_t*      qs   = (uint16_t*) (ids + kLfBatch);  // [kLfBatch] their partitions
+    uint32_t*      cnt  = ids + kLfBatch + kLfBatch / 2;  // [F]
+    uint32_t*      off  = cnt + F;            // [F] batch offsets
+    uint32_t*      cur  = off + F;            // [F] next list slot
+    uint32_t*      wtot = cur + F;            // [16] wave totals of the scan
+    const uint32_t tid  = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t wg   = blockIdx.x;
+    for (uint32_t q = tid; q < F; q += kLfThreads) {
+        cur[q] = list_start[q] + wgq_off[wg * F + q];
+        cnt[q] = 0;
+    }
     __syncthreads();
     const uint64_t region = (uint64_t) wg * cap;
     const uint32_t used   = wg_used[wg];
-    constexpr int  U      = 8;
-    for (uint32_t i0 = threadIdx.x; i0 < used; i0 += blockDim.x * U) {
-        uint32_t m[U];
+    for (uint32_t b0 = 0; b0 < used; b0 += kLfBatch) {
+        const uint32_t nb = min(kLfBatch, used - b0);
+        uint32_t       m[kLfPer], rk[kLfPer];
 #pragma unroll
-        for (int j = 0; j < U; j++) {
-            const uint32_t i = i0 + j * blockDim.x;
+        for (int j = 0; j < (int) kLfPer; j++) {
+            const uint32_t i = b0 + tid + j * kLfThreads;
             m[j]             = i < used ? meta[region + i] : kNoEntry;
         }
 #pragma unroll
-        for (int j = 0; j < U; j++) {
+        for (int j = 0; j < (int) kLfPer; j++)
+            if (m[j] != kNoEntry) rk[j] = atomicAdd(&cnt[m[j] & 0xFFFFu], 1u);
+        __syncthreads();
+        // exclusive scan of cnt over F (<= 1024) partitions: one per thread, wave scans + totals
+        const uint32_t c    = tid < F ? cnt[tid] : 0u;
+        const uint32_t incl = wave_incl_scan(c);
+        if (lane == 63) wtot[wave] = incl;
+        __syncthreads();
+        uint32_t wbase = 0;
+        for (uint32_t w = 0; w < wave; w++) wbase += wtot[w];
+        if (tid < F) off[tid] = wbase + incl - c;
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < (int) kLfPer; j++) {
             if (m[j] == kNoEntry) continue;
             const uint32_t q   = m[j] & 0xFFFFu;
-            const uint32_t pos = atomicAdd(&cur[q], 1u);
-            list[pos] = (uint32_t) (region + i0 + j * blockDim.x) | (((m[j] >> 16) & 31u) << kListIdBits);
+            const uint32_t pos = off[q] + rk[j];
+            ids[pos] = (uint32_t) (region + b0 + tid + j * kLfThreads) | (((m[j] >> 16) & 31u) << kListIdBits);
+            qs[pos]  = (uint16_t) q;
         }
+        __syncthreads();
+        for (uint32_t pos = tid; pos < nb; pos += kLfThreads) {
+            const uint32_t q = qs[pos];
+            list[cur[q] + (pos - off[q])] = ids[pos];
+        }
+        __syncthreads();
+        if (tid < F) {
+            cur[tid] += cnt[tid];
+            cnt[tid] = 0;
+        }
+        __syncthreads();
     }
 }
 
@@ -1212,8 +1251,9 @@ void launch_scatter(const ScatterParams& p0, int src, uint32_t grid, hipStream_t
 void launch_list_fill(const uint32_t* meta, const uint32_t* wg_used, uint64_t cap, uint32_t log2F,
                       const uint32_t* wgq_off, const uint32_t* list_start, uint32_t* list,
                       uint32_t grid, hipStream_t st) {
-    k_list_fill<<<grid, 1024, (1u << log2F) * sizeof(uint32_t), st>>>(meta, wg_used, cap, log2F,
-                                                                      wgq_off, list_start, list);
+    const size_t lds = (kLfBatch + kLfBatch / 2 + 3 * (1u << log2F) + 16) * sizeof(uint32_t);
+    (void) hipFuncSetAttribute((const void*) &k_list_fill, hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds);
+    k_list_fill<<<grid, kLfThreads, lds, st>>>(meta, wg_used, cap, log2F, wgq_off, list_start, list);
 }
 
 void launch_plan(const uint32_t* wgq_chunks, const uint32_t* wgq_elems, uint32_t G, uint32_t log2F,
