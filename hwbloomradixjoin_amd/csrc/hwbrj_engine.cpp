@@ -358,7 +358,14 @@ int Engine::run(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     sp.wgq_chunks = wgqcS.as<uint32_t>();
     sp.wgq_elems  = wgqeS.as<uint32_t>();
     sp.cap        = capS;
+    const bool dbg_sc = getenv("HWBRJ_DBG") != nullptr;  // dev-only phase stamps
+    if (dbg_sc) {
+        ok &= dbgS.ensure((size_t) G * 64);
+        HWBRJ_CHECK(hipMemsetAsync(dbgS.p, 0, dbgS.bytes, stream));
+        sp.dbg = dbgS.as<uint64_t>();
+    }
     launch_scatter(sp, g.mode == MODE_GLOBAL ? SRC_CODES : SRC_TUPLES, G, stream);
+    sp.dbg = nullptr;
     HWBRJ_CHECK(hipEventRecord(ev_[4], stream));
     launch_plan(wgqcS.as<uint32_t>(), wgqeS.as<uint32_t>(), G, g.log2F, CH, nseg, wgqoS.as<uint32_t>(),
                 lstartS.as<uint32_t>(), estartS.as<uint64_t>(), istartS.as<uint32_t>(), stream);
@@ -421,6 +428,13 @@ int Engine::run(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
             for (int k = 0; k < 6; k++) sp_[k] += (double) hp[b * 8 + k] / PG;
         for (uint32_t b = 0; b < F; b++)
             for (int k = 0; k < 6; k++) sj[k] += (double) hj[b * 8 + k] / F;
+        std::vector<uint64_t> hs(G * 8);
+        HWBRJ_CHECK(hipMemcpy(hs.data(), dbgS.p, hs.size() * 8, hipMemcpyDeviceToHost));
+        double ss[6] = {0};
+        for (uint32_t b = 0; b < G; b++)
+            for (int k = 0; k < 6; k++) ss[k] += (double) hs[b * 8 + k] / G;
+        fprintf(stderr, "[dbg] S scatter cyc/WG: hash %.0f load+flush %.0f rank %.0f b1 %.0f write+plan %.0f b2 %.0f\n",
+                ss[0], ss[1], ss[2], ss[3], ss[4], ss[5]);
         fprintf(stderr, "[dbg] probe cyc/WG: top %.0f test %.0f b1 %.0f scan+b2 %.0f write %.0f b3+copy %.0f\n",
                 sp_[0], sp_[1], sp_[2], sp_[3], sp_[4], sp_[5]);
     }

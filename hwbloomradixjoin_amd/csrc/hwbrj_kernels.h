@@ -21,10 +21,10 @@ struct ScatterParams {
     uint32_t*        wg_used;      // [G] chunks used by each workgroup
     uint32_t*        wgq_chunks;   // [G][F] chunks of partition q in workgroup wg's region
     uint32_t*        wgq_elems;    // [G][F] elements of partition q in workgroup wg's region
+    uint64_t*        dbg;          // dev-only: per-workgroup phase cycles (HWBRJ_DBG), or nullptr
     uint64_t         cap;          // chunk capacity of one workgroup region
     Geometry         g;
     const CrcTables* tabs;
-    uint32_t         ablate;       // dev-only timing ablation (HWBRJ_SC_ABLATE); results invalid if != 0
 };
 
 struct BuildParams {

@@ -41,6 +41,17 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
     return v;
 }
 
+// Inclusive wave64 prefix sum on the VALU (DPP row shifts + row broadcasts; no LDS traffic).
+__device__ __forceinline__ uint32_t wave_incl_scan_dpp(uint32_t v) {
+    v += (uint32_t) __builtin_amdgcn_update_dpp(0, (int) v, 0x111, 0xf, 0xf, false);  // row_shr:1
+    v += (uint32_t) __builtin_amdgcn_update_dpp(0, (int) v, 0x112, 0xf, 0xf, false);  // row_shr:2
+    v += (uint32_t) __builtin_amdgcn_update_dpp(0, (int) v, 0x114, 0xf, 0xf, false);  // row_shr:4
+    v += (uint32_t) __builtin_amdgcn_update_dpp(0, (int) v, 0x118, 0xf, 0xf, false);  // row_shr:8
+    v += (uint32_t) __builtin_amdgcn_update_dpp(0, (int) v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    v += (uint32_t) __builtin_amdgcn_update_dpp(0, (int) v, 0x143, 0xc, 0xf, false);  // row_bcast:31
+    return v;
+}
+
 __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
@@ -239,14 +250,26 @@ __global__ __launch_bounds__(1024) void k_probe_global(const uint2* S, uint64_t 
 }
 
 // ================================================================= K3: SWWC partitioning
-// One workgroup per CU (the 128 KiB stage fills the LDS). Each round a workgroup takes 4096
-// elements; element e of partition q goes to stage slot fill[q]++. A partition whose stage reaches
-// 32 elements is flushed as one 128-byte chunk into the workgroup's private chunk region (no
-// cross-workgroup coordination); a round that overfills a partition (skew) writes its extra whole
-// chunks directly. Chunk metadata = partition | count << 16.
+// One workgroup per CU (the 128 KiB stage fills the LDS), private contiguous chunk region per
+// workgroup (no cross-workgroup coordination). A round takes kScRound elements (8 per thread):
+//   A  hash the round's words (loaded two rounds ahead), copy out the stage lines planned in the
+//      previous round (a fixed number of buffer stores per thread), rank every word in its
+//      partition's stage (ds_add_rtn on fill[q]);
+//   B1 (barrier) B  write the previous round's overflow words and this round's in-stage words;
+//      one thread per partition plans the flush of every stage that reached 32 words;
+//   B2 (barrier).
+// A plan turns floor(fill/32) chunks into consecutive chunk ids: the first is the stage
+// line, further ones (only when a round overfills a partition by > 32, i.e. skew) are written
+// directly by the threads holding those overflow words. Chunk metadata = partition | count << 16.
+// (Reference pass-1: src/parallel_radix_join_bloom.c:758-852, SWWC variant :611-700.)
 constexpr int      kScThreads = 1024;
+constexpr int      kScPre     = 1;                        // rounds of loads in flight (1 or 2)
+constexpr int      kScE       = 8;                        // elements per thread per round
+constexpr uint32_t kScRound   = kScThreads * kScE;        // elements per workgroup round
+constexpr int      kScK       = 3;                        // flush tasks per thread per round (fixed)
 constexpr uint32_t kCbBits    = 22;                       // ncb: chunk base | nchunks << 22
 constexpr uint32_t kCbMask    = (1u << kCbBits) - 1u;
+constexpr uint32_t kOob       = 0x7FFFFFF0u;              // buffer offset that is always dropped
 
 template <int SRC, int MODE, int FMT>
 __device__ __forceinline__ void sc_word(uint32_t x, const Geometry& g, const uint32_t* fwd,
@@ -271,208 +294,230 @@ __device__ __forceinline__ void sc_word(uint32_t x, const Geometry& g, const uin
     }
 }
 
-template <int SRC, int MODE, int FMT, int kScE>
-__global__ __launch_bounds__(kScThreads) void k_scatter(ScatterParams P) {
-    constexpr uint32_t kScRound = kScThreads * kScE;  // elements per workgroup round
-    constexpr uint32_t kNone    = 0xFFFFFFFFu;        // no pending word
-    constexpr uint32_t kDirect  = 0x80000000u;        // pending word goes to the pool, not the stage
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    const uint32_t F     = 1u << P.g.log2F;
-    uint32_t*      stage = lds;            // F * 32
-    uint32_t*      fill  = stage + F * 32; // F: words in the stage (incl. pending ones)
-    uint32_t*      ncb   = fill + F;       // F: chunk base | nchunks << kCbBits (this round)
-    uint32_t*      tch   = ncb + F;        // F: chunks of q (this workgroup)
-    uint32_t*      tel   = tch + F;        // F: elements of q (this workgroup)
-    uint32_t*      flq   = tel + F;        // F: flush queue
-    uint32_t*      fwd   = flq + F;        // 128
-    uint32_t*      misc  = fwd + 128;      // [0],[1] flush counts by round parity, [2] chunks used
+template <int SRC>
+struct ScRaw {  // one round's raw loads of this thread (tuples: keys only; codes: 4 per uint4)
+    uint32_t k[SRC == SRC_TUPLES ? kScE : 1];
+    uint4    v[SRC == SRC_TUPLES ? 1 : kScE / 4];
+};
 
-    const int tid = threadIdx.x;
+template <int SRC, int MODE, int FMT>
+__global__ __launch_bounds__(kScThreads) void k_scatter(ScatterParams P) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    constexpr int NL = SRC == SRC_TUPLES ? kScE / 2 : kScE / 4;  // uint4 loads per thread per round
+    const uint32_t F     = 1u << P.g.log2F;
+    uint32_t*      stage = lds;             // F * 32
+    uint32_t*      fill  = stage + F * 32;  // F + 1 (entry F: invalid elements)
+    uint32_t*      ncb   = fill + F + 4;    // 2 x F: plan by round parity (chunk base | nchunks << 22)
+    uint32_t*      tch   = ncb + 2 * F;     // F: chunks of q (this workgroup)
+    uint32_t*      tel   = tch + F;         // F: elements of q (this workgroup)
+    uint32_t*      flq   = tel + F;         // F: partitions flushed by the last plan
+    uint32_t*      fwd   = flq + F;         // 128: CRC nibble table
+    uint32_t*      misc  = fwd + 128;       // [0] chunks used, [1 + parity] flushes of a round's plan
+    const int      tid   = threadIdx.x;
+    for (uint32_t i = tid; i < F + 1; i += kScThreads) fill[i] = 0;
     for (uint32_t i = tid; i < F; i += kScThreads) {
-        fill[i] = 0;
-        tch[i]  = 0;
-        tel[i]  = 0;
+        tch[i] = 0;
+        tel[i] = 0;
     }
     load_tab(fwd, &P.tabs->fwd[0][0]);
     if (tid < 4) misc[tid] = 0;
-    __syncthreads();
 
     const uint64_t n     = P.n_dev ? *P.n_dev : P.n;
     const uint64_t units = (n + 3) >> 2;
-    const uint64_t G     = gridDim.x, wg = blockIdx.x;
-    const uint64_t e0    = 4 * (wg * units / G);
-    const uint64_t e1r   = 4 * ((wg + 1) * units / G);
-    const uint64_t e1    = e1r < n ? e1r : n;
-    const uint32_t len   = e1 > e0 ? (uint32_t) (e1 - e0) : 0u;  // < 2^32 per workgroup
+    const uint64_t G = gridDim.x, wg = blockIdx.x;
+    const uint64_t e0  = 4 * (wg * units / G);
+    const uint64_t e1r = 4 * ((wg + 1) * units / G);
+    const uint64_t e1  = e1r < n ? e1r : n;
+    const uint32_t len = __builtin_amdgcn_readfirstlane(e1 > e0 ? (uint32_t) (e1 - e0) : 0u);
     uint32_t* __restrict__ pool = P.pool + wg * P.cap * 32;
     uint32_t* __restrict__ meta = P.meta + wg * P.cap;
+    constexpr uint32_t EB = SRC == SRC_TUPLES ? 8u : 4u;  // bytes per element
+    const auto rsrc = buf_rsrc((const uint8_t*) P.src + e0 * EB, len * EB);  // OOB loads return 0
+    const auto rpool = buf_rsrc(pool, (uint32_t) (P.cap * 128));
+    const auto rmeta = buf_rsrc(meta, (uint32_t) (P.cap * 4));
+    __syncthreads();
 
-    // Raw round data is prefetched one round ahead so the loads overlap the LDS phases below.
-    constexpr int      NR      = (SRC == SRC_TUPLES) ? kScE / 2 : kScE / 4;  // uint4 per round
-    constexpr uint32_t RSTRIDE = (SRC == SRC_TUPLES) ? 2 * kScThreads : 4 * kScThreads;
-    const uint2*    tsrc = (const uint2*) P.src + e0;
-    const uint32_t* csrc = (const uint32_t*) P.src + e0;
-    uint4 pre[NR];
-    auto fetch = [&](uint32_t base) {
+    auto load_round = [&](uint32_t base, ScRaw<SRC>& R) {
+        if (SRC == SRC_TUPLES) {  // keys only (the payload is not needed by the count join)
 #pragma unroll
-        for (int h = 0; h < NR; h++) {
-            if (SRC == SRC_TUPLES) {
-                const uint32_t i = base + (uint32_t) h * RSTRIDE + 2 * tid;
-                if (i + 1 < len) pre[h] = *(const uint4*) (tsrc + i);
-                else if (i < len) pre[h] = make_uint4(tsrc[i].x, 0, 0, 0);
-            } else {
-                const uint32_t i = base + (uint32_t) h * RSTRIDE + 4 * tid;
-                if (i + 3 < len) {
-                    pre[h] = *(const uint4*) (csrc + i);
-                } else {
-                    pre[h].x = i < len ? csrc[i] : 0u;
-                    pre[h].y = i + 1 < len ? csrc[i + 1] : 0u;
-                    pre[h].z = i + 2 < len ? csrc[i + 2] : 0u;
-                    pre[h].w = 0u;
-                }
+            for (int j = 0; j < kScE; j++) {
+                const uint32_t i = base + j * kScThreads + tid;
+                R.k[j] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, i < len ? i * EB : kOob, 0, 0);
+            }
+        } else {
+#pragma unroll
+            for (int h = 0; h < NL; h++) {
+                const uint32_t i = base + h * (4 * kScThreads) + 4 * tid;
+                const v4u x = __builtin_amdgcn_raw_buffer_load_b128(rsrc, i < len ? i * EB : kOob, 0, 0);
+                R.v[h]      = make_uint4(x.x, x.y, x.z, x.w);
             }
         }
     };
-    uint32_t pend[kScE], pendw[kScE];  // overflow words of the previous round
-#pragma unroll
-    for (int j = 0; j < kScE; j++) pend[j] = kNone;
-    uint32_t wv[kScE], q[kScE], e[kScE];
-    bool     v[kScE];
-#pragma unroll
-    for (int j = 0; j < kScE; j++) v[j] = false;
-    // Overflow words of the previous round are parked in registers (read ncb before it changes).
-    auto capture_pending = [&]() {
-#pragma unroll
-        for (int j = 0; j < kScE; j++) {
-            pend[j] = kNone;
-            if (v[j] && e[j] >= 32) {  // whole extra chunks go to the pool, the rest start the stage
-                const uint32_t qq = q[j], ch = e[j] >> 5, sl = e[j] & 31u;
-                const uint32_t cb = ncb[qq];
-                pend[j]  = ch < (cb >> kCbBits) ? (kDirect | (((cb & kCbMask) + ch) * 32 + sl))
-                                                : qq * 32 + sl;
-                pendw[j] = wv[j];
-            }
+    // element j of this thread in the round at `base`, and its index inside the workgroup's slice
+    auto elem = [&](const ScRaw<SRC>& R, uint32_t base, int j, uint32_t& x, uint32_t& idx) {
+        if (SRC == SRC_TUPLES) {
+            x   = R.k[j];
+            idx = base + j * kScThreads + tid;
+        } else {
+            const int h = j >> 2, t = j & 3;
+            x   = t == 0 ? R.v[h].x : t == 1 ? R.v[h].y : t == 2 ? R.v[h].z : R.v[h].w;
+            idx = base + h * (4 * kScThreads) + 4 * tid + t;
         }
     };
-    // D: flush every full stage of the previous round as one 128-byte line (8 lanes x 16 B).
-    // Issued after this round's prefetched words are consumed and before the next prefetch, so the
-    // stores are acknowledged during the round's compute (vmcnt also counts stores on CDNA).
-    auto flush_prev = [&](uint32_t pp) {
-        const uint32_t nfl = misc[pp];
-        for (uint32_t i = tid >> 3; i < nfl; i += kScThreads / 8) {
-            const uint32_t qq = flq[i];
-            const uint32_t l8 = tid & 7;
-            const uint32_t cb = ncb[qq];
-            const uint4    vv = *(const uint4*) &stage[qq * 32 + l8 * 4];
-            if (P.ablate & 2u) {
-                asm volatile("" ::"v"(vv.x), "v"(vv.y), "v"(vv.z), "v"(vv.w));
-            } else {
-                *(uint4*) &pool[(cb & kCbMask) * 32 + l8 * 4] = vv;
-                if (!(P.ablate & 1u))  // metas of this flush's chunks
-                    for (uint32_t c = l8; c < (cb >> kCbBits); c += 8)
-                        meta[(cb & kCbMask) + c] = qq | (32u << 16);
-            }
-        }
+    // Copy out the stage lines of the last plan: task k = (flush entry k >> 3, 16-byte lane k & 7).
+    uint32_t par = 0;  // round parity: misc[1 + par] counts this round's plan
+    auto flush_copy = [&]() {
+        const uint32_t nf = misc[1 + (par ^ 1u)];  // plan of the previous round
+        auto task = [&](uint32_t k) {
+            const bool     ok = k < nf * 8;
+            const uint32_t qq = flq[ok ? k >> 3 : 0];
+            const uint32_t l8 = k & 7;
+            const uint32_t cb = ncb[(par ^ 1u) * F + qq] & kCbMask;
+            const v4u      v  = *(const v4u*) &stage[qq * 32 + l8 * 4];
+            __builtin_amdgcn_raw_buffer_store_b128(v, rpool, ok ? (cb * 32 + l8 * 4) * 4 : kOob, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(qq | (32u << 16), rmeta, ok && l8 == 0 ? cb * 4 : kOob, 0, 0);
+        };
+#pragma unroll
+        for (int i = 0; i < kScK; i++) task(tid + i * kScThreads);
+        for (uint32_t k = kScK * kScThreads + tid; k < nf * 8; k += kScThreads) task(k);  // rare
     };
-    if (len) fetch(0);
-    uint32_t par = 0;  // round parity (selects the flush counter)
-    for (uint32_t base = 0; base < len; base += kScRound, par ^= 1u) {
-        capture_pending();
-        uint32_t x[kScE];
-#pragma unroll
-        for (int h = 0; h < NR; h++) {
-            if (SRC == SRC_TUPLES) {
-                const uint32_t i = base + (uint32_t) h * RSTRIDE + 2 * tid;
-                x[2 * h]         = pre[h].x;
-                x[2 * h + 1]     = pre[h].z;
-                v[2 * h]         = i < len;
-                v[2 * h + 1]     = i + 1 < len;
-            } else {
-                const uint32_t i = base + (uint32_t) h * RSTRIDE + 4 * tid;
-                x[4 * h]         = pre[h].x;
-                x[4 * h + 1]     = pre[h].y;
-                x[4 * h + 2]     = pre[h].z;
-                x[4 * h + 3]     = pre[h].w;
-#pragma unroll
-                for (int j = 0; j < 4; j++) v[4 * h + j] = i + j < len;
-            }
+
+    uint64_t tph[6] = {0, 0, 0, 0, 0, 0}, tlast = __builtin_amdgcn_s_memtime();
+    (void) tlast;
+    auto stamp = [&](int k) {  // dev-only phase stamps (build with -DHWBRJ_STAMPS, run with HWBRJ_DBG)
+#ifdef HWBRJ_STAMPS
+        if (P.dbg) {
+            const uint64_t t = __builtin_amdgcn_s_memtime();
+            tph[k] += t - tlast;
+            tlast = t;
         }
-        // ---- A1: hash this round's words (consumes the prefetched registers)
+#else
+        (void) k;
+#endif
+    };
+    ScRaw<SRC> RA, RB;
+    load_round(0, RA);
+    if (kScPre == 2) load_round(kScRound, RB);
+    // overflow words of the previous round: partition | slot << 11 (kNoPend: none), word
+    constexpr uint32_t kNoPend = 0xFFFFFFFFu;
+    uint32_t pq[kScE], pw[kScE];
+#pragma unroll
+    for (int j = 0; j < kScE; j++) pq[j] = kNoPend;
+
+    auto round = [&](uint32_t base, ScRaw<SRC>& R) {
+        // ---- A: hash (consumes R), refill R two rounds ahead, copy out the last plan, rank
+        uint32_t q[kScE], w[kScE];
 #pragma unroll
         for (int j = 0; j < kScE; j++) {
-            if (P.ablate & 4u) {
-                wv[j] = x[j];
-                q[j]  = x[j] & (F - 1u);
-            } else {
-                sc_word<SRC, MODE, FMT>(x[j], P.g, fwd, wv[j], q[j]);
+            uint32_t x, idx;
+            elem(R, base, j, x, idx);
+            sc_word<SRC, MODE, FMT>(x, P.g, fwd, w[j], q[j]);
+            if (idx >= len) q[j] = F;  // invalid: ranked on the dummy counter
+            if ((j & 1) == 1) __builtin_amdgcn_sched_barrier(0);  // bound the CRC reads in flight
+        }
+        stamp(0);
+        load_round(base + kScPre * kScRound, R);
+        flush_copy();
+        if (tid == 0) misc[1 + par] = 0;  // (last read by the previous round's flush_copy)
+        stamp(1);
+#pragma unroll
+        for (int j = 0; j < kScE; j++) q[j] |= atomicAdd(&fill[q[j]], 1u) << 11;  // q | slot << 11
+        stamp(2);
+        __syncthreads();  // B1: last plan copied out; every rank of this round taken
+        stamp(3);
+        // ---- B: overflow words of the previous round, in-stage words of this round, plan
+#pragma unroll
+        for (int j = 0; j < kScE; j++) {  // (plan of the previous round: ncb[par ^ 1])
+            if (pq[j] != kNoPend) {
+                const uint32_t qq = pq[j] & 2047u, sl = pq[j] >> 11;
+                const uint32_t cb = ncb[(par ^ 1u) * F + qq], nch = cb >> kCbBits;
+                if (sl >= nch * 32) stage[qq * 32 + sl - nch * 32] = pw[j];
+                else pool[((cb & kCbMask) + (sl >> 5)) * 32 + (sl & 31u)] = pw[j];  // skew only
             }
         }
-        flush_prev(par ^ 1u);
-        if (base + kScRound < len) fetch(base + kScRound);
-        // ---- A2: rank every word in its partition's stage
 #pragma unroll
         for (int j = 0; j < kScE; j++) {
-            if (P.ablate & 8u) {
-                e[j] = 0;
-                asm volatile("" ::"v"(wv[j]), "v"(q[j]));
-                v[j] = false;
-            } else {
-                e[j] = v[j] ? atomicAdd(&fill[q[j]], 1u) : 0u;
+            const uint32_t qq = q[j] & 2047u, sl = q[j] >> 11;
+            const bool     ok = qq < F;
+            if (ok && sl < 32) stage[qq * 32 + sl] = w[j];
+            pq[j] = ok && sl >= 32 ? q[j] : kNoPend;
+            pw[j] = w[j];
+        }
+        {
+            // one thread per partition (F <= 1024): flush plan
+            const uint32_t qq  = tid;
+            const uint32_t f   = qq < F ? fill[qq] : 0u;
+            const uint32_t nch = f >> 5;
+            // wave prefix of (chunks, flushes); one LDS atomic per wave for the bases
+            const uint32_t v    = nch | (nch ? (1u << 16) : 0u);
+            const uint32_t incl = wave_incl_scan_dpp(v);
+            const uint32_t tot  = __builtin_amdgcn_readlane(incl, 63);
+            uint32_t       wbc = 0, wbf = 0;
+            if ((tid & 63) == 0 && tot) {
+                wbc = atomicAdd(&misc[0], tot & 0xFFFFu);
+                wbf = atomicAdd(&misc[1 + par], tot >> 16);
+            }
+            wbc = __builtin_amdgcn_readfirstlane(wbc);
+            wbf = __builtin_amdgcn_readfirstlane(wbf);
+            if (nch) {
+                const uint32_t cb = wbc + (incl & 0xFFFFu) - nch;  // region-local chunk
+                ncb[par * F + qq] = cb | (nch << kCbBits);
+                flq[wbf + (incl >> 16) - 1] = qq;
+                fill[qq]          = f & 31u;
+                tch[qq] += nch;
+                tel[qq] += nch * 32;
+                for (uint32_t c = 1; c < nch; c++) meta[cb + c] = qq | (32u << 16);  // direct chunks
+            }
+        }
+        stamp(4);
+        __syncthreads();  // B2: plan visible
+        stamp(5);
+        par ^= 1u;
+    };
+    uint32_t base = 0;
+    if (kScPre == 2) {
+        for (; base + kScRound < len; base += 2 * kScRound) {
+            round(base, RA);
+            round(base + kScRound, RB);
+        }
+        if (base < len) round(base, RA);
+    } else {
+        for (; base < len; base += kScRound) round(base, RA);
+    }
+    // ---- tail: last plan, the last overflow words, then every partial stage as a partial chunk
+    {
+        flush_copy();
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < kScE; j++) {
+            if (pq[j] != kNoPend) {
+                const uint32_t qq = pq[j] & 2047u, sl = pq[j] >> 11;
+                const uint32_t cb = ncb[(par ^ 1u) * F + qq], nch = cb >> kCbBits;
+                if (sl >= nch * 32) stage[qq * 32 + sl - nch * 32] = pw[j];
+                else pool[((cb & kCbMask) + (sl >> 5)) * 32 + (sl & 31u)] = pw[j];
             }
         }
         __syncthreads();
-        // ---- B: previous round's overflow words, this round's in-stage words; C: flush plan
-        if (tid == 0) misc[par ^ 1u] = 0;
-#pragma unroll
-        for (int j = 0; j < kScE; j++) {
-            if (pend[j] != kNone) {
-                if (pend[j] & kDirect) pool[pend[j] & ~kDirect] = pendw[j];
-                else stage[pend[j]] = pendw[j];
-            }
-            if (v[j] && e[j] < 32) stage[q[j] * 32 + e[j]] = wv[j];
-        }
         for (uint32_t qq = tid; qq < F; qq += kScThreads) {
             const uint32_t f = fill[qq];
-            if (f >= 32) {
-                const uint32_t c  = f >> 5;
-                const uint32_t cb = atomicAdd(&misc[2], c);
-                ncb[qq]           = cb | (c << kCbBits);
-                tch[qq] += c;
-                tel[qq] += c * 32;
-                fill[qq]          = f & 31u;
-                flq[atomicAdd(&misc[par], 1u)] = qq;
+            if (f > 0) {
+                const uint32_t cb = atomicAdd(&misc[0], 1u);
+                meta[cb]          = qq | (f << 16);
+                for (uint32_t s2 = 0; s2 < f; s2++) pool[cb * 32 + s2] = stage[qq * 32 + s2];
+                tch[qq] += 1;
+                tel[qq] += f;
             }
         }
         __syncthreads();
-    }
-    capture_pending();
-    flush_prev(par ^ 1u);
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < kScE; j++) {
-        if (pend[j] != kNone) {
-            if (pend[j] & kDirect) pool[pend[j] & ~kDirect] = pendw[j];
-            else stage[pend[j]] = pendw[j];
+        if (tid == 0) P.wg_used[wg] = misc[0];
+        if (P.dbg && tid == 0)
+            for (int k = 0; k < 6; k++) P.dbg[wg * 8 + k] = tph[k];
+        // this workgroup's row of the (workgroup x partition) chunk / element matrices (k_plan
+        // scans them column-wise: no global atomics)
+        for (uint32_t qq = tid; qq < F; qq += kScThreads) {
+            P.wgq_chunks[wg * F + qq] = tch[qq];
+            P.wgq_elems[wg * F + qq]  = tel[qq];
         }
-    }
-    __syncthreads();
-    for (uint32_t qq = tid; qq < F; qq += kScThreads) {
-        const uint32_t f = fill[qq];
-        if (f > 0) {
-            const uint32_t cb = atomicAdd(&misc[2], 1u);
-            meta[cb]          = qq | (f << 16);
-            for (uint32_t s2 = 0; s2 < f; s2++) pool[cb * 32 + s2] = stage[qq * 32 + s2];
-            tch[qq] += 1;
-            tel[qq] += f;
-        }
-    }
-    __syncthreads();
-    if (tid == 0) P.wg_used[wg] = misc[2];
-    // this workgroup's row of the (workgroup x partition) chunk / element matrices (k_plan scans
-    // them column-wise: no global atomics)
-    for (uint32_t qq = tid; qq < F; qq += kScThreads) {
-        P.wgq_chunks[wg * F + qq] = tch[qq];
-        P.wgq_elems[wg * F + qq]  = tel[qq];
     }
 }
 
@@ -1209,32 +1254,18 @@ void launch_probe_global(const uint2* S, uint64_t n, const Geometry& g, const Cr
 
 size_t scatter_lds_bytes(uint32_t log2F) {
     const size_t F = 1u << log2F;
-    return (F * 32 + F * 5 + 128 + 4) * sizeof(uint32_t);  // stage, 5 arrays, table, misc
-}
-
-static int scatter_elems() {  // dev knob for A/B runs: HWBRJ_SCE=4|8 elements per thread/round
-    const char* v = getenv("HWBRJ_SCE");
-    return (v && atoi(v) == 8) ? 8 : 4;
+    return (F * 32 + F + 4 + 5 * F + 128 + 4) * sizeof(uint32_t);  // stage, fill, ncb x2, 3 arrays, table, misc
 }
 
 template <int SRC, int MODE, int FMT>
 static void scatter_inst(const ScatterParams& p, uint32_t grid, hipStream_t st) {
     const size_t lds = scatter_lds_bytes(p.g.log2F);
-    if (scatter_elems() == 8) {
-        (void) hipFuncSetAttribute((const void*) &k_scatter<SRC, MODE, FMT, 8>,
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds);
-        k_scatter<SRC, MODE, FMT, 8><<<grid, kScThreads, lds, st>>>(p);
-    } else {
-        (void) hipFuncSetAttribute((const void*) &k_scatter<SRC, MODE, FMT, 4>,
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds);
-        k_scatter<SRC, MODE, FMT, 4><<<grid, kScThreads, lds, st>>>(p);
-    }
+    (void) hipFuncSetAttribute((const void*) &k_scatter<SRC, MODE, FMT>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds);
+    k_scatter<SRC, MODE, FMT><<<grid, kScThreads, lds, st>>>(p);
 }
 
-void launch_scatter(const ScatterParams& p0, int src, uint32_t grid, hipStream_t st) {
-    ScatterParams p = p0;
-    const char*   ab = getenv("HWBRJ_SC_ABLATE");
-    p.ablate         = ab ? (uint32_t) atoi(ab) : 0u;
+void launch_scatter(const ScatterParams& p, int src, uint32_t grid, hipStream_t st) {
     const Geometry& g = p.g;
     if (src == SRC_CODES) return scatter_inst<SRC_CODES, MODE_GLOBAL, FMT_CODE>(p, grid, st);
     switch (g.mode) {
