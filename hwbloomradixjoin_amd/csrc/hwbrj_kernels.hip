@@ -831,8 +831,10 @@ __global__ __launch_bounds__(1024) void k_build(BuildParams P) {
 // item's list entries and chunks are loaded while the current one is tested. Survivors are
 // written into the item's own region grouped by join sub-partition (LDS counters + one scan), so
 // the join reads them in place: surv_cnt[it][sub] / surv_off[it][sub] describe the runs.
-constexpr int      kPC      = 4;              // chunk quads per thread per item
+constexpr int      kPC      = 3;              // chunk quads per thread per item
 constexpr uint32_t kProbeCH = 128u * kPC;     // chunks per probe item (1024 threads, 8 per chunk)
+constexpr uint32_t kScrCap  = 128;            // compacted survivors per wave and item (LDS scratch)
+constexpr int      kDense   = kScrCap / 64;   // dense ranking rounds per wave
 
 __device__ __forceinline__ uint32_t find_q(const uint32_t* item_start, uint32_t F, uint32_t it) {
     uint32_t lo = 0, hi = F - 1;
@@ -847,7 +849,7 @@ __device__ __forceinline__ uint32_t find_q(const uint32_t* item_start, uint32_t 
 // covers list positions [lq0 + p * CH, min(lq1, lq0 + (p + 1) * CH)). Survivors of an item are
 // written at seg * surv_seg_stride + lb * 32 (lb = first list position of the piece).
 
-template <int KIND, int ABL = 0>  // ABL: dev-only ablations (1 no ranks/writes, 2 nothing passes)
+template <int KIND, bool SEG1>
 __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     constexpr uint32_t NT  = 1024;
@@ -858,20 +860,22 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
     constexpr bool  onebit = KIND == KIND_BLOCK_PK1 || KIND == KIND_BASIC_K1;
     constexpr int   NW     = kPC * 4;   // words per thread per item
     const uint32_t  segw   = slices ? g.seg_words : 0;  // multiple of 4
+    const uint32_t  scap   = P.stage_cap;               // survivor words per stage buffer
+    const uint32_t  sstr   = scap + 64;                 // stage buffer stride (64 dummy slots)
     uint32_t*       slice  = lds;
     uint32_t*       inv    = slice + segw;
-    uint32_t*       subc   = inv + 128;  // NSUB counters of the current item
-    uint32_t*       subo   = subc + 64;  // NSUB run offsets of the current item
-    uint32_t*       misc   = subo + 64;  // [0] survivors of the current item
-    uint32_t*       stage  = misc + 4;   // survivors of the current item, by sub (stage_cap words)
-    const int       tid    = threadIdx.x;
+    uint32_t*       subc   = inv + 128;       // 3 x 128: per-sub counters (+64 dummies), by item
+    uint32_t*       subow  = subc + 3 * 128;  // 16 waves x NSUB: each wave's copy of the offsets
+    uint32_t*       scratch = subow + 16 * NSUB;  // 16 waves x (kScrCap + 64): compacted survivors
+    uint32_t*       stage  = scratch + 16 * (kScrCap + 64);  // 2 x sstr, double-buffered by item
+    const int       tid    = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     load_tab(inv, &P.tabs->inv[0][0]);
-    for (uint32_t i = tid; i < 64; i += NT) subc[i] = 0;
+    for (uint32_t i = tid; i < 3 * 128; i += NT) subc[i] = 0;
     const uint32_t I    = P.item_start[F];
     // uniform values computed on the VALU are pinned to SGPRs (readfirstlane)
     const uint32_t it0  = __builtin_amdgcn_readfirstlane((uint32_t) ((uint64_t) blockIdx.x * I / gridDim.x));
     const uint32_t it1  = __builtin_amdgcn_readfirstlane((uint32_t) ((uint64_t) (blockIdx.x + 1) * I / gridDim.x));
-    const uint32_t nseg = slices ? g.nseg : 1;
+    const uint32_t nseg = SEG1 || !slices ? 1u : g.nseg;
     uint64_t tph[6] = {0, 0, 0, 0, 0, 0}, tlast = __builtin_amdgcn_s_memtime();
     (void) tlast;
     auto stamp = [&](int k) {  // dev-only phase stamps (build with -DHWBRJ_STAMPS, run with HWBRJ_DBG)
@@ -885,32 +889,35 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
         (void) k;
 #endif
     };
-    // Copy-out of the previous item's staged survivors and its run table. A fixed number of
-    // buffer stores whatever the counts (out-of-range ones are dropped): issued right after the
-    // next loads, so the compiler never has to wait for them (vmcnt counts stores on gfx9).
-    constexpr uint32_t kNoItem = 0x80000000u;  // copy_out has nothing to write
-    uint32_t  prev_total = 0, prev_it = kNoItem, subc_v = 0, subo_v = 0;
+    // Copy-out of the previous item's staged survivors and its run table: a fixed number of
+    // buffer stores whatever the counts (out-of-range ones are dropped), so the compiler never has
+    // to wait for them (vmcnt counts stores on gfx9).
+    constexpr uint32_t kNoItem = 0x80000000u;
+    uint32_t  prev_total = 0, prev_it = kNoItem, prev_buf = 0, subc_v = 0, subo_v = 0;
     uint32_t* prev_out   = P.surv;
     auto copy_out = [&]() {
         const uint32_t nbytes = ((prev_total + 3u) & ~3u) * 4u;  // item region holds round_up(total, 4)
         const auto     ro     = buf_rsrc(prev_out, nbytes);
+        const v4u*     src    = (const v4u*) (stage + prev_buf * sstr);
 #pragma unroll
         for (int k = 0; k < kPC; k++) {
             const uint32_t i = tid + k * NT;
-            const v4u      v = ((const v4u*) stage)[i];  // LDS reads past the stage are never stored
+            const v4u      v = src[min(i, scap / 4 - 1)];  // reads past the stage are never stored
             __builtin_amdgcn_raw_buffer_store_b128(v, ro, i * 16, 0, 0);
         }
-        const uint32_t tb = prev_it == kNoItem ? 0u : NSUB * 4;  // run table of the previous item
+        const uint32_t tb = prev_it == kNoItem ? 0u : NSUB * 4;  // run table (wave 0 holds it)
         const auto rc = buf_rsrc(P.surv_cnt + (uint64_t) (prev_it & ~kNoItem) * NSUB, tb);
         const auto rf = buf_rsrc(P.surv_off + (uint64_t) (prev_it & ~kNoItem) * NSUB, tb);
         __builtin_amdgcn_raw_buffer_store_b32(subc_v, rc, tid * 4, 0, 0);
         __builtin_amdgcn_raw_buffer_store_b32(subo_v, rf, tid * 4, 0, 0);
     };
-    uint64_t filtered = 0;  // thread 63: survivors of this workgroup's items
+    uint64_t filtered = 0;  // wave 0: survivors of this workgroup's items
+    uint32_t nstep    = 0;  // items processed (selects the counter / stage buffers)
     // Outer loop: runs of items with one (q, seg), i.e. one slice segment in LDS. Inner loop:
-    // the pieces of the run, software-pipelined (chunks of piece p+1 and list entries of p+2 are
-    // in flight while piece p is tested, ranked and written; two register buffers alternate, so
-    // no load result is ever copied; past the end the loads re-read the last piece).
+    // the pieces of the run, software-pipelined: piece p is tested while p+1 and p+2 are in flight
+    // (three register buffers rotate, so no load result is ever copied; past the end the loads
+    // re-read the last piece). One barrier per piece: every wave scans the per-sub counters itself,
+    // counters are triple-buffered and the stage double-buffered.
     uint32_t it = it0;
     while (it < it1) {
         const uint32_t q    = __builtin_amdgcn_readfirstlane(find_q(P.item_start, F, it));
@@ -924,7 +931,8 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
         const uint32_t rend = min(it1, qi0 + (seg + 1) * npc);  // end of this (q, seg) run
         const uint32_t p1   = p0 + (rend - it);
         const uint32_t rit0 = it;  // item index of piece p0
-        if (slices) {  // (every wave is past the previous item's test phase: barrier B1)
+        if (slices) {
+            __syncthreads();  // every wave is done with the previous slice
             const uint4* src = (const uint4*) (P.slices + ((uint64_t) q * nseg + seg) * segw);
             uint4*       dst = (uint4*) slice;
             for (uint32_t i = tid; i < segw / 4; i += NT) dst[i] = src[i];
@@ -932,41 +940,57 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
         }
         auto lb_of = [&](uint32_t p) { return lq0 + p * kProbeCH; };
         auto le_of = [&](uint32_t p) { return min(lq1, lq0 + (p + 1) * kProbeCH); };
-        uint32_t   entA[kPC], entB[kPC];
-        Sweep<kPC> SA, SB;
+        uint32_t   eA[kPC], eB[kPC], eC[kPC];
+        Sweep<kPC> SA, SB, SC;
         {
-            const uint32_t pn = min(p0 + 1, p1 - 1);
-            load_list_u<kPC>(P.list, lb_of(p0), le_of(p0), entB);
-            load_list_u<kPC>(P.list, lb_of(pn), le_of(pn), entA);
-            load_chunks_u<kPC>(P.pool, entB, lb_of(p0), le_of(p0), SA);
-            copy_out();  // (previous run's last item, or nothing) -- the same vmcnt pattern as a step
-            prev_total = 0;
-            prev_it    = kNoItem;
+            const uint32_t pa = min(p0 + 1, p1 - 1), pb = min(p0 + 2, p1 - 1);
+            load_list_u<kPC>(P.list, lb_of(p0), le_of(p0), eA);
+            load_list_u<kPC>(P.list, lb_of(pa), le_of(pa), eB);
+            load_list_u<kPC>(P.list, lb_of(pb), le_of(pb), eC);
+            load_chunks_u<kPC>(P.pool, eA, lb_of(p0), le_of(p0), SA);
+            load_chunks_u<kPC>(P.pool, eB, lb_of(pa), le_of(pa), SB);
         }
-        // Sc: words of piece p (registers); en: list entries of p+1 -> Sn; enn <- list of p+2.
-        auto step = [&](uint32_t p, Sweep<kPC>& Sc, Sweep<kPC>& Sn, const uint32_t (&en)[kPC],
+        // Sc: words of piece p (registers); en: list entries of p+2 -> Sl; enn <- list of p+3.
+        auto step = [&](uint32_t p, Sweep<kPC>& Sc, Sweep<kPC>& Sl, const uint32_t (&en)[kPC],
                         uint32_t (&enn)[kPC]) {
-            const uint32_t p2 = min(p + 2, p1 - 1);
-            const uint32_t pn = min(p + 1, p1 - 1);
-            load_chunks_u<kPC>(P.pool, en, lb_of(pn), le_of(pn), Sn);
-            load_list_u<kPC>(P.list, lb_of(p2), le_of(p2), enn);
-            copy_out();
+            const uint32_t p2  = min(p + 2, p1 - 1);
+            const uint32_t p3  = min(p + 3, p1 - 1);
+            const uint32_t cb3 = nstep % 3;  // counter buffer of this piece
+            load_chunks_u<kPC>(P.pool, en, lb_of(p2), le_of(p2), Sl);
+            load_list_u<kPC>(P.list, lb_of(p3), le_of(p3), enn);
             stamp(0);
-            // ---- test: all slice reads first, then pass bits, then ranks (LDS counters per sub)
+            uint32_t* cnt = subc + cb3 * 128;
+            uint32_t* scr = scratch + wave * (kScrCap + 64);
+            // ---- test. One-bit kinds: all slice reads first, then per word slot the pass bit, its
+            // wave ballot and the compaction of the wave's survivors into its scratch (no exec
+            // masking: non-survivors write a per-lane dummy slot).
             uint32_t pass = 0;  // bit i: word i survives
+            uint32_t nsv  = 0;  // survivors of this wave (uniform)
             if (onebit) {
                 uint32_t wv[NW], bb[NW];  // slice word, bit index inside the segment
 #pragma unroll
                 for (int i = 0; i < NW; i++) {
-                    const Loc L = locate<KIND>(sweep_word(Sc, i >> 2, i & 3), g, inv);
-                    bb[i]       = L.base + L.h;
-                    wv[i]       = slice[bb[i] >> 5];
+                    const uint32_t w = sweep_word(Sc, i >> 2, i & 3);
+                    if (KIND == KIND_BLOCK_PK1 && SEG1) {
+                        bb[i] = ((w & g.lbmask) << g.log2B) + (w >> (32u - g.log2F));
+                    } else {
+                        const Loc L = locate<KIND>(w, g, inv);
+                        bb[i]       = L.base + L.h;
+                    }
+                    wv[i] = slice[bb[i] >> 5];
                 }
 #pragma unroll
                 for (int i = 0; i < NW; i++) {
-                    bool ok = (uint32_t) (i & 3) < Sc.n[i >> 2] && ((wv[i] >> (bb[i] & 31u)) & 1u);
-                    if (nseg > 1) ok = ok && locate<KIND>(sweep_word(Sc, i >> 2, i & 3), g, inv).seg == seg;
-                    pass |= (ok ? 1u : 0u) << i;
+                    const uint32_t w = sweep_word(Sc, i >> 2, i & 3);
+                    uint32_t ok = (wv[i] >> (bb[i] & 31u)) & ((uint32_t) (i & 3) < Sc.n[i >> 2] ? 1u : 0u);
+                    if (!SEG1) ok &= locate<KIND>(w, g, inv).seg == seg ? 1u : 0u;
+                    pass |= ok << i;
+                    const uint64_t m   = __builtin_amdgcn_ballot_w64(ok != 0);
+                    const uint32_t pre = __builtin_amdgcn_mbcnt_hi((uint32_t) (m >> 32),
+                                                                   __builtin_amdgcn_mbcnt_lo((uint32_t) m, 0u));
+                    const uint32_t at  = nsv + pre;
+                    scr[ok && at < kScrCap ? at : kScrCap + lane] = w;
+                    nsv += (uint32_t) __builtin_popcountll(m);
                 }
             } else {
 #pragma unroll
@@ -974,64 +998,77 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
                     bool ok = (uint32_t) (i & 3) < Sc.n[i >> 2];
                     if (slices && ok) {
                         const Loc L = locate<KIND>(sweep_word(Sc, i >> 2, i & 3), g, inv);
-                        ok          = (nseg == 1 || L.seg == seg) && apply_bits<KIND, false>(L, g, slice);
+                        ok          = (SEG1 || L.seg == seg) && apply_bits<KIND, false>(L, g, slice);
                     }
                     pass |= (ok ? 1u : 0u) << i;
                 }
+                nsv = kScrCap + 1;  // (word-by-word ranking)
             }
-            if (ABL == 2) pass = 0;
-            if (ABL == 3) {  // loads only: keep every loaded word alive, test nothing
+            // ---- ranks inside the piece's sub runs
+            const bool dense = nsv <= kScrCap;  // wave-uniform
+            uint32_t   dc[kDense], dr[kDense];   // dense: code; rank << 16 | sub
+            uint32_t   rank2[NW / 2];            // word by word: two 16-bit ranks per register
+            if (dense) {
 #pragma unroll
-                for (int j = 0; j < kPC; j++) asm volatile("" ::"v"(Sc.v[j].x), "v"(Sc.v[j].y), "v"(Sc.v[j].z), "v"(Sc.v[j].w));
-                pass = 0;
-            }
-            if (ABL == 1) {
-                if (pass) atomicAdd(&subc[0], __popc(pass));
-                pass = 0;
-            }
-            uint32_t rank2[NW / 2];  // two 16-bit ranks per register (a piece holds <= 16K words)
-#pragma unroll
-            for (int i = 0; i < NW; i += 2) {
-                uint32_t r[2] = {0, 0};
-#pragma unroll
-                for (int u = 0; u < 2; u++) {
-                    const uint32_t c = decode_k<KIND>(sweep_word(Sc, (i + u) >> 2, (i + u) & 3), q, g.log2F);
-                    const uint32_t s = (c >> g.sub_shift) & (NSUB - 1u);
-                    if ((pass >> (i + u)) & 1u) r[u] = atomicAdd(&subc[s], 1u);
+                for (int k = 0; k < kDense; k++) {
+                    const uint32_t j  = lane + 64u * k;
+                    const uint32_t c  = decode_k<KIND>(scr[j], q, g.log2F);
+                    const uint32_t s  = (c >> g.sub_shift) & (NSUB - 1u);
+                    const bool     ok = j < nsv;
+                    dc[k] = c;
+                    dr[k] = s | (atomicAdd(&cnt[ok ? s : 64u + lane], 1u) << 16);  // dummies: 64..127
                 }
-                rank2[i / 2] = r[0] | (r[1] << 16);
+            } else {
+#pragma unroll
+                for (int i = 0; i < NW; i += 2) {
+                    uint32_t r[2] = {0, 0};
+#pragma unroll
+                    for (int u = 0; u < 2; u++) {
+                        const uint32_t c = decode_k<KIND>(sweep_word(Sc, (i + u) >> 2, (i + u) & 3), q, g.log2F);
+                        const uint32_t s = (c >> g.sub_shift) & (NSUB - 1u);
+                        if ((pass >> (i + u)) & 1u) r[u] = atomicAdd(&cnt[s], 1u);
+                    }
+                    rank2[i / 2] = r[0] | (r[1] << 16);
+                }
             }
             stamp(1);
-            __syncthreads();  // B1
+            __syncthreads();  // B1: every rank of this piece taken; the previous piece staged
             stamp(2);
-            if (tid < 64) {
-                const uint32_t c    = tid < NSUB ? subc[tid] : 0u;
-                const uint32_t incl = wave_incl_scan(c);
-                subc_v              = c;
-                subo_v              = incl - c;
-                if (tid < NSUB) {
-                    subo[tid] = incl - c;
-                    subc[tid] = 0;
-                }
-                if (tid == 63) {
-                    filtered += incl;
-                    misc[0] = incl;
-                }
+            // ---- every wave: run offsets of this piece (DPP scan over the NSUB counters)
+            const uint32_t cs    = lane < (int) NSUB ? cnt[lane] : 0u;
+            const uint32_t incl  = wave_incl_scan_dpp(cs);
+            const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
+            uint32_t*      subo  = subow + wave * NSUB;
+            if (lane < (int) NSUB) subo[lane] = incl - cs;  // wave-private copy
+            if (wave == 0) subc[((nstep + 2) % 3) * 128 + lane] = 0;  // read two pieces ago
+            copy_out();  // previous piece (its stage buffer is complete: barrier B1)
+            if (wave == 0) {
+                subc_v = cs;
+                subo_v = incl - cs;
+                filtered += total;
             }
-            __syncthreads();  // B2
             stamp(3);
             uint32_t* __restrict__ out = P.surv + (uint64_t) seg * P.surv_seg_stride + (uint64_t) lb_of(p) * 32;
-            const uint32_t total  = __builtin_amdgcn_readfirstlane(misc[0]);
-            const bool     staged = total <= P.stage_cap;
-            if (staged) {  // LDS stage (copied out coalesced at the next step)
+            const uint32_t buf    = nstep & 1u;
+            const bool     staged = total <= scap;
+            uint32_t*      stg    = stage + buf * sstr;
+            const auto     ro     = buf_rsrc(out, total * 4);
+            if (dense) {
+#pragma unroll
+                for (int k = 0; k < kDense; k++) {
+                    const bool     ok = lane + 64u * k < nsv;
+                    const uint32_t o  = subo[dr[k] & 0xFFFFu] + (dr[k] >> 16);
+                    if (staged) stg[ok ? o : scap + lane] = dc[k];
+                    else __builtin_amdgcn_raw_buffer_store_b32(dc[k], ro, ok ? o * 4 : 0x7FFFFFF0u, 0, 0);
+                }
+            } else if (staged) {  // LDS stage (copied out coalesced at the next piece)
 #pragma unroll
                 for (int i = 0; i < NW; i++) {
                     const uint32_t c = decode_k<KIND>(sweep_word(Sc, i >> 2, i & 3), q, g.log2F);
                     const uint32_t o = subo[(c >> g.sub_shift) & (NSUB - 1u)] + ((rank2[i / 2] >> (16 * (i & 1))) & 0xFFFFu);
-                    if ((pass >> i) & 1u) stage[o] = c;
+                    stg[(pass >> i) & 1u ? o : scap + lane] = c;
                 }
-            } else {  // more survivors than the stage holds: scattered global (buffer) stores
-                const auto ro = buf_rsrc(out, total * 4);
+            } else {  // more survivors than a stage buffer holds: scattered global (buffer) stores
 #pragma unroll
                 for (int i = 0; i < NW; i++) {
                     const uint32_t c = decode_k<KIND>(sweep_word(Sc, i >> 2, i & 3), q, g.log2F);
@@ -1040,20 +1077,23 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
                 }
             }
             stamp(4);
-            __syncthreads();  // B3: stage complete (copied out at the start of the next step)
             prev_total = staged ? total : 0u;
             prev_out   = out;
+            prev_buf   = buf;
             prev_it    = rit0 + (p - p0);
+            nstep++;
             stamp(5);
         };
-        for (uint32_t p = p0; p < p1; p += 2) {
-            step(p, SA, SB, entA, entB);
-            if (p + 1 < p1) step(p + 1, SB, SA, entB, entA);
+        for (uint32_t p = p0; p < p1; p += 3) {
+            step(p, SA, SC, eC, eA);
+            if (p + 1 < p1) step(p + 1, SB, SA, eA, eB);
+            if (p + 2 < p1) step(p + 2, SC, SB, eB, eC);
         }
         it = rend;
     }
+    __syncthreads();  // the last piece is staged
     copy_out();
-    if (tid == 63 && filtered) atomicAdd((unsigned long long*) P.filtered, (unsigned long long) filtered);
+    if (tid == 0 && filtered) atomicAdd((unsigned long long*) P.filtered, (unsigned long long) filtered);
     if (P.dbg && tid == 0)
         for (int k = 0; k < 6; k++) P.dbg[blockIdx.x * 8 + k] = tph[k];
 }
@@ -1313,20 +1353,12 @@ static void build_inst(const BuildParams& p, uint32_t F, size_t lds, hipStream_t
 
 template <int KIND>
 static void probe_inst(const ProbeParams& p, uint32_t grid, size_t lds, hipStream_t st) {
-    (void) hipFuncSetAttribute((const void*) &k_probe<KIND>, hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds);
-    const char* ab = getenv("HWBRJ_PR_ABLATE");  // dev-only timing knob; results invalid if set
-    const int   a  = ab ? atoi(ab) : 0;
-    if (KIND == KIND_BLOCK_PK1 && a == 1) {
-        (void) hipFuncSetAttribute((const void*) &k_probe<KIND, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds);
-        k_probe<KIND, 1><<<grid, 1024, lds, st>>>(p);
-    } else if (KIND == KIND_BLOCK_PK1 && a == 3) {
-        (void) hipFuncSetAttribute((const void*) &k_probe<KIND, 3>, hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds);
-        k_probe<KIND, 3><<<grid, 1024, lds, st>>>(p);
-    } else if (KIND == KIND_BLOCK_PK1 && a == 2) {
-        (void) hipFuncSetAttribute((const void*) &k_probe<KIND, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds);
-        k_probe<KIND, 2><<<grid, 1024, lds, st>>>(p);
+    if (KIND == KIND_PASS || p.g.nseg == 1) {  // one slice segment per partition: no per-word segment check
+        (void) hipFuncSetAttribute((const void*) &k_probe<KIND, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds);
+        k_probe<KIND, true><<<grid, 1024, lds, st>>>(p);
     } else {
-        k_probe<KIND><<<grid, 1024, lds, st>>>(p);
+        (void) hipFuncSetAttribute((const void*) &k_probe<KIND, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds);
+        k_probe<KIND, false><<<grid, 1024, lds, st>>>(p);
     }
 }
 
@@ -1343,10 +1375,12 @@ void launch_build(const BuildParams& p, uint32_t F, hipStream_t st) {
 // Probe LDS: slice segment + tables + a survivor stage using what is left of the CU's 160 KiB.
 size_t probe_lds_bytes(const Geometry& g, uint32_t* stage_cap) {
     const bool   slices = g.mode == MODE_SLICE_BLOCK || g.mode == MODE_SLICE_BASIC;
-    const size_t base   = ((slices ? g.seg_words : 0) + 128 + 64 + 64 + 4) * sizeof(uint32_t);
-    size_t       cap    = std::min<size_t>(kProbeCH * 32, (163840 - base) / 4) & ~(size_t) 3;
+    const size_t NSUB   = (size_t) 1 << g.log2NSUB;
+    const size_t base   = ((slices ? g.seg_words : 0) + 128 + 3 * 128 + 16 * NSUB + 16 * (kScrCap + 64)) * sizeof(uint32_t);
+    // 2 buffers of cap words + 64 dummy slots each
+    size_t cap = std::min<size_t>(kProbeCH * 32, (163840 - base) / 8 - 64) & ~(size_t) 3;
     if (stage_cap) *stage_cap = (uint32_t) cap;
-    return base + cap * 4;
+    return base + 2 * (cap + 64) * 4;
 }
 
 void launch_probe(const ProbeParams& p0, uint32_t grid, hipStream_t st) {
