@@ -321,7 +321,7 @@ int Engine::run(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     sp.wgq_chunks = wgqcR.as<uint32_t>();
     sp.wgq_elems  = wgqeR.as<uint32_t>();
     sp.cap        = capR;
-    launch_scatter(sp, SRC_TUPLES, G, stream);
+    launch_scatter(sp, SRC_TUPLES, SIDE_R, G, stream);
     HWBRJ_CHECK(hipEventRecord(ev_[1], stream));
     launch_plan(wgqcR.as<uint32_t>(), wgqeR.as<uint32_t>(), G, g.log2F, CH, 1, wgqoR.as<uint32_t>(),
                 lstartR.as<uint32_t>(), estartR.as<uint64_t>(), istartR.as<uint32_t>(), stream);
@@ -364,7 +364,7 @@ int Engine::run(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
         HWBRJ_CHECK(hipMemsetAsync(dbgS.p, 0, dbgS.bytes, stream));
         sp.dbg = dbgS.as<uint64_t>();
     }
-    launch_scatter(sp, g.mode == MODE_GLOBAL ? SRC_CODES : SRC_TUPLES, G, stream);
+    launch_scatter(sp, g.mode == MODE_GLOBAL ? SRC_CODES : SRC_TUPLES, SIDE_S, G, stream);
     sp.dbg = nullptr;
     HWBRJ_CHECK(hipEventRecord(ev_[4], stream));
     launch_plan(wgqcS.as<uint32_t>(), wgqeS.as<uint32_t>(), G, g.log2F, CH, nseg, wgqoS.as<uint32_t>(),

@@ -78,7 +78,8 @@ void   launch_build_global(const uint2* R, uint64_t n, const Geometry& g, const 
 void   launch_probe_global(const uint2* S, uint64_t n, const Geometry& g, const CrcTables* tabs,
                            const uint32_t* bm, uint32_t* out, uint64_t* out_count, hipStream_t st);
 size_t scatter_lds_bytes(uint32_t log2F);
-void   launch_scatter(const ScatterParams& p, int src, uint32_t grid, hipStream_t st);
+enum { SIDE_R = 0, SIDE_S = 1 };  // which relation a scatter partitions (kernel name only)
+void   launch_scatter(const ScatterParams& p, int src, int side, uint32_t grid, hipStream_t st);
 void   launch_list_fill(const uint32_t* meta, const uint32_t* wg_used, uint64_t cap,
                         uint32_t log2F, const uint32_t* wgq_off, const uint32_t* list_start,
                         uint32_t* list, uint32_t grid, hipStream_t st);

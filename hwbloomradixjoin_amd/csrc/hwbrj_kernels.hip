@@ -301,7 +301,7 @@ struct ScRaw {  // one round's raw loads of this thread (tuples: keys only; code
 };
 
 template <int SRC, int MODE, int FMT>
-__global__ __launch_bounds__(kScThreads) void k_scatter(ScatterParams P) {
+__device__ __forceinline__ void scatter_body(const ScatterParams& P) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     constexpr int NL = SRC == SRC_TUPLES ? kScE / 2 : kScE / 4;  // uint4 loads per thread per round
     const uint32_t F     = 1u << P.g.log2F;
@@ -1297,25 +1297,33 @@ size_t scatter_lds_bytes(uint32_t log2F) {
     return (F * 32 + F + 4 + 5 * F + 128 + 4) * sizeof(uint32_t);  // stage, fill, ncb x2, 3 arrays, table, misc
 }
 
+// The R and S scatters are one body under two kernel names, so per-kernel profiles (rocprofv3
+// --kernel-trace --stats) report the two phases separately.
 template <int SRC, int MODE, int FMT>
-static void scatter_inst(const ScatterParams& p, uint32_t grid, hipStream_t st) {
+__global__ __launch_bounds__(kScThreads) void k_scatter_r(ScatterParams P) { scatter_body<SRC, MODE, FMT>(P); }
+template <int SRC, int MODE, int FMT>
+__global__ __launch_bounds__(kScThreads) void k_scatter_s(ScatterParams P) { scatter_body<SRC, MODE, FMT>(P); }
+
+template <int SRC, int MODE, int FMT>
+static void scatter_inst(const ScatterParams& p, int side, uint32_t grid, hipStream_t st) {
     const size_t lds = scatter_lds_bytes(p.g.log2F);
-    (void) hipFuncSetAttribute((const void*) &k_scatter<SRC, MODE, FMT>,
-                               hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds);
-    k_scatter<SRC, MODE, FMT><<<grid, kScThreads, lds, st>>>(p);
+    const void*  fn  = side == SIDE_R ? (const void*) &k_scatter_r<SRC, MODE, FMT> : (const void*) &k_scatter_s<SRC, MODE, FMT>;
+    (void) hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds);
+    if (side == SIDE_R) k_scatter_r<SRC, MODE, FMT><<<grid, kScThreads, lds, st>>>(p);
+    else k_scatter_s<SRC, MODE, FMT><<<grid, kScThreads, lds, st>>>(p);
 }
 
-void launch_scatter(const ScatterParams& p, int src, uint32_t grid, hipStream_t st) {
+void launch_scatter(const ScatterParams& p, int src, int side, uint32_t grid, hipStream_t st) {
     const Geometry& g = p.g;
-    if (src == SRC_CODES) return scatter_inst<SRC_CODES, MODE_GLOBAL, FMT_CODE>(p, grid, st);
+    if (src == SRC_CODES) return scatter_inst<SRC_CODES, MODE_GLOBAL, FMT_CODE>(p, side, grid, st);
     switch (g.mode) {
         case MODE_SLICE_BLOCK:
             if (g.format == FMT_PACKED)
-                return scatter_inst<SRC_TUPLES, MODE_SLICE_BLOCK, FMT_PACKED>(p, grid, st);
-            return scatter_inst<SRC_TUPLES, MODE_SLICE_BLOCK, FMT_CODE>(p, grid, st);
+                return scatter_inst<SRC_TUPLES, MODE_SLICE_BLOCK, FMT_PACKED>(p, side, grid, st);
+            return scatter_inst<SRC_TUPLES, MODE_SLICE_BLOCK, FMT_CODE>(p, side, grid, st);
         case MODE_SLICE_BASIC:
-            return scatter_inst<SRC_TUPLES, MODE_SLICE_BASIC, FMT_CODE>(p, grid, st);
-        default: return scatter_inst<SRC_TUPLES, MODE_NOBLOOM, FMT_CODE>(p, grid, st);
+            return scatter_inst<SRC_TUPLES, MODE_SLICE_BASIC, FMT_CODE>(p, side, grid, st);
+        default: return scatter_inst<SRC_TUPLES, MODE_NOBLOOM, FMT_CODE>(p, side, grid, st);
     }
 }
 

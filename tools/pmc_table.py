@@ -11,7 +11,7 @@ for d in sys.argv[1:]:
             by_kernel[(r["Kernel_Name"], r["Counter_Name"])].append(r)
         for (k, c), rs in by_kernel.items():
             rs.sort(key=lambda r: int(r["Start_Timestamp"]))
-            n = 2 if k == "k_scatter" or k == "k_list_fill" else 1
+            n = 2 if k == "k_list_fill" else 1
             for j, r in enumerate(rs[-n:]):
                 name = k if n == 1 else f"{k}#{'RS'[j]}"
                 vals[name][c] = float(r["Counter_Value"])

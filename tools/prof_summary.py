@@ -28,19 +28,16 @@ def one(path_glob):
 
 def last_join(names):
     """Indices of the dispatches of the last join (from the last R scatter on)."""
-    sc = [i for i, n in enumerate(names) if n == "k_scatter"]
-    if len(sc) < 2:
-        return list(range(len(names)))
-    start = sc[-2]
-    return list(range(start, len(names)))
+    sc = [i for i, n in enumerate(names) if n == "k_scatter_r"]
+    return list(range(sc[-1] if sc else 0, len(names)))
 
 
 def label(names, idx):
     out, nsc = [], 0
     for i in idx:
         n = names[i]
-        if n == "k_scatter":
-            out.append("r_scatter" if nsc == 0 else "s_scatter")
+        if n in ("k_scatter_r", "k_scatter_s"):
+            out.append(n[2:].replace("scatter_", "") + "_scatter")
             nsc += 1
         elif n in ("k_plan", "k_list_fill"):
             out.append("r_index" if nsc <= 1 else "s_index")

@@ -3,8 +3,8 @@ import csv, glob, sys
 f = glob.glob(f"{sys.argv[1]}/**/*kernel_trace.csv", recursive=True)[0]
 rows = sorted(csv.DictReader(open(f)), key=lambda r: int(r["Start_Timestamp"]))
 names = [r["Kernel_Name"].split("(")[0] for r in rows]
-sc = [i for i, n in enumerate(names) if n.startswith("void hwbrj::k_scatter") or n.startswith("k_scatter")]
-start = sc[-2] if len(sc) >= 2 else 0
+sc = [i for i, n in enumerate(names) if "k_scatter_r" in n]
+start = sc[-1] if sc else 0
 t0 = int(rows[start]["Start_Timestamp"])
 for r, n in zip(rows[start:], names[start:]):
     d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
