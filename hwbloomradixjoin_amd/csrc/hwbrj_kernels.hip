@@ -263,7 +263,6 @@ __global__ __launch_bounds__(1024) void k_probe_global(const uint2* S, uint64_t 
 // directly by the threads holding those overflow words. Chunk metadata = partition | count << 16.
 // (Reference pass-1: src/parallel_radix_join_bloom.c:758-852, SWWC variant :611-700.)
 constexpr int      kScThreads = 1024;
-constexpr int      kScPre     = 1;                        // rounds of loads in flight (1 or 2)
 constexpr int      kScE       = 8;                        // elements per thread per round
 constexpr uint32_t kScRound   = kScThreads * kScE;        // elements per workgroup round
 constexpr int      kScK       = 3;                        // flush tasks per thread per round (fixed)
@@ -271,9 +270,29 @@ constexpr uint32_t kCbBits    = 22;                       // ncb: chunk base | n
 constexpr uint32_t kCbMask    = (1u << kCbBits) - 1u;
 constexpr uint32_t kOob       = 0x7FFFFFF0u;              // buffer offset that is always dropped
 
+// 4 x BYTE_k of x, in one VALU op (SDWA source select): byte offset of entry (x >> 8k) & 255.
+template <int K>
+__device__ __forceinline__ uint32_t byte_x4(uint32_t x) {
+    static_assert(K >= 0 && K < 4, "byte index");
+    uint32_t r;
+    if (K == 0) asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0" : "=v"(r) : "v"(x));
+    if (K == 1) asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1" : "=v"(r) : "v"(x));
+    if (K == 2) asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2" : "=v"(r) : "v"(x));
+    if (K == 3) asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3" : "=v"(r) : "v"(x));
+    return r;
+}
+
+// CRC32-C code of a key from a 4 x 256 byte table in static LDS (row 0 has f(kSeed) folded in:
+// code = f(key ^ kSeed) = f(key) ^ f(kSeed)); 4 SDWA ops, 4 LDS reads with immediate row offsets.
+__device__ __forceinline__ uint32_t crc_bytes(const uint32_t* tab, uint32_t key) {
+    const char* b = (const char*) tab;
+    auto T = [&](uint32_t off) { return *(const uint32_t*) (b + off); };
+    return T(byte_x4<0>(key)) ^ T(byte_x4<1>(key) + 1024) ^ T(byte_x4<2>(key) + 2048) ^ T(byte_x4<3>(key) + 3072);
+}
+
 template <int SRC, int MODE, int FMT>
-__device__ __forceinline__ void sc_word(uint32_t x, const Geometry& g, const uint32_t* fwd,
-                                        uint32_t& w, uint32_t& q) {
+__device__ __forceinline__ void sc_word_lds0(uint32_t x, const Geometry& g, const uint32_t* tab,
+                                             uint32_t& w, uint32_t& q) {
     const uint32_t F1 = (1u << g.log2F) - 1u;
     if (SRC == SRC_CODES) {  // already a code (fallback survivors)
         w = x;
@@ -281,7 +300,7 @@ __device__ __forceinline__ void sc_word(uint32_t x, const Geometry& g, const uin
         return;
     }
     const uint32_t key  = x;
-    const uint32_t code = key_code(fwd, key);
+    const uint32_t code = crc_bytes(tab, key);
     if (MODE == MODE_SLICE_BASIC) {
         q = mod_m(crapwow(kSeed, key), (uint32_t) g.m) & F1;
         w = code;
@@ -300,27 +319,40 @@ struct ScRaw {  // one round's raw loads of this thread (tuples: keys only; code
     uint4    v[SRC == SRC_TUPLES ? 1 : kScE / 4];
 };
 
+// LDS: static CRC byte table (4 KiB, at 0, so its row offsets are immediates); dynamic (words):
+// stage F x 32 | 64 dummy slots | fill F + 4 | ncb 2F | tch F | tel F | flq F | misc 8
 template <int SRC, int MODE, int FMT>
 __device__ __forceinline__ void scatter_body(const ScatterParams& P) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    __shared__ uint32_t crc_tab[1024];
     constexpr int NL = SRC == SRC_TUPLES ? kScE / 2 : kScE / 4;  // uint4 loads per thread per round
+    static_assert(kScThreads == 1024, "one CRC table entry per thread");
     const uint32_t F     = 1u << P.g.log2F;
-    uint32_t*      stage = lds;             // F * 32
-    uint32_t*      fill  = stage + F * 32;  // F + 1 (entry F: invalid elements)
-    uint32_t*      ncb   = fill + F + 4;    // 2 x F: plan by round parity (chunk base | nchunks << 22)
-    uint32_t*      tch   = ncb + 2 * F;     // F: chunks of q (this workgroup)
-    uint32_t*      tel   = tch + F;         // F: elements of q (this workgroup)
-    uint32_t*      flq   = tel + F;         // F: partitions flushed by the last plan
-    uint32_t*      fwd   = flq + F;         // 128: CRC nibble table
-    uint32_t*      misc  = fwd + 128;       // [0] chunks used, [1 + parity] flushes of a round's plan
-    const int      tid   = threadIdx.x;
+    uint32_t*      stage = lds;                  // F * 32, then 64 per-lane dummy slots
+    uint32_t*      fill  = stage + F * 32 + 64;  // F + 1 (entry F: invalid elements)
+    uint32_t*      ncb   = fill + F + 4;         // 2 x F: plan by round parity (chunk base | nchunks << 22)
+    uint32_t*      tch   = ncb + 2 * F;          // F: chunks of q (this workgroup)
+    uint32_t*      tel   = tch + F;              // F: elements of q (this workgroup)
+    uint32_t*      flq   = tel + F;              // F: partitions flushed by the last plan
+    uint32_t*      misc  = flq + F;  // [0] chunks used, [1 + parity] flushes of a plan, [3 + parity] skew
+    const int      tid   = threadIdx.x, lane = tid & 63;
+    const uint32_t dummy = F * 32 + lane;        // stage index of this lane's dummy slot
     for (uint32_t i = tid; i < F + 1; i += kScThreads) fill[i] = 0;
     for (uint32_t i = tid; i < F; i += kScThreads) {
         tch[i] = 0;
         tel[i] = 0;
     }
-    load_tab(fwd, &P.tabs->fwd[0][0]);
-    if (tid < 4) misc[tid] = 0;
+    {  // byte table row k, entry b = f(b << 8k) from the nibble tables; f(kSeed) folded into row 0
+        const uint32_t* src = &P.tabs->fwd[0][0];
+        const uint32_t  k = tid >> 8, b = tid & 255;
+        uint32_t        v = src[(2 * k) * 16 + (b & 15u)] ^ src[(2 * k + 1) * 16 + (b >> 4)];
+        if (k == 0) {
+#pragma unroll
+            for (int j = 0; j < 8; j++) v ^= src[j * 16 + ((kSeed >> (4 * j)) & 15u)];
+        }
+        crc_tab[tid] = v;
+    }
+    if (tid < 8) misc[tid] = 0;
 
     const uint64_t n     = P.n_dev ? *P.n_dev : P.n;
     const uint64_t units = (n + 3) >> 2;
@@ -337,8 +369,14 @@ __device__ __forceinline__ void scatter_body(const ScatterParams& P) {
     const auto rmeta = buf_rsrc(meta, (uint32_t) (P.cap * 4));
     __syncthreads();
 
+    // Loads of the round at `base`: a full round of tuples takes the lane offset in voffset and the
+    // round offset in soffset (no per-element VALU); a partial round checks every index.
     auto load_round = [&](uint32_t base, ScRaw<SRC>& R) {
-        if (SRC == SRC_TUPLES) {  // keys only (the payload is not needed by the count join)
+        if (SRC == SRC_TUPLES && base + kScRound <= len) {
+#pragma unroll
+            for (int j = 0; j < kScE; j++)
+                R.k[j] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, tid * EB, (base + j * kScThreads) * EB, 0);
+        } else if (SRC == SRC_TUPLES) {  // keys only (the payload is not needed by the count join)
 #pragma unroll
             for (int j = 0; j < kScE; j++) {
                 const uint32_t i = base + j * kScThreads + tid;
@@ -395,54 +433,87 @@ __device__ __forceinline__ void scatter_body(const ScatterParams& P) {
         (void) k;
 #endif
     };
-    ScRaw<SRC> RA, RB;
+    ScRaw<SRC> RA;
     load_round(0, RA);
-    if (kScPre == 2) load_round(kScRound, RB);
-    // overflow words of the previous round: partition | slot << 11 (kNoPend: none), word
+    // Overflow words of the previous round (rank >= 32 in their partition's stage), written after
+    // the flush copy-out freed the stage line. Usual form (no partition of that round reached 64):
+    // stage index q * 32 + slot (the word goes to index - 32), or kNoPend. Skew form (pskew): the
+    // packed q | slot << 11, resolved against the plan (words beyond the stage line go to the
+    // directly written chunks).
     constexpr uint32_t kNoPend = 0xFFFFFFFFu;
     uint32_t pq[kScE], pw[kScE];
+    bool     pskew = false;
 #pragma unroll
     for (int j = 0; j < kScE; j++) pq[j] = kNoPend;
+    auto write_pending = [&]() {
+        if (!pskew) {
+#pragma unroll
+            for (int j = 0; j < kScE; j++) stage[pq[j] != kNoPend ? pq[j] - 32u : dummy] = pw[j];
+        } else {  // (plan of the previous round: ncb[par ^ 1])
+#pragma unroll
+            for (int j = 0; j < kScE; j++) {
+                const bool     ok = pq[j] != kNoPend;
+                const uint32_t qq = ok ? pq[j] & 2047u : 0u, sl = pq[j] >> 11;
+                const uint32_t cb = ncb[(par ^ 1u) * F + qq], nch = cb >> kCbBits;
+                const bool     st = sl >= nch * 32;
+                stage[ok && st ? qq * 32 + sl - nch * 32 : dummy] = pw[j];
+                const uint32_t po = ((cb & kCbMask) + (sl >> 5)) * 128 + (sl & 31u) * 4;
+                __builtin_amdgcn_raw_buffer_store_b32(pw[j], rpool, ok && !st ? po : kOob, 0, 0);
+            }
+        }
+    };
 
     auto round = [&](uint32_t base, ScRaw<SRC>& R) {
-        // ---- A: hash (consumes R), refill R two rounds ahead, copy out the last plan, rank
+        const bool full = base + kScRound <= len;  // uniform
+        // ---- A: hash (consumes R), refill R, copy out the last plan, rank
         uint32_t q[kScE], w[kScE];
 #pragma unroll
         for (int j = 0; j < kScE; j++) {
             uint32_t x, idx;
             elem(R, base, j, x, idx);
-            sc_word<SRC, MODE, FMT>(x, P.g, fwd, w[j], q[j]);
-            if (idx >= len) q[j] = F;  // invalid: ranked on the dummy counter
+            sc_word_lds0<SRC, MODE, FMT>(x, P.g, crc_tab, w[j], q[j]);
             if ((j & 1) == 1) __builtin_amdgcn_sched_barrier(0);  // bound the CRC reads in flight
         }
-        stamp(0);
-        load_round(base + kScPre * kScRound, R);
-        flush_copy();
-        if (tid == 0) misc[1 + par] = 0;  // (last read by the previous round's flush_copy)
-        stamp(1);
+        if (!full) {
 #pragma unroll
-        for (int j = 0; j < kScE; j++) q[j] |= atomicAdd(&fill[q[j]], 1u) << 11;  // q | slot << 11
+            for (int j = 0; j < kScE; j++) {
+                uint32_t x, idx;
+                elem(R, base, j, x, idx);
+                if (idx >= len) q[j] = F;  // invalid: ranked on the dummy counter
+            }
+        }
+        stamp(0);
+        load_round(base + kScRound, R);
+        flush_copy();
+        if (tid == 0) {
+            misc[1 + par]        = 0;  // (last read by the previous round's flush_copy)
+            misc[3 + (par ^ 1u)] = 0;  // (last read by the previous round's phase B)
+        }
+        stamp(1);
+        bool sk = false;  // a slot >= 63: some partition reaches 64 words this round
+#pragma unroll
+        for (int j = 0; j < kScE; j++) {
+            q[j] |= atomicAdd(&fill[q[j]], 1u) << 11;  // q | slot << 11
+            sk |= q[j] >= (63u << 11) && (q[j] & 2047u) < F;
+        }
+        if (__builtin_amdgcn_ballot_w64(sk) != 0 && lane == 0) misc[3 + par] = 1u;
         stamp(2);
         __syncthreads();  // B1: last plan copied out; every rank of this round taken
         stamp(3);
         // ---- B: overflow words of the previous round, in-stage words of this round, plan
-#pragma unroll
-        for (int j = 0; j < kScE; j++) {  // (plan of the previous round: ncb[par ^ 1])
-            if (pq[j] != kNoPend) {
-                const uint32_t qq = pq[j] & 2047u, sl = pq[j] >> 11;
-                const uint32_t cb = ncb[(par ^ 1u) * F + qq], nch = cb >> kCbBits;
-                if (sl >= nch * 32) stage[qq * 32 + sl - nch * 32] = pw[j];
-                else pool[((cb & kCbMask) + (sl >> 5)) * 32 + (sl & 31u)] = pw[j];  // skew only
-            }
-        }
+        write_pending();
+        const bool skew = __builtin_amdgcn_readfirstlane(misc[3 + par]) != 0;
 #pragma unroll
         for (int j = 0; j < kScE; j++) {
             const uint32_t qq = q[j] & 2047u, sl = q[j] >> 11;
-            const bool     ok = qq < F;
-            if (ok && sl < 32) stage[qq * 32 + sl] = w[j];
-            pq[j] = ok && sl >= 32 ? q[j] : kNoPend;
+            const uint32_t a  = qq * 32 + sl;
+            const bool     ok = full || qq < F;
+            stage[ok && sl < 32 ? a : dummy] = w[j];
+            if (!skew) pq[j] = ok && sl >= 32 ? a : kNoPend;
+            else pq[j] = ok && sl >= 32 ? q[j] : kNoPend;
             pw[j] = w[j];
         }
+        pskew = skew;
         {
             // one thread per partition (F <= 1024): flush plan
             const uint32_t qq  = tid;
@@ -453,7 +524,7 @@ __device__ __forceinline__ void scatter_body(const ScatterParams& P) {
             const uint32_t incl = wave_incl_scan_dpp(v);
             const uint32_t tot  = __builtin_amdgcn_readlane(incl, 63);
             uint32_t       wbc = 0, wbf = 0;
-            if ((tid & 63) == 0 && tot) {
+            if (lane == 0 && tot) {
                 wbc = atomicAdd(&misc[0], tot & 0xFFFFu);
                 wbf = atomicAdd(&misc[1 + par], tot >> 16);
             }
@@ -474,29 +545,12 @@ __device__ __forceinline__ void scatter_body(const ScatterParams& P) {
         stamp(5);
         par ^= 1u;
     };
-    uint32_t base = 0;
-    if (kScPre == 2) {
-        for (; base + kScRound < len; base += 2 * kScRound) {
-            round(base, RA);
-            round(base + kScRound, RB);
-        }
-        if (base < len) round(base, RA);
-    } else {
-        for (; base < len; base += kScRound) round(base, RA);
-    }
+    for (uint32_t base = 0; base < len; base += kScRound) round(base, RA);
     // ---- tail: last plan, the last overflow words, then every partial stage as a partial chunk
     {
         flush_copy();
         __syncthreads();
-#pragma unroll
-        for (int j = 0; j < kScE; j++) {
-            if (pq[j] != kNoPend) {
-                const uint32_t qq = pq[j] & 2047u, sl = pq[j] >> 11;
-                const uint32_t cb = ncb[(par ^ 1u) * F + qq], nch = cb >> kCbBits;
-                if (sl >= nch * 32) stage[qq * 32 + sl - nch * 32] = pw[j];
-                else pool[((cb & kCbMask) + (sl >> 5)) * 32 + (sl & 31u)] = pw[j];
-            }
-        }
+        write_pending();
         __syncthreads();
         for (uint32_t qq = tid; qq < F; qq += kScThreads) {
             const uint32_t f = fill[qq];
@@ -1294,7 +1348,7 @@ void launch_probe_global(const uint2* S, uint64_t n, const Geometry& g, const Cr
 
 size_t scatter_lds_bytes(uint32_t log2F) {
     const size_t F = 1u << log2F;
-    return (F * 32 + F + 4 + 5 * F + 128 + 4) * sizeof(uint32_t);  // stage, fill, ncb x2, 3 arrays, table, misc
+    return (F * 32 + 64 + F + 4 + 5 * F + 8) * sizeof(uint32_t);  // stage, dummies, fill, ncb x2, 3 arrays, misc (+4 KiB static)
 }
 
 // The R and S scatters are one body under two kernel names, so per-kernel profiles (rocprofv3
