@@ -270,24 +270,42 @@ constexpr uint32_t kCbBits    = 22;                       // ncb: chunk base | n
 constexpr uint32_t kCbMask    = (1u << kCbBits) - 1u;
 constexpr uint32_t kOob       = 0x7FFFFFF0u;              // buffer offset that is always dropped
 
-// 4 x BYTE_k of x, in one VALU op (SDWA source select): byte offset of entry (x >> 8k) & 255.
-template <int K>
-__device__ __forceinline__ uint32_t byte_x4(uint32_t x) {
+// 4 x (byte K of x) or (byte K of x) / 4, in one VALU op (SDWA source select).
+template <int K, bool RIGHT>
+__device__ __forceinline__ uint32_t byte_sh2(uint32_t x) {
     static_assert(K >= 0 && K < 4, "byte index");
     uint32_t r;
-    if (K == 0) asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0" : "=v"(r) : "v"(x));
-    if (K == 1) asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1" : "=v"(r) : "v"(x));
-    if (K == 2) asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2" : "=v"(r) : "v"(x));
-    if (K == 3) asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3" : "=v"(r) : "v"(x));
+#define HWBRJ_SDWA(op, sel) asm(op "_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:" sel : "=v"(r) : "v"(x))
+    if (!RIGHT) {
+        if (K == 0) HWBRJ_SDWA("v_lshlrev_b32", "BYTE_0");
+        if (K == 1) HWBRJ_SDWA("v_lshlrev_b32", "BYTE_1");
+        if (K == 2) HWBRJ_SDWA("v_lshlrev_b32", "BYTE_2");
+        if (K == 3) HWBRJ_SDWA("v_lshlrev_b32", "BYTE_3");
+    } else {
+        if (K == 0) HWBRJ_SDWA("v_lshrrev_b32", "BYTE_0");
+        if (K == 1) HWBRJ_SDWA("v_lshrrev_b32", "BYTE_1");
+        if (K == 2) HWBRJ_SDWA("v_lshrrev_b32", "BYTE_2");
+        if (K == 3) HWBRJ_SDWA("v_lshrrev_b32", "BYTE_3");
+    }
+#undef HWBRJ_SDWA
     return r;
 }
 
-// CRC32-C code of a key from a 4 x 256 byte table in static LDS (row 0 has f(kSeed) folded in:
-// code = f(key ^ kSeed) = f(key) ^ f(kSeed)); 4 SDWA ops, 4 LDS reads with immediate row offsets.
-__device__ __forceinline__ uint32_t crc_bytes(const uint32_t* tab, uint32_t key) {
-    const char* b = (const char*) tab;
+// CRC32-C code of a key from the 8 x 16 nibble table in static LDS (at address 0, so row offsets
+// are immediates; row 0 has f(kSeed) folded in: code = f(key ^ kSeed) = f(key) ^ f(kSeed)).
+// 16 entries per row sit in 16 distinct banks: the reads are conflict-free. Byte offsets of the
+// entries: even nibbles from key & 0x0F0F0F0F (<< 2), odd ones from key & 0xF0F0F0F0 (>> 2).
+__device__ __forceinline__ uint32_t crc_nib(const uint32_t* tab, uint32_t key) {
+    const char*    b = (const char*) tab;
+    const uint32_t y = key & 0x0F0F0F0Fu, z = key & 0xF0F0F0F0u;
     auto T = [&](uint32_t off) { return *(const uint32_t*) (b + off); };
-    return T(byte_x4<0>(key)) ^ T(byte_x4<1>(key) + 1024) ^ T(byte_x4<2>(key) + 2048) ^ T(byte_x4<3>(key) + 3072);
+    const uint32_t t0 = T(byte_sh2<0, false>(y)), t1 = T(byte_sh2<0, true>(z) + 64);
+    const uint32_t t2 = T(byte_sh2<1, false>(y) + 128), t3 = T(byte_sh2<1, true>(z) + 192);
+    const uint32_t t4 = T(byte_sh2<2, false>(y) + 256), t5 = T(byte_sh2<2, true>(z) + 320);
+    const uint32_t t6 = T(byte_sh2<3, false>(y) + 384), t7 = T(byte_sh2<3, true>(z) + 448);
+    const uint32_t a = __builtin_amdgcn_bitop3_b32(t0, t1, t2, 0x96);  // three-way xor
+    const uint32_t c = __builtin_amdgcn_bitop3_b32(t3, t4, t5, 0x96);
+    return __builtin_amdgcn_bitop3_b32(a, c, t6 ^ t7, 0x96);
 }
 
 template <int SRC, int MODE, int FMT>
@@ -300,7 +318,7 @@ __device__ __forceinline__ void sc_word_lds0(uint32_t x, const Geometry& g, cons
         return;
     }
     const uint32_t key  = x;
-    const uint32_t code = crc_bytes(tab, key);
+    const uint32_t code = crc_nib(tab, key);
     if (MODE == MODE_SLICE_BASIC) {
         q = mod_m(crapwow(kSeed, key), (uint32_t) g.m) & F1;
         w = code;
@@ -319,14 +337,13 @@ struct ScRaw {  // one round's raw loads of this thread (tuples: keys only; code
     uint4    v[SRC == SRC_TUPLES ? 1 : kScE / 4];
 };
 
-// LDS: static CRC byte table (4 KiB, at 0, so its row offsets are immediates); dynamic (words):
+// LDS: static CRC nibble table (512 B, at 0, so its row offsets are immediates); dynamic (words):
 // stage F x 32 | 64 dummy slots | fill F + 4 | ncb 2F | tch F | tel F | flq F | misc 8
 template <int SRC, int MODE, int FMT>
 __device__ __forceinline__ void scatter_body(const ScatterParams& P) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    __shared__ uint32_t crc_tab[1024];
+    __shared__ uint32_t crc_tab[128];
     constexpr int NL = SRC == SRC_TUPLES ? kScE / 2 : kScE / 4;  // uint4 loads per thread per round
-    static_assert(kScThreads == 1024, "one CRC table entry per thread");
     const uint32_t F     = 1u << P.g.log2F;
     uint32_t*      stage = lds;                  // F * 32, then 64 per-lane dummy slots
     uint32_t*      fill  = stage + F * 32 + 64;  // F + 1 (entry F: invalid elements)
@@ -342,11 +359,10 @@ __device__ __forceinline__ void scatter_body(const ScatterParams& P) {
         tch[i] = 0;
         tel[i] = 0;
     }
-    {  // byte table row k, entry b = f(b << 8k) from the nibble tables; f(kSeed) folded into row 0
+    if (tid < 128) {  // nibble table; f(kSeed) folded into row 0
         const uint32_t* src = &P.tabs->fwd[0][0];
-        const uint32_t  k = tid >> 8, b = tid & 255;
-        uint32_t        v = src[(2 * k) * 16 + (b & 15u)] ^ src[(2 * k + 1) * 16 + (b >> 4)];
-        if (k == 0) {
+        uint32_t        v   = src[tid];
+        if (tid < 16) {
 #pragma unroll
             for (int j = 0; j < 8; j++) v ^= src[j * 16 + ((kSeed >> (4 * j)) & 15u)];
         }
@@ -1348,7 +1364,7 @@ void launch_probe_global(const uint2* S, uint64_t n, const Geometry& g, const Cr
 
 size_t scatter_lds_bytes(uint32_t log2F) {
     const size_t F = 1u << log2F;
-    return (F * 32 + 64 + F + 4 + 5 * F + 8) * sizeof(uint32_t);  // stage, dummies, fill, ncb x2, 3 arrays, misc (+4 KiB static)
+    return (F * 32 + 64 + F + 4 + 5 * F + 8) * sizeof(uint32_t);  // stage, dummies, fill, ncb x2, 3 arrays, misc (+512 B static)
 }
 
 // The R and S scatters are one body under two kernel names, so per-kernel profiles (rocprofv3
