@@ -23,7 +23,7 @@ __all__ = [
 ]
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG_DIR, "libhwbrj.so")
+LIB_PATH = os.environ.get("HWBRJ_LIB") or os.path.join(PKG_DIR, "libhwbrj.so")  # HWBRJ_LIB: dev-only variant builds
 CLI_PATH = os.path.join(PKG_DIR, "mchashjoins")
 
 # src/bloom_filter.h:10 (BASIC, BLOCKED) + this build's SECTORIZED

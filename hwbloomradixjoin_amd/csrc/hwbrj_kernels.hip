@@ -263,9 +263,17 @@ __global__ __launch_bounds__(1024) void k_probe_global(const uint2* S, uint64_t 
 // directly by the threads holding those overflow words. Chunk metadata = partition | count << 16.
 // (Reference pass-1: src/parallel_radix_join_bloom.c:758-852, SWWC variant :611-700.)
 constexpr int      kScThreads = 1024;
-constexpr int      kScE       = 8;                        // elements per thread per round
+#ifndef HWBRJ_SC_E
+#define HWBRJ_SC_E 8
+#define HWBRJ_SC_K 3
+#endif
+#ifndef HWBRJ_SC_PRE
+#define HWBRJ_SC_PRE 1
+#endif
+constexpr int      kScPre     = HWBRJ_SC_PRE;             // rounds of loads in flight (1 or 2)
+constexpr int      kScE       = HWBRJ_SC_E;                        // elements per thread per round
 constexpr uint32_t kScRound   = kScThreads * kScE;        // elements per workgroup round
-constexpr int      kScK       = 3;                        // flush tasks per thread per round (fixed)
+constexpr int      kScK       = HWBRJ_SC_K;                        // flush tasks per thread per round (fixed)
 constexpr uint32_t kCbBits    = 22;                       // ncb: chunk base | nchunks << 22
 constexpr uint32_t kCbMask    = (1u << kCbBits) - 1u;
 constexpr uint32_t kOob       = 0x7FFFFFF0u;              // buffer offset that is always dropped
@@ -318,13 +326,21 @@ __device__ __forceinline__ void sc_word_lds0(uint32_t x, const Geometry& g, cons
         return;
     }
     const uint32_t key  = x;
+#ifdef HWBRJ_ABL_NOCRC
+    const uint32_t code = key * 0x9E3779B1u;  // dev ablation (results invalid)
+#else
     const uint32_t code = crc_nib(tab, key);
+#endif
     if (MODE == MODE_SLICE_BASIC) {
         q = mod_m(crapwow(kSeed, key), (uint32_t) g.m) & F1;
         w = code;
     } else if (MODE == MODE_SLICE_BLOCK && FMT == FMT_PACKED) {
         q = code & F1;
+#ifdef HWBRJ_ABL_NOCRAP
+        w = (code >> g.log2F) | (key << (32u - g.log2F));  // dev ablation (results invalid)
+#else
         w = (code >> g.log2F) | ((crapwow(kSeed, key) & (g.B - 1u)) << (32u - g.log2F));
+#endif
     } else {
         q = code & F1;
         w = code;
@@ -428,6 +444,9 @@ __device__ __forceinline__ void scatter_body(const ScatterParams& P) {
             const uint32_t l8 = k & 7;
             const uint32_t cb = ncb[(par ^ 1u) * F + qq] & kCbMask;
             const v4u      v  = *(const v4u*) &stage[qq * 32 + l8 * 4];
+#ifdef HWBRJ_ABL_NOSTORE
+            if (v.x == 0x12345678u && v.y == 0x9abcdef0u)  // dev ablation: practically never stores
+#endif
             __builtin_amdgcn_raw_buffer_store_b128(v, rpool, ok ? (cb * 32 + l8 * 4) * 4 : kOob, 0, 0);
             __builtin_amdgcn_raw_buffer_store_b32(qq | (32u << 16), rmeta, ok && l8 == 0 ? cb * 4 : kOob, 0, 0);
         };
@@ -449,8 +468,9 @@ __device__ __forceinline__ void scatter_body(const ScatterParams& P) {
         (void) k;
 #endif
     };
-    ScRaw<SRC> RA;
+    ScRaw<SRC> RA, RB;
     load_round(0, RA);
+    if (kScPre == 2) load_round(kScRound, RB);
     // Overflow words of the previous round (rank >= 32 in their partition's stage), written after
     // the flush copy-out freed the stage line. Usual form (no partition of that round reached 64):
     // stage index q * 32 + slot (the word goes to index - 32), or kNoPend. Skew form (pskew): the
@@ -499,7 +519,7 @@ __device__ __forceinline__ void scatter_body(const ScatterParams& P) {
             }
         }
         stamp(0);
-        load_round(base + kScRound, R);
+        load_round(base + kScPre * kScRound, R);
         flush_copy();
         if (tid == 0) {
             misc[1 + par]        = 0;  // (last read by the previous round's flush_copy)
@@ -561,22 +581,46 @@ __device__ __forceinline__ void scatter_body(const ScatterParams& P) {
         stamp(5);
         par ^= 1u;
     };
-    for (uint32_t base = 0; base < len; base += kScRound) round(base, RA);
+    uint32_t base = 0;
+    if (kScPre == 2) {
+        for (; base + kScRound < len; base += 2 * kScRound) {
+            round(base, RA);
+            round(base + kScRound, RB);
+        }
+        if (base < len) round(base, RA);
+    } else {
+        for (; base < len; base += kScRound) round(base, RA);
+    }
     // ---- tail: last plan, the last overflow words, then every partial stage as a partial chunk
     {
         flush_copy();
         __syncthreads();
         write_pending();
         __syncthreads();
-        for (uint32_t qq = tid; qq < F; qq += kScThreads) {
-            const uint32_t f = fill[qq];
-            if (f > 0) {
-                const uint32_t cb = atomicAdd(&misc[0], 1u);
-                meta[cb]          = qq | (f << 16);
-                for (uint32_t s2 = 0; s2 < f; s2++) pool[cb * 32 + s2] = stage[qq * 32 + s2];
+        {  // one thread per partition (F <= 1024): chunk ids of the partial stages (wave scan)
+            const uint32_t qq   = tid;
+            const uint32_t f    = qq < F ? fill[qq] : 0u;
+            const uint32_t has  = f > 0 ? 1u : 0u;
+            const uint32_t incl = wave_incl_scan_dpp(has);
+            const uint32_t tot  = __builtin_amdgcn_readlane(incl, 63);
+            uint32_t       wb   = 0;
+            if (lane == 0 && tot) wb = atomicAdd(&misc[0], tot);
+            wb = __builtin_amdgcn_readfirstlane(wb);
+            if (has) {
+                const uint32_t cb = wb + incl - 1u;
+                ncb[qq]  = cb;
+                meta[cb] = qq | (f << 16);
                 tch[qq] += 1;
                 tel[qq] += f;
             }
+        }
+        __syncthreads();
+        // copy-out of the partial stages, 16 bytes per task (words past the count are never read)
+        for (uint32_t k = tid; k < F * 8; k += kScThreads) {
+            const uint32_t qq = k >> 3, l8 = k & 7;
+            const bool     ok = fill[qq] > 0;
+            const v4u      v  = *(const v4u*) &stage[qq * 32 + l8 * 4];
+            __builtin_amdgcn_raw_buffer_store_b128(v, rpool, ok ? (ncb[qq] * 32 + l8 * 4) * 4 : kOob, 0, 0);
         }
         __syncthreads();
         if (tid == 0) P.wg_used[wg] = misc[0];
