@@ -18,7 +18,9 @@ import numpy as np
 __all__ = [
     "BASIC", "BLOCKED", "SECTORIZED", "BloomFilterArgs", "Relation", "Result", "Stats",
     "BPRO", "PRO", "assert_args", "join_device", "generate_device", "generate_device_range",
-    "generate_host",
+    "generate_host", "nonunique_threshold", "create_relation_nonunique",
+    "create_relation_nonunique_from_pk", "create_relation_fk_from_pk", "create_relation_zipf",
+    "rand_stream", "reference_relations",
     "export_filter", "hash_crc", "hash_crapwow", "lib", "LIB_PATH", "shard_range",
 ]
 
@@ -93,6 +95,20 @@ def lib() -> ctypes.CDLL:
         L.hwbrj_generate_host.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
                                           ctypes.c_uint64, ctypes.c_uint64, ctypes.c_double,
                                           ctypes.c_uint64, ctypes.c_int]
+        L.hwbrj_nonunique_threshold.restype = ctypes.c_uint64
+        L.hwbrj_nonunique_threshold.argtypes = [ctypes.c_uint64, ctypes.c_double, ctypes.c_int]
+        L.hwbrj_create_relation_nonunique.restype = ctypes.c_int
+        L.hwbrj_create_relation_nonunique.argtypes = [ctypes.c_void_p, ctypes.c_uint64,
+                                                      ctypes.c_int64, ctypes.c_uint32]
+        for fn in (L.hwbrj_create_relation_nonunique_from_pk, L.hwbrj_create_relation_fk_from_pk):
+            fn.restype = ctypes.c_int
+            fn.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64,
+                           ctypes.c_int64, ctypes.c_double, ctypes.c_uint32]
+        L.hwbrj_create_relation_zipf.restype = ctypes.c_int
+        L.hwbrj_create_relation_zipf.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
+                                                 ctypes.c_double, ctypes.c_uint32, ctypes.c_int]
+        L.hwbrj_rand_stream.restype = ctypes.c_int
+        L.hwbrj_rand_stream.argtypes = [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint64]
         L.hwbrj_export_filter.restype = ctypes.c_int
         L.hwbrj_export_filter.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
         L.hwbrj_hash_crc.restype = ctypes.c_uint32
@@ -248,6 +264,73 @@ def generate_host(n: int, nthreads: int, maxid: int, threshold: int, selectivity
     _err(lib().hwbrj_generate_host(out.ctypes.data, n, nthreads, maxid, threshold, selectivity,
                                    seed, host_threads), "hwbrj_generate_host")
     return out
+
+
+def nonunique_threshold(r_size: int, selectivity: float, full_range: bool) -> int:
+    """src/main.c:421-427: the key bound of --non-unique / --full-range relations."""
+    return int(lib().hwbrj_nonunique_threshold(r_size, selectivity, 1 if full_range else 0))
+
+
+def create_relation_nonunique(n: int, maxid: int, seed: int) -> np.ndarray:
+    """src/generator.c:585-605 after srand(seed): n random keys in [0, maxid), payload = row."""
+    out = np.empty((n, 2), dtype=np.int32)
+    _err(lib().hwbrj_create_relation_nonunique(out.ctypes.data, n, maxid, seed),
+         "hwbrj_create_relation_nonunique")
+    return out
+
+
+def _from_pk(fn, name, n, pk, threshold, selectivity, seed):
+    pk = np.ascontiguousarray(pk, dtype=np.int32)
+    out = np.empty((n, 2), dtype=np.int32)
+    _err(fn(out.ctypes.data, n, pk.ctypes.data, pk.shape[0], threshold, selectivity, seed), name)
+    return out
+
+
+def create_relation_nonunique_from_pk(n: int, pk: np.ndarray, threshold: int, selectivity: float,
+                                      seed: int) -> np.ndarray:
+    """src/generator.c:608-646 (the --non-unique S relation)."""
+    return _from_pk(lib().hwbrj_create_relation_nonunique_from_pk,
+                    "hwbrj_create_relation_nonunique_from_pk", n, pk, threshold, selectivity, seed)
+
+
+def create_relation_fk_from_pk(n: int, pk: np.ndarray, threshold: int, selectivity: float,
+                               seed: int) -> np.ndarray:
+    """src/generator.c:531-582 (the --full-range S relation)."""
+    return _from_pk(lib().hwbrj_create_relation_fk_from_pk, "hwbrj_create_relation_fk_from_pk",
+                    n, pk, threshold, selectivity, seed)
+
+
+def create_relation_zipf(n: int, alphabet_size: int, theta: float, seed: int,
+                         host_threads: int = 0) -> np.ndarray:
+    """src/generator.c:659-676 + src/genzipf.c:28-158 (the -z S relation), payload = row."""
+    out = np.empty((n, 2), dtype=np.int32)
+    _err(lib().hwbrj_create_relation_zipf(out.ctypes.data, n, alphabet_size, theta, seed,
+                                          host_threads), "hwbrj_create_relation_zipf")
+    return out
+
+
+def rand_stream(seed: int, n: int) -> np.ndarray:
+    """The first n values of glibc rand() after srand(seed), from the library's restatement."""
+    out = np.empty(n, dtype=np.int32)
+    _err(lib().hwbrj_rand_stream(seed, out.ctypes.data, n), "hwbrj_rand_stream")
+    return out
+
+
+def reference_relations(r_size: int, s_size: int, selectivity: float = 1.0, skew: float = 0.0,
+                        non_unique: bool = False, full_range: bool = False, r_seed: int = 12345,
+                        s_seed: int = 54321, nthreads: int = 2, host_threads: int = 0):
+    """(R, S) as the reference's main() builds them (src/main.c:410-466), on the host:
+    --full-range, --non-unique and -z are bit-exact (keys and order) to the reference for the same
+    seeds; the default PK/FK relations have the reference's key multiset in a seeded order."""
+    if full_range or non_unique:
+        thr = nonunique_threshold(r_size, selectivity, full_range)
+        R = create_relation_nonunique(r_size, thr, r_seed)
+        mk = create_relation_fk_from_pk if full_range else create_relation_nonunique_from_pk
+        return R, mk(s_size, R, thr, selectivity, s_seed)
+    R = generate_host(r_size, nthreads, r_size, r_size, 1.0, r_seed, host_threads)
+    if skew > 0:
+        return R, create_relation_zipf(s_size, r_size, skew, s_seed, host_threads)
+    return R, generate_host(s_size, nthreads, 2**31 - 1, r_size, selectivity, s_seed, host_threads)
 
 
 def export_filter(m_bits: int) -> np.ndarray:

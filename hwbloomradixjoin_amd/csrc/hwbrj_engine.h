@@ -57,4 +57,18 @@ class Engine {
 Engine* engine_for_current_device();
 void    set_last_error(const std::string& s);
 
+// glibc's rand() (stdlib/random_r.c TYPE_3) with private state (hwbrj_gen.cpp).
+struct GlibcRand {
+    int32_t st[31];
+    int     f = 3, r = 0;
+    void    seed(uint32_t s);
+    int32_t next() {
+        st[f]           = (int32_t) ((uint32_t) st[f] + (uint32_t) st[r]);
+        const int32_t v = (int32_t) ((uint32_t) st[f] >> 1);
+        f               = f == 30 ? 0 : f + 1;
+        r               = r == 30 ? 0 : r + 1;
+        return v;
+    }
+};
+
 }  // namespace hwbrj

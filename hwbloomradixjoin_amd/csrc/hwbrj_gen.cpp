@@ -1,0 +1,229 @@
+// hwbrj_gen.cpp -- the reference's rand()-driven relation generators on the host, bit-exact.
+//
+// The reference builds these relations with glibc rand() after srand(-x / -y seed)
+// (src/main.c:410-466):
+//   --non-unique  R: create_relation_nonunique          src/generator.c:585-605 (random_gen :271-279)
+//                 S: create_relation_nonunique_from_pk  :608-646
+//   --full-range  R: create_relation_nonunique          (threshold = ceil(INT_MAX * q))
+//                 S: create_relation_fk_from_pk         :531-582
+//   -z <theta>    S: create_relation_zipf -> gen_zipf   :659-676, src/genzipf.c:28-158
+// Their counts depend on the exact rand() sequence, so rand() is restated here (glibc's TYPE_3
+// additive feedback generator behind rand(), with its own state instead of libc's global one) and
+// every draw happens in the reference's order, including the Knuth shuffles. The only deliberate
+// difference: gen_zipf leaves payloads uninitialised (genzipf.c:147-148); here payload = row index.
+//
+// Host code, compiled without floating-point contraction: RAND_RANGE's a*b+c must round like the
+// reference's x86-64 build (no FMA).
+#include <math.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <climits>
+#include <thread>
+#include <vector>
+
+#include "hwbrj_engine.h"
+
+#pragma clang fp contract(off)
+
+namespace hwbrj {
+
+// glibc stdlib/random_r.c, TYPE_3 (degree 31, separation 3): srandom_r seeds the 31 words with
+// the Park-Miller LCG (Schrage's method), then discards 310 outputs; random_r adds the lagged word
+// and returns the sum >> 1. RAND_MAX = 2^31 - 1.
+void GlibcRand::seed(uint32_t s) {
+    if (s == 0) s = 1;
+    int32_t word = (int32_t) s;
+    st[0]        = word;
+    for (int i = 1; i < 31; i++) {
+        const int64_t hi = word / 127773, lo = word % 127773;
+        int64_t       w  = 16807 * lo - 2836 * hi;
+        if (w < 0) w += 2147483647;
+        word  = (int32_t) w;
+        st[i] = word;
+    }
+    f = 3;
+    r = 0;
+    for (int i = 0; i < 310; i++) (void) next();
+}
+
+// ------------------------------------------------------------------ src/generator.c helpers
+static constexpr double kRandMaxP1 = (double) 2147483647 + 1;  // (double) RAND_MAX + 1
+
+// RAND_RANGE(O, N) = O + (double) rand() / ((double) RAND_MAX + 1) * (N - O)   (generator.c:25)
+static inline double rand_range(GlibcRand& g, double O, double N) {
+    const double x = (double) g.next() / kRandMaxP1;
+    const double s = x * (N - O);
+    return O + s;
+}
+
+// random_gen (generator.c:271-279): keys in [minid, maxid), payload = index in `rel`.
+static void random_gen(GlibcRand& g, tuple_t* rel, uint64_t n, int64_t minid, int64_t maxid) {
+    for (uint64_t i = 0; i < n; i++) {
+        rel[i].key     = (int32_t) rand_range(g, (double) minid, (double) maxid);
+        rel[i].payload = (int32_t) i;
+    }
+}
+
+// knuth_shuffle (generator.c:99-109): keys only; the loop index is an int.
+static void knuth_shuffle(GlibcRand& g, tuple_t* rel, uint64_t n) {
+    for (int i = (int) n - 1; i > 0; i--) {
+        const int64_t j   = (int64_t) rand_range(g, 0.0, (double) i);
+        const int32_t tmp = rel[i].key;
+        rel[i].key        = rel[j].key;
+        rel[j].key        = tmp;
+    }
+}
+
+}  // namespace hwbrj
+
+using namespace hwbrj;
+
+extern "C" {
+
+uint64_t hwbrj_nonunique_threshold(uint64_t r_size, double selectivity, int full_range) {
+    // src/main.c:421-427
+    const double t = ceil((double) INT_MAX * selectivity);
+    if (full_range) return (uint64_t) t;
+    return (double) r_size < t ? r_size : (uint64_t) t;
+}
+
+int hwbrj_rand_stream(uint32_t seed, int32_t* out, uint64_t n) {
+    GlibcRand g;
+    g.seed(seed);
+    for (uint64_t i = 0; i < n; i++) out[i] = g.next();
+    return 0;
+}
+
+int hwbrj_create_relation_nonunique(tuple_t* out, uint64_t n, int64_t maxid, uint32_t seed) {
+    if (!out && n) {
+        set_last_error("null output");
+        return 2;
+    }
+    GlibcRand g;
+    g.seed(seed);  // seed_generator (generator.c:75-81, main.c:410)
+    random_gen(g, out, n, 0, maxid);
+    return 0;
+}
+
+int hwbrj_create_relation_nonunique_from_pk(tuple_t* out, uint64_t n, const tuple_t* pk,
+                                            uint64_t npk, int64_t threshold, double selectivity,
+                                            uint32_t seed) {
+    if ((!out && n) || (!pk && npk) || (npk == 0 && n > 0) || n > (uint64_t) INT_MAX) {
+        set_last_error("invalid arguments (|S| must be < 2^31 and the pk relation non-empty)");
+        return 2;
+    }
+    GlibcRand g;
+    g.seed(seed);
+    const uint64_t above = (uint64_t) ((double) n * (1 - selectivity));  // generator.c:616
+    if (above > n) {
+        set_last_error("selectivity out of range");
+        return 2;
+    }
+    random_gen(g, out, above, threshold + 1, INT_MAX);
+    for (int i = (int) above; i < (int) n; i++) {  // :632-637
+        const int j    = (int) rand_range(g, 0.0, (double) npk);
+        out[i].key     = pk[j].key;
+        out[i].payload = i;
+    }
+    knuth_shuffle(g, out, n);
+    return 0;
+}
+
+int hwbrj_create_relation_fk_from_pk(tuple_t* out, uint64_t n, const tuple_t* pk, uint64_t npk,
+                                     int64_t threshold, double selectivity, uint32_t seed) {
+    if ((!out && n) || (!pk && npk) || n > (uint64_t) INT_MAX) {
+        set_last_error("invalid arguments (|S| must be < 2^31)");
+        return 2;
+    }
+    GlibcRand g;
+    g.seed(seed);
+    const uint64_t above = (uint64_t) ((double) n * (1 - selectivity));  // generator.c:548
+    if (above > n) {
+        set_last_error("selectivity out of range");
+        return 2;
+    }
+    const uint64_t below = n - above;
+    if (below > 0 && npk == 0) {
+        set_last_error("empty pk relation");
+        return 2;
+    }
+    random_gen(g, out + below, above, threshold + 1, INT_MAX);  // unmatched tuples last
+    uint64_t off = 0;
+    while (off < below) {  // whole copies of pk, then the remainder (:560-571)
+        const uint64_t c = std::min(npk, below - off);
+        memcpy(out + off, pk, c * sizeof(tuple_t));
+        off += c;
+    }
+    knuth_shuffle(g, out, n);
+    return 0;
+}
+
+// src/genzipf.c:28-158 via create_relation_zipf (generator.c:659-676). The rand() stream is drawn
+// in order on one thread; the binary searches over the CDF run on `host_threads` threads.
+int hwbrj_create_relation_zipf(tuple_t* out, uint64_t n, uint64_t alphabet_size, double theta,
+                               uint32_t seed, int host_threads) {
+    if ((!out && n) || alphabet_size == 0 || alphabet_size > (uint64_t) UINT_MAX ||
+        n > (uint64_t) UINT_MAX) {
+        set_last_error("invalid arguments (alphabet and |S| must be in [1, 2^32))");
+        return 2;
+    }
+    const unsigned int size = (unsigned int) alphabet_size;
+    GlibcRand          g;
+    g.seed(seed);
+    int T = host_threads > 0 ? host_threads : (int) std::thread::hardware_concurrency();
+    T     = std::max(1, std::min(T, 64));
+    auto par = [&](uint64_t total, auto&& fn) {
+        std::vector<std::thread> th;
+        for (int t = 0; t < T; t++)
+            th.emplace_back([&, t] { fn(total * t / T, total * (t + 1) / T); });
+        for (auto& x : th) x.join();
+    };
+    // gen_alphabet (:28-53): 1..size, permuted by rand()
+    std::vector<uint32_t> alphabet(size);
+    for (unsigned int i = 0; i < size; i++) alphabet[i] = i + 1;
+    for (unsigned int i = size - 1; i > 0; i--) {
+        const unsigned int k   = (unsigned int) ((unsigned long) i * (unsigned long) g.next() /
+                                                 (unsigned long) 2147483647);
+        const uint32_t     tmp = alphabet[i];
+        alphabet[i]            = alphabet[k];
+        alphabet[k]            = tmp;
+    }
+    // gen_zipf_lut (:60-92): the two sequential sums of 1 / pow(i, theta); the pow terms are
+    // computed in parallel (same values), the sums in the reference's order.
+    std::vector<double> lut(size);
+    par(size, [&](uint64_t b, uint64_t e) {
+        for (uint64_t i = b; i < e; i++) lut[i] = 1.0 / pow((double) (unsigned int) (i + 1), theta);
+    });
+    double scaling = 0.0;
+    for (unsigned int i = 0; i < size; i++) scaling += lut[i];
+    double sum = 0.0;
+    for (unsigned int i = 0; i < size; i++) {
+        sum += lut[i];
+        lut[i] = sum / scaling;
+    }
+    // the stream (:119-150): r = rand() / RAND_MAX, binary search, key = alphabet[pos]
+    for (uint64_t i = 0; i < n; i++) out[i].key = g.next();
+    par(n, [&](uint64_t b, uint64_t e) {
+        for (uint64_t i = b; i < e; i++) {
+            const double r     = ((double) out[i].key) / 2147483647;
+            unsigned int left  = 0, right = size - 1, pos;
+            if (lut[0] >= r) {
+                pos = 0;
+            } else {
+                while (right - left > 1) {
+                    const unsigned int m = (left + right) / 2;
+                    if (lut[m] < r) left = m;
+                    else right = m;
+                }
+                pos = right;
+            }
+            out[i].key     = (int32_t) alphabet[pos];
+            out[i].payload = (int32_t) i;
+        }
+    });
+    return 0;
+}
+
+}  // extern "C"

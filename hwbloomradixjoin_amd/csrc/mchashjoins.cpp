@@ -4,9 +4,10 @@
 // Differences from the reference driver (DESIGN.md "CLI"):
 //   -b sectorized    selects this build's SECTORIZED filter (the reference silently runs BASIC);
 //   -a               PRO is the only algorithm behind this boundary (others print an error);
-//   -z / --non-unique / --full-range are not generated yet (error);
-//   relations are generated with the reference's key multiset and a seeded (-x / -y) Feistel
-//   shuffle instead of the time-seeded Knuth shuffle (src/generator.c:173-176).
+//   -z / --non-unique / --full-range relations are the reference's exactly (restated glibc
+//   rand() after srand(-x / -y), hwbrj_gen.cpp); the default PK/FK relations have the reference's
+//   key multiset in a seeded (-x / -y) Feistel order instead of the time-seeded Knuth shuffle
+//   (src/generator.c:173-176).
 #include <getopt.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -48,6 +49,9 @@ static void print_help(const char* prog) {
         "       -x --r-seed=<x>    Seed value for generating relation R <x> [12345]     \n"
         "       -y --s-seed=<y>    Seed value for generating relation S <y> [54321]     \n"
         "       -q --s-sel=<q>     Selectivity for %% of S-tuples with a match in R [1.0]\n"
+        "       -z --skew=<z>      Zipf skew parameter for probe relation S <z> [0.0]   \n"
+        "       --non-unique       Use non-unique (duplicated) keys in input relations  \n"
+        "       --full-range       Spread keys in relns. in full 32-bit integer range   \n"
         "       -R --r-file=<Rf>   The file to load build relation R from <Rf> [R.tbl]  \n"
         "       -S --s-file=<Sf>   The file to load probe relation S from <Sf> [S.tbl]  \n"
         "                                                                               \n"
@@ -61,7 +65,9 @@ static void print_help(const char* prog) {
         "        --version         Show version                                         \n");
 }
 
-// src/generator.c:685-741: "key payload" or "key,payload" per line, '#' comments.
+// src/generator.c:685-741 (read_relation): the first line is a header and is skipped; data lines
+// are "key payload", "key,payload" or a bare key (payload 0). Reads at most n tuples; a shorter
+// file gives a shorter relation (the reference would repeat its last tuple).
 static int load_relation(relation_t* rel, const char* path, uint64_t n) {
     FILE* fp = fopen(path, "r");
     if (!fp) {
@@ -72,12 +78,19 @@ static int load_relation(relation_t* rel, const char* path, uint64_t n) {
     rel->num_tuples = n;
     char     line[256];
     uint64_t i = 0;
+    if (!fgets(line, sizeof line, fp)) line[0] = 0;  // header
+    bool warn = true;
     while (i < n && fgets(line, sizeof line, fp)) {
-        if (line[0] == '#') continue;
         for (char* c = line; *c; c++)
             if (*c == ',' || *c == '|') *c = ' ';
-        long long k, p;
-        if (sscanf(line, "%lld %lld", &k, &p) != 2) continue;
+        long long k = 0, p = 0;
+        const int got = sscanf(line, "%lld %lld", &k, &p);
+        if (got < 1) continue;
+        if (got == 1) p = 0;
+        if (warn && k < 0) {  // :732-735
+            warn = false;
+            printf("[WARN ] key=%d, payload=%d\n", (int32_t) k, (int32_t) p);
+        }
         rel->tuples[i].key     = (int32_t) k;
         rel->tuples[i].payload = (int32_t) p;
         i++;
@@ -154,10 +167,6 @@ int main(int argc, char** argv) {
         }
     }
     if (P.bloom) assert_args(&P.bf);  // src/main.c:730
-    if (P.skew > 0 || nonunique || fullrange) {
-        printf("[ERROR] -z / --non-unique / --full-range generation is not available in this build\n");
-        exit(EXIT_FAILURE);
-    }
     if (P.gpus != 1) {
         printf("[ERROR] --gpus=%d: the CLI drives one device; use bench.py for N>1\n", P.gpus);
         exit(EXIT_FAILURE);
@@ -165,22 +174,37 @@ int main(int argc, char** argv) {
     if (P.nthreads == 0) P.nthreads = 1;
     const int hthreads = (int) std::thread::hardware_concurrency();
 
+    // Relation creation in the order of src/main.c:402-468 (each relation seeded by -x / -y).
     relation_t relR, relS;
+    auto alloc = [](relation_t* rel, uint64_t n) {
+        rel->num_tuples = n;
+        rel->tuples     = (tuple_t*) malloc(sizeof(tuple_t) * (n ? n : 1));
+        if (!rel->tuples) {
+            perror("out of memory");
+            exit(EXIT_FAILURE);
+        }
+    };
+    auto check = [](int rc, const char* what) {
+        if (rc) {
+            printf("[ERROR] generating %s: %s\n", what, hwbrj_last_error());
+            exit(EXIT_FAILURE);
+        }
+    };
     fprintf(stdout, "[INFO ] %s relation R with size = %.3lf MiB, #tuples = %llu : ",
             P.loadS ? "Loading" : "Creating", 8.0 * P.r_size / 1024.0 / 1024.0,
             (unsigned long long) P.r_size);
     fflush(stdout);
+    uint64_t threshold = 0;
     if (P.loadR) {
         if (load_relation(&relR, P.loadR, P.r_size)) exit(EXIT_FAILURE);
+    } else if (fullrange || nonunique) {  // :421-427
+        threshold = hwbrj_nonunique_threshold(P.r_size, P.selectivity, fullrange);
+        alloc(&relR, P.r_size);
+        check(hwbrj_create_relation_nonunique(relR.tuples, P.r_size, (int64_t) threshold, P.r_seed), "R");
     } else {
-        relR.num_tuples = P.r_size;
-        relR.tuples     = (tuple_t*) malloc(sizeof(tuple_t) * (P.r_size ? P.r_size : 1));
-        if (!relR.tuples ||
-            hwbrj_generate_host(relR.tuples, P.r_size, P.nthreads, P.r_size, P.r_size, 1.0,
-                                P.r_seed, hthreads)) {
-            printf("[ERROR] generating R: %s\n", hwbrj_last_error());
-            exit(EXIT_FAILURE);
-        }
+        alloc(&relR, P.r_size);
+        check(hwbrj_generate_host(relR.tuples, P.r_size, P.nthreads, P.r_size, P.r_size, 1.0,
+                                  P.r_seed, hthreads), "R");
     }
     printf("OK \n");
     fprintf(stdout, "[INFO ] %s relation S with size = %.3lf MiB, #tuples = %lld : ",
@@ -189,15 +213,22 @@ int main(int argc, char** argv) {
     fflush(stdout);
     if (P.loadS) {
         if (load_relation(&relS, P.loadS, P.s_size)) exit(EXIT_FAILURE);
+    } else if (fullrange) {  // :448-450
+        alloc(&relS, P.s_size);
+        check(hwbrj_create_relation_fk_from_pk(relS.tuples, P.s_size, relR.tuples, relR.num_tuples,
+                                               (int64_t) threshold, P.selectivity, P.s_seed), "S");
+    } else if (nonunique) {  // :451-453
+        alloc(&relS, P.s_size);
+        check(hwbrj_create_relation_nonunique_from_pk(relS.tuples, P.s_size, relR.tuples,
+                                                      relR.num_tuples, (int64_t) threshold,
+                                                      P.selectivity, P.s_seed), "S");
+    } else if (P.skew > 0) {  // :457-460 (-q is ignored, as in the reference)
+        alloc(&relS, P.s_size);
+        check(hwbrj_create_relation_zipf(relS.tuples, P.s_size, P.r_size, P.skew, P.s_seed, hthreads), "S");
     } else {
-        relS.num_tuples = P.s_size;
-        relS.tuples     = (tuple_t*) malloc(sizeof(tuple_t) * (P.s_size ? P.s_size : 1));
-        if (!relS.tuples ||
-            hwbrj_generate_host(relS.tuples, P.s_size, P.nthreads, INT_MAX, P.r_size, P.selectivity,
-                                P.s_seed, hthreads)) {
-            printf("[ERROR] generating S: %s\n", hwbrj_last_error());
-            exit(EXIT_FAILURE);
-        }
+        alloc(&relS, P.s_size);
+        check(hwbrj_generate_host(relS.tuples, P.s_size, P.nthreads, INT_MAX, P.r_size, P.selectivity,
+                                  P.s_seed, hthreads), "S");
     }
     printf("OK \n");
     printf("[INFO ] Running join algorithm %s ...\n", P.algo.c_str());

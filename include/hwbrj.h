@@ -112,6 +112,29 @@ int hwbrj_generate_device_range(tuple_t * d_out, uint64_t n, uint64_t offset, ui
 int hwbrj_generate_host(tuple_t * out, uint64_t n, uint32_t nthreads, uint64_t maxid,
                         uint64_t threshold, double selectivity, uint64_t seed, int host_threads);
 
+/* ---- the reference's rand()-driven generators, on the host, bit-exact ----
+ * Each seeds its own restatement of glibc rand() (srand(seed), src/generator.c:75-81) and draws in
+ * the reference's order, so keys AND order equal the reference's relation for the same seed.
+ *   hwbrj_create_relation_nonunique          src/generator.c:585-605 (random_gen, :271-279):
+ *                                            keys in [0, maxid), payload = row
+ *   hwbrj_create_relation_nonunique_from_pk  src/generator.c:608-646 (--non-unique S)
+ *   hwbrj_create_relation_fk_from_pk         src/generator.c:531-582 (--full-range S)
+ *   hwbrj_create_relation_zipf               src/generator.c:659-676 + src/genzipf.c:28-158 (-z S);
+ *                                            payload = row (the reference leaves it uninitialised)
+ *   hwbrj_nonunique_threshold                src/main.c:421-427 (threshold for R and S) */
+uint64_t hwbrj_nonunique_threshold(uint64_t r_size, double selectivity, int full_range);
+int      hwbrj_create_relation_nonunique(tuple_t * out, uint64_t n, int64_t maxid, uint32_t seed);
+int      hwbrj_create_relation_nonunique_from_pk(tuple_t * out, uint64_t n, const tuple_t * pk,
+                                                 uint64_t npk, int64_t threshold,
+                                                 double selectivity, uint32_t seed);
+int      hwbrj_create_relation_fk_from_pk(tuple_t * out, uint64_t n, const tuple_t * pk,
+                                          uint64_t npk, int64_t threshold, double selectivity,
+                                          uint32_t seed);
+int      hwbrj_create_relation_zipf(tuple_t * out, uint64_t n, uint64_t alphabet_size,
+                                    double theta, uint32_t seed, int host_threads);
+/* The first n values rand() returns after srand(seed) (test hook for the restatement). */
+int      hwbrj_rand_stream(uint32_t seed, int32_t * out, uint64_t n);
+
 /* The filter built by the last join, in the reference's byte layout (src/bloom_filter.c:143-171:
  * m/8 bytes, bit h of a block at byte h>>3, bit h&7). nbytes must be m/8. */
 int hwbrj_export_filter(uint8_t * host_out, uint64_t nbytes);

@@ -12,6 +12,7 @@
 #include <stdatomic.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <math.h>
 #include <string.h>
 #include <time.h>
 
@@ -288,6 +289,126 @@ orc_shuffle_keys(int32_t * keys, uint64_t n, uint64_t seed)
         keys[i - 1]  = keys[j];
         keys[j]      = tmp;
     }
+}
+
+/* ------------------------------------------- rand()-driven generators (libc rand itself) */
+/* The reference calls glibc srand()/rand() (src/generator.c:75-81); so does this restatement, so
+ * the draws are the reference's by construction. Not thread-safe (libc's global state), like the
+ * reference's generator. */
+#define ORC_RAND_RANGE(O, N) ((O) + ((double) rand() / ((double) RAND_MAX + 1) * ((N) - (O))))
+
+/* src/generator.c:271-279 */
+static void
+orc_random_gen(orc_tuple_t * rel, uint64_t n, int64_t minid, int64_t maxid)
+{
+    for (uint64_t i = 0; i < n; i++) {
+        rel[i].key     = ORC_RAND_RANGE(minid, maxid);
+        rel[i].payload = i;
+    }
+}
+
+/* src/generator.c:99-109 */
+static void
+orc_knuth_shuffle(orc_tuple_t * rel, uint64_t n)
+{
+    int i;
+    for (i = n - 1; i > 0; i--) {
+        int64_t j    = ORC_RAND_RANGE(0, i);
+        int32_t tmp  = rel[i].key;
+        rel[i].key   = rel[j].key;
+        rel[j].key   = tmp;
+    }
+}
+
+/* src/generator.c:585-605 after srand(seed) (src/main.c:410) */
+void
+orc_gen_nonunique(orc_tuple_t * out, uint64_t n, int64_t maxid, uint32_t seed)
+{
+    srand(seed);
+    orc_random_gen(out, n, 0, maxid);
+}
+
+/* src/generator.c:608-646 */
+void
+orc_gen_nonunique_from_pk(orc_tuple_t * out, uint64_t n, const orc_tuple_t * pk, uint64_t npk,
+                          int64_t threshold, double selectivity, uint32_t seed)
+{
+    srand(seed);
+    uint64_t ntuples_above = n * (1 - selectivity);
+    orc_random_gen(out, ntuples_above, threshold + 1, 2147483647);
+    int i, j;
+    for (i = ntuples_above; i < (int) n; i++) {
+        j              = ORC_RAND_RANGE(0, npk);
+        out[i].key     = pk[j].key;
+        out[i].payload = i;
+    }
+    orc_knuth_shuffle(out, n);
+}
+
+/* src/generator.c:531-582 */
+void
+orc_gen_fk_from_pk(orc_tuple_t * out, uint64_t n, const orc_tuple_t * pk, uint64_t npk,
+                   int64_t threshold, double selectivity, uint32_t seed)
+{
+    srand(seed);
+    uint64_t ntuples_above = n * (1 - selectivity);
+    uint64_t ntuples_below = n - ntuples_above;
+    orc_random_gen(out + ntuples_below, ntuples_above, threshold + 1, 2147483647);
+    int iters = ntuples_below / npk, i;
+    for (i = 0; i < iters; i++) memcpy(out + i * npk, pk, npk * sizeof(orc_tuple_t));
+    int64_t remainder = ntuples_below % npk;
+    if (remainder > 0) memcpy(out + i * npk, pk, remainder * sizeof(orc_tuple_t));
+    orc_knuth_shuffle(out, n);
+}
+
+/* src/genzipf.c:28-158 (gen_alphabet, gen_zipf_lut, gen_zipf) via create_relation_zipf
+ * (src/generator.c:659-676). Payload = row (the reference leaves it uninitialised). */
+int
+orc_gen_zipf(orc_tuple_t * out, uint64_t n, unsigned int alphabet_size, double zipf_factor,
+             uint32_t seed)
+{
+    srand(seed);
+    uint32_t * alphabet = malloc(alphabet_size * sizeof(*alphabet));
+    double *   lut      = malloc(alphabet_size * sizeof(*lut));
+    if (!alphabet || !lut) {
+        free(alphabet);
+        free(lut);
+        return 1;
+    }
+    for (unsigned int i = 0; i < alphabet_size; i++) alphabet[i] = i + 1;
+    for (unsigned int i = alphabet_size - 1; i > 0; i--) {
+        unsigned int k   = (unsigned long) i * rand() / RAND_MAX;
+        unsigned int tmp = alphabet[i];
+        alphabet[i]      = alphabet[k];
+        alphabet[k]      = tmp;
+    }
+    double scaling_factor = 0.0, sum = 0.0;
+    for (unsigned int i = 1; i <= alphabet_size; i++) scaling_factor += 1.0 / pow(i, zipf_factor);
+    for (unsigned int i = 1; i <= alphabet_size; i++) {
+        sum += 1.0 / pow(i, zipf_factor);
+        lut[i - 1] = sum / scaling_factor;
+    }
+    for (uint64_t i = 0; i < n; i++) {
+        double       r    = ((double) rand()) / RAND_MAX;
+        unsigned int left = 0, right = alphabet_size - 1, m, pos;
+        if (lut[0] >= r)
+            pos = 0;
+        else {
+            while (right - left > 1) {
+                m = (left + right) / 2;
+                if (lut[m] < r)
+                    left = m;
+                else
+                    right = m;
+            }
+            pos = right;
+        }
+        out[i].key     = alphabet[pos];
+        out[i].payload = i;
+    }
+    free(lut);
+    free(alphabet);
+    return 0;
 }
 
 /* ------------------------------------------------------------- radix join */

@@ -62,6 +62,18 @@ int      orc_gen_keys(int32_t * keys, uint64_t num_tuples, uint32_t nthreads, ui
  * (src/generator.c:173-176), so any fixed seed is an equally valid order. */
 void     orc_shuffle_keys(int32_t * keys, uint64_t n, uint64_t seed);
 
+/* The rand()-driven generators (src/generator.c:531-646, :659-676, src/genzipf.c:28-158), calling
+ * libc srand(seed)/rand() exactly as the reference does. Payload = row (zipf: the reference leaves
+ * it uninitialised). */
+void     orc_gen_nonunique(orc_tuple_t * out, uint64_t n, int64_t maxid, uint32_t seed);
+void     orc_gen_nonunique_from_pk(orc_tuple_t * out, uint64_t n, const orc_tuple_t * pk,
+                                   uint64_t npk, int64_t threshold, double selectivity,
+                                   uint32_t seed);
+void     orc_gen_fk_from_pk(orc_tuple_t * out, uint64_t n, const orc_tuple_t * pk, uint64_t npk,
+                            int64_t threshold, double selectivity, uint32_t seed);
+int      orc_gen_zipf(orc_tuple_t * out, uint64_t n, unsigned int alphabet_size,
+                      double zipf_factor, uint32_t seed);
+
 typedef struct orc_timing_t {
     double total_usec;     /* src/parallel_radix_join_bloom.c:1521-1522 */
     double partition_usec; /* :1525-1527 */

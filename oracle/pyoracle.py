@@ -55,8 +55,43 @@ def lib() -> ctypes.CDLL:
         L.orc_bloom_popcount.argtypes = [ctypes.c_void_p]
         L.orc_bloom_args_invalid.restype = ctypes.c_int
         L.orc_bloom_args_invalid.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64]
+        L.orc_gen_nonunique.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int64,
+                                        ctypes.c_uint32]
+        for fn in (L.orc_gen_nonunique_from_pk, L.orc_gen_fk_from_pk):
+            fn.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64,
+                           ctypes.c_int64, ctypes.c_double, ctypes.c_uint32]
+        L.orc_gen_zipf.restype = ctypes.c_int
+        L.orc_gen_zipf.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint, ctypes.c_double,
+                                   ctypes.c_uint32]
         _L = L
     return _L
+
+
+def threshold(r_size: int, q: float, full_range: bool) -> int:
+    """src/main.c:421-427."""
+    import math
+    t = math.ceil(2147483647 * q)
+    return t if full_range else int(min(r_size, t))
+
+
+def reference_relations(r_size: int, s_size: int, q: float, mode: str, skew: float = 0.0,
+                        r_seed: int = 12345, s_seed: int = 54321):
+    """(R, S) of src/main.c:410-466 for mode 'nonunique' | 'fullrange' | 'zipf', drawn with libc
+    rand() itself. zipf: R = keys 1..r_size in order (its order does not matter)."""
+    L = lib()
+    R = np.empty((r_size, 2), dtype=np.int32)
+    S = np.empty((s_size, 2), dtype=np.int32)
+    if mode == "zipf":
+        R[:, 0] = np.arange(1, r_size + 1)
+        R[:, 1] = np.arange(r_size)
+        if L.orc_gen_zipf(S.ctypes.data, s_size, r_size, skew, s_seed):
+            raise MemoryError
+        return R, S
+    thr = threshold(r_size, q, mode == "fullrange")
+    L.orc_gen_nonunique(R.ctypes.data, r_size, thr, r_seed)
+    fn = L.orc_gen_fk_from_pk if mode == "fullrange" else L.orc_gen_nonunique_from_pk
+    fn(S.ctypes.data, s_size, R.ctypes.data, r_size, thr, q, s_seed)
+    return R, S
 
 
 class _Bloom(ctypes.Structure):  # orc_bloom_t

@@ -221,6 +221,58 @@ def test_bpro_host_boundary_stdout(hw, capfd):
     assert res.totalresults == g["results"]
 
 
+@pytest.fixture(scope="module")
+def gen3(hw):
+    """The rand()-driven relations of SURVEY.md s8c F3 (bit-exact reference generators, host)."""
+    g = json.load(open(os.path.join(HERE, "golden", "survey_counts.json")))["F3_generators"]
+    kw = dict(r_seed=g["r_seed"], s_seed=g["s_seed"], host_threads=8)
+    return g, {
+        "nonunique": hw.reference_relations(g["r"], g["s"], g["nonunique"]["q"], non_unique=True, **kw),
+        "fullrange": hw.reference_relations(g["r"], g["s"], 0.01, full_range=True, **kw),
+        "zipf": hw.reference_relations(g["r"], g["s"], skew=g["zipf"]["z"], **kw),
+    }
+
+
+@pytest.mark.parametrize("mode", ["nonunique", "zipf"])
+def test_generator_goldens(hw, cuda, gen3, mode):
+    g, rels = gen3
+    R, S = rels[mode]
+    row = g[mode]
+    st = hw.join_device(to_dev(cuda, R), to_dev(cuda, S), hw.BloomFilterArgs(hw.BLOCKED, g["m"], row["k"], g["B"]))
+    assert (st.filtered, st.matches) == (row["filtered"], row["results"])
+
+
+@pytest.mark.parametrize("mode", ["nonunique", "fullrange", "zipf"])
+@pytest.mark.parametrize("a", [None, ("basic", 1 << 24, 1, 0), ("blocked", 1 << 24, 3, 512),
+                               ("sectorized", 1 << 24, 2, 1024)], ids=str)
+def test_generator_relations_vs_oracle(hw, cuda, orc, gen3, mode, a):
+    """Duplicate build keys (non-unique / full-range R) and heavy probe skew (Zipf S)."""
+    R, S = gen3[1][mode]
+    args = mk(hw, a)
+    st = hw.join_device(to_dev(cuda, R), to_dev(cuda, S), args)
+    if args is None:
+        res, filt, _ = orc.bpro(R, S, 8, 0, 0, 0, 0, use_bloom=False)
+    else:
+        res, filt, _ = orc.bpro(R, S, 8, args.variant, args.m, args.k, args.B)
+    assert (st.filtered, st.matches) == (filt, res)
+
+
+def test_cli_generator_flags_end_to_end(hw):
+    g = json.load(open(os.path.join(HERE, "golden", "survey_counts.json")))["F3_generators"]
+    row = g["nonunique"]
+    out = subprocess.run([hw.CLI_PATH, "-a", "PRO", "-r", str(g["r"]), "-s", str(g["s"]), "-q", str(row["q"]),
+                          "--non-unique", "-b", "blocked", "-m", str(g["m"]), "-k", "1"],
+                         capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert f"S-tuples after filter: {row['filtered']}" in out.stdout
+    assert f"[INFO ] Results = {row['results']}. DONE." in out.stdout
+    out = subprocess.run([hw.CLI_PATH, "-r", str(g["r"]), "-s", str(g["s"] // 4), "-z", "0.75",
+                          "-b", "blocked", "-m", str(g["m"]), "-k", "1"],
+                         capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert f"[INFO ] Results = {g['s'] // 4}. DONE." in out.stdout
+
+
 def test_cli_end_to_end(hw):
     g = GOLD["F3_grid"]
     out = subprocess.run([hw.CLI_PATH, "-a", "PRO", "-r", str(g["r"]), "-s", str(g["s"]), "-q", "0.01",
