@@ -17,7 +17,7 @@ import numpy as np
 
 __all__ = [
     "BASIC", "BLOCKED", "SECTORIZED", "BloomFilterArgs", "Relation", "Result", "Stats",
-    "BPRO", "PRO", "assert_args", "join_device", "generate_device", "generate_device_range",
+    "BPRO", "PRO", "BPRH", "BPRHO", "BRJ", "PRH", "PRHO", "RJ", "assert_args", "join_device", "generate_device", "generate_device_range",
     "generate_host", "nonunique_threshold", "create_relation_nonunique",
     "create_relation_nonunique_from_pk", "create_relation_fk_from_pk", "create_relation_zipf",
     "rand_stream", "reference_relations",
@@ -77,6 +77,12 @@ def lib() -> ctypes.CDLL:
                            ctypes.POINTER(_BloomArgs)]
         L.PRO.restype = ctypes.POINTER(_Result)
         L.PRO.argtypes = [ctypes.POINTER(_Relation), ctypes.POINTER(_Relation), ctypes.c_int]
+        for nm in ("BPRH", "BPRHO", "BRJ"):
+            getattr(L, nm).restype = ctypes.POINTER(_Result)
+            getattr(L, nm).argtypes = L.BPRO.argtypes
+        for nm in ("PRH", "PRHO", "RJ"):
+            getattr(L, nm).restype = ctypes.POINTER(_Result)
+            getattr(L, nm).argtypes = L.PRO.argtypes
         L.assert_args.argtypes = [ctypes.POINTER(_BloomArgs)]
         L.hwbrj_join_device.restype = ctypes.c_int
         L.hwbrj_join_device.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
@@ -218,6 +224,42 @@ def PRO(relR: Relation, relS: Relation, nthreads: int) -> Result:
     out = Result(r.contents.totalresults, r.contents.nthreads)
     ctypes.CDLL(None).free(r)
     return out
+
+
+def _run(name: str, relR: Relation, relS: Relation, nthreads: int, args=None) -> Result:
+    fn = getattr(lib(), name)
+    r = (fn(ctypes.byref(relR._c), ctypes.byref(relS._c), int(nthreads), ctypes.byref(args._c()))
+         if args is not None else fn(ctypes.byref(relR._c), ctypes.byref(relS._c), int(nthreads)))
+    out = Result(r.contents.totalresults, r.contents.nthreads)
+    ctypes.CDLL(None).free(r)
+    return out
+
+
+def BPRH(relR, relS, nthreads, args):
+    """src/parallel_radix_join_bloom.c:1789-1795 (same MI355X operator as BPRO)."""
+    return _run("BPRH", relR, relS, nthreads, args)
+
+
+def BPRHO(relR, relS, nthreads, args):
+    """src/parallel_radix_join_bloom.c:1797-1804 (same MI355X operator as BPRO)."""
+    return _run("BPRHO", relR, relS, nthreads, args)
+
+
+def BRJ(relR, relS, nthreads, args):
+    """src/parallel_radix_join_bloom.c:1806-1930 (same MI355X operator as BPRO)."""
+    return _run("BRJ", relR, relS, nthreads, args)
+
+
+def PRH(relR, relS, nthreads):
+    return _run("PRH", relR, relS, nthreads)
+
+
+def PRHO(relR, relS, nthreads):
+    return _run("PRHO", relR, relS, nthreads)
+
+
+def RJ(relR, relS, nthreads):
+    return _run("RJ", relR, relS, nthreads)
 
 
 def _ptr(t) -> int:

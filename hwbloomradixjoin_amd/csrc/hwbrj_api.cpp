@@ -227,6 +227,29 @@ result_t* PRO(relation_t* relR, relation_t* relS, int nthreads) {
     return run_host_join(relR, relS, nthreads, nullptr);
 }
 
+// The other entries of the reference's algorithm table (src/main.c:331-339) that run the same
+// partitioned join: BPRH / BPRHO plug a different per-partition join function into the same
+// join_init_run (src/parallel_radix_join_bloom.c:1789-1804), BRJ is its single-threaded form
+// (:1806-1930). On the MI355X the per-partition join is always k_join, so they are this operator.
+result_t* BPRH(relation_t* relR, relation_t* relS, int nthreads, bloom_filter_args_t* a) {
+    return run_host_join(relR, relS, nthreads, a);
+}
+result_t* BPRHO(relation_t* relR, relation_t* relS, int nthreads, bloom_filter_args_t* a) {
+    return run_host_join(relR, relS, nthreads, a);
+}
+result_t* BRJ(relation_t* relR, relation_t* relS, int nthreads, bloom_filter_args_t* a) {
+    return run_host_join(relR, relS, nthreads, a);
+}
+result_t* PRH(relation_t* relR, relation_t* relS, int nthreads) {
+    return run_host_join(relR, relS, nthreads, nullptr);
+}
+result_t* PRHO(relation_t* relR, relation_t* relS, int nthreads) {
+    return run_host_join(relR, relS, nthreads, nullptr);
+}
+result_t* RJ(relation_t* relR, relation_t* relS, int nthreads) {
+    return run_host_join(relR, relS, nthreads, nullptr);
+}
+
 result_t* hwbrj_BPRO(relation_t* relR, relation_t* relS, int nthreads,
                      bloom_filter_args_t* bloom_filter_args) {
     return run_host_join(relR, relS, nthreads, bloom_filter_args);

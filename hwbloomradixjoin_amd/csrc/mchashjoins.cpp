@@ -3,7 +3,8 @@
 //
 // Differences from the reference driver (DESIGN.md "CLI"):
 //   -b sectorized    selects this build's SECTORIZED filter (the reference silently runs BASIC);
-//   -a               PRO is the only algorithm behind this boundary (others print an error);
+//   -a               PRO, PRH, PRHO and RJ all run the MI355X partitioned join (their CPU join
+//                    functions differ, their counts do not); NPO / NPO_st print an error;
 //   -z / --non-unique / --full-range relations are the reference's exactly (restated glibc
 //   rand() after srand(-x / -y), hwbrj_gen.cpp); the default PK/FK relations have the reference's
 //   key multiset in a seeded (-x / -y) Feistel order instead of the time-seeded Knuth shuffle
@@ -39,7 +40,7 @@ struct Params {
 static void print_help(const char* prog) {
     printf("Usage: %s [options]\n", prog);
     printf(
-        "    Join algorithm selection, algorithms : PRO (MI355X)                         \n"
+        "    Join algorithm selection, algorithms : PRO, PRH, PRHO, RJ (MI355X)          \n"
         "       -a --algo=<name>    Run the hash join algorithm named <name> [PRO]      \n"
         "                                                                               \n"
         "    Other join configuration options, with default values in [] :              \n"
@@ -132,9 +133,10 @@ int main(int argc, char** argv) {
     while ((c = getopt_long(argc, argv, "a:n:p:q:r:s:o:x:y:z:R:S:b:m:k:B:Z:A:hv", opts, &idx)) != -1) {
         switch (c) {
             case 0: break;
-            case 'a':
-                if (strcmp(optarg, "PRO") != 0) {
-                    printf("[ERROR] Join algorithm named `%s' does not exist in this build (PRO only)!\n",
+            case 'a':  // src/main.c:331-339 (NPO / NPO_st do not partition: not in this build)
+                if (strcmp(optarg, "PRO") != 0 && strcmp(optarg, "PRH") != 0 &&
+                    strcmp(optarg, "PRHO") != 0 && strcmp(optarg, "RJ") != 0) {
+                    printf("[ERROR] Join algorithm named `%s' does not exist in this build!\n",
                            optarg);
                     print_help(argv[0]);
                     exit(EXIT_SUCCESS);
@@ -232,8 +234,18 @@ int main(int argc, char** argv) {
     }
     printf("OK \n");
     printf("[INFO ] Running join algorithm %s ...\n", P.algo.c_str());
-    result_t* res = P.bloom ? BPRO(&relR, &relS, (int) P.nthreads, &P.bf)
-                            : PRO(&relR, &relS, (int) P.nthreads);
+    // src/main.c:331-339 algos[] and :473-478 (joinAlgoBloom when -b is not "no")
+    struct Algo {
+        const char* name;
+        result_t* (*join)(relation_t*, relation_t*, int);
+        result_t* (*bloom)(relation_t*, relation_t*, int, bloom_filter_args_t*);
+    };
+    static const Algo algos[] = {{"PRO", PRO, BPRO}, {"PRH", PRH, BPRH}, {"PRHO", PRHO, BPRHO}, {"RJ", RJ, BRJ}};
+    const Algo* algo = &algos[0];
+    for (const Algo& a : algos)
+        if (P.algo == a.name) algo = &a;
+    result_t* res = P.bloom ? algo->bloom(&relR, &relS, (int) P.nthreads, &P.bf)
+                            : algo->join(&relR, &relS, (int) P.nthreads);
     printf("[INFO ] Results = %llu. DONE.\n", (unsigned long long) res->totalresults);
     free(relR.tuples);
     free(relS.tuples);

@@ -69,6 +69,22 @@ result_t * BPRO(relation_t * relR, relation_t * relS, int nthreads,
                 bloom_filter_args_t * bloom_filter_args);
 result_t * PRO(relation_t * relR, relation_t * relS, int nthreads);
 void       assert_args(bloom_filter_args_t * args);
+/* The reference's other partitioned-join entries (src/main.c:331-339). They differ only in the
+ * per-partition join function the CPU build plugs into join_init_run (histogram-reorder build for
+ * PRH, + SIMD/prefetch probe for PRHO) or in running single-threaded (RJ); the counts are the
+ * same. On the MI355X the per-partition join is k_join for all of them, so they run BPRO / PRO.
+ *   BPRH, BPRHO   src/parallel_radix_join_bloom.h:68-87 (impl. :1789-1804)
+ *   BRJ           src/parallel_radix_join_bloom.c:1806-1930
+ *   PRH, PRHO, RJ src/parallel_radix_join.h:49-82 */
+result_t * BPRH(relation_t * relR, relation_t * relS, int nthreads,
+                bloom_filter_args_t * bloom_filter_args);
+result_t * BPRHO(relation_t * relR, relation_t * relS, int nthreads,
+                 bloom_filter_args_t * bloom_filter_args);
+result_t * BRJ(relation_t * relR, relation_t * relS, int nthreads,
+               bloom_filter_args_t * bloom_filter_args);
+result_t * PRH(relation_t * relR, relation_t * relS, int nthreads);
+result_t * PRHO(relation_t * relR, relation_t * relS, int nthreads);
+result_t * RJ(relation_t * relR, relation_t * relS, int nthreads);
 /* The same two operators under prefixed names, for linking next to the reference's own
  * parallel_radix_join*.o (which also define BPRO/PRO): see INTEGRATION.md. */
 result_t * hwbrj_BPRO(relation_t * relR, relation_t * relS, int nthreads,

@@ -219,6 +219,11 @@ def test_bpro_host_boundary_stdout(hw, capfd):
     assert "PARTITION-TIME-USECS, PROBE-TIME-USECS, JOIN-TIME-USECS:" in out
     res = hw.PRO(R, S, 2)
     assert res.totalresults == g["results"]
+    a = hw.BloomFilterArgs(hw.BLOCKED, g["m"], 1, 1024)
+    for fn in (hw.BPRH, hw.BPRHO, hw.BRJ):  # the other join_init_run entries: same counts
+        assert fn(R, S, 2, a).totalresults == g["results"]
+    for fn in (hw.PRH, hw.PRHO, hw.RJ):
+        assert fn(R, S, 2).totalresults == g["results"]
 
 
 @pytest.fixture(scope="module")
@@ -266,7 +271,7 @@ def test_cli_generator_flags_end_to_end(hw):
     assert out.returncode == 0, out.stdout + out.stderr
     assert f"S-tuples after filter: {row['filtered']}" in out.stdout
     assert f"[INFO ] Results = {row['results']}. DONE." in out.stdout
-    out = subprocess.run([hw.CLI_PATH, "-r", str(g["r"]), "-s", str(g["s"] // 4), "-z", "0.75",
+    out = subprocess.run([hw.CLI_PATH, "-a", "PRHO", "-r", str(g["r"]), "-s", str(g["s"] // 4), "-z", "0.75",
                           "-b", "blocked", "-m", str(g["m"]), "-k", "1"],
                          capture_output=True, text=True, timeout=600)
     assert out.returncode == 0, out.stdout + out.stderr
