@@ -243,7 +243,7 @@ void Engine::release() {
     for (DevBuf* b : {&poolR, &metaR, &usedR, &wgqcR, &wgqeR, &wgqoR, &lstartR, &estartR, &istartR,
                       &listR, &poolS, &metaS, &usedS, &wgqcS, &wgqeS, &wgqoS, &lstartS, &estartS,
                       &istartS, &listS, &slices, &bitmap, &rjoin, &rqs, &surv, &survcnt, &survoff,
-                      &dense, &small})
+                      &dense, &small, &colR, &colS})
         b->release();
     have_filter_ = false;
 }
@@ -274,6 +274,10 @@ int Engine::run(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     const uint64_t LR = (uint64_t) G * capR, LS = (uint64_t) G * capS;  // max chunks
     const uint64_t items_max = (LS / CH + F + 1) * nseg;
     // list entries hold a 27-bit chunk id (hwbrj_kernels.hip, K4); metas a 22-bit region offset
+    if (G > 512) {
+        set_last_error("more than 512 scatter workgroups (k_plan row groups)");
+        return 3;
+    }
     if (LS > (1ull << 27) || LR > (1ull << 27) || capS >= (1u << 22) || capR >= (1u << 22)) {
         set_last_error("relation too large for 27-bit chunk ids (|S| or |R| > ~4.2e9 tuples per GPU)");
         return 3;
@@ -289,7 +293,7 @@ int Engine::run(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     ok &= rjoin.ensure(nR * 4) && rqs.ensure((NJ + 1) * 8ull);
     ok &= surv.ensure(nseg * LS * 128) && survcnt.ensure(items_max * NSUB * 4) &&
           survoff.ensure(items_max * NSUB * 4);
-    ok &= small.ensure(64);
+    ok &= small.ensure(64) && colR.ensure(F * 12) && colS.ensure(F * 12);  // u64 elems | u32 chunks
     if (slice_mode) ok &= slices.ensure((uint64_t) F * nseg * g.seg_words * 4);
     if (g.mode == MODE_GLOBAL) ok &= bitmap.ensure(((g.m + 31) / 32) * 4) && dense.ensure(nS * 4);
     if (!ok) {
@@ -323,10 +327,11 @@ int Engine::run(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     sp.cap        = capR;
     launch_scatter(sp, SRC_TUPLES, SIDE_R, G, stream);
     HWBRJ_CHECK(hipEventRecord(ev_[1], stream));
-    launch_plan(wgqcR.as<uint32_t>(), wgqeR.as<uint32_t>(), G, g.log2F, CH, 1, wgqoR.as<uint32_t>(),
-                lstartR.as<uint32_t>(), estartR.as<uint64_t>(), istartR.as<uint32_t>(), stream);
+    launch_plan(wgqcR.as<uint32_t>(), wgqeR.as<uint32_t>(), G, g.log2F, wgqoR.as<uint32_t>(),
+                colR.as<uint32_t>() + 2 * F, colR.as<uint64_t>(), stream);
     launch_list_fill(metaR.as<uint32_t>(), usedR.as<uint32_t>(), capR, g.log2F, wgqoR.as<uint32_t>(),
-                     lstartR.as<uint32_t>(), listR.as<uint32_t>(), G, stream);
+                     colR.as<uint32_t>() + 2 * F, colR.as<uint64_t>(), CH, 1, lstartR.as<uint32_t>(),
+                     estartR.as<uint64_t>(), istartR.as<uint32_t>(), listR.as<uint32_t>(), G, stream);
     HWBRJ_CHECK(hipEventRecord(ev_[2], stream));
     BuildParams bp{};
     bp.g          = g;
@@ -367,10 +372,11 @@ int Engine::run(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     launch_scatter(sp, g.mode == MODE_GLOBAL ? SRC_CODES : SRC_TUPLES, SIDE_S, G, stream);
     sp.dbg = nullptr;
     HWBRJ_CHECK(hipEventRecord(ev_[4], stream));
-    launch_plan(wgqcS.as<uint32_t>(), wgqeS.as<uint32_t>(), G, g.log2F, CH, nseg, wgqoS.as<uint32_t>(),
-                lstartS.as<uint32_t>(), estartS.as<uint64_t>(), istartS.as<uint32_t>(), stream);
+    launch_plan(wgqcS.as<uint32_t>(), wgqeS.as<uint32_t>(), G, g.log2F, wgqoS.as<uint32_t>(),
+                colS.as<uint32_t>() + 2 * F, colS.as<uint64_t>(), stream);
     launch_list_fill(metaS.as<uint32_t>(), usedS.as<uint32_t>(), capS, g.log2F, wgqoS.as<uint32_t>(),
-                     lstartS.as<uint32_t>(), listS.as<uint32_t>(), G, stream);
+                     colS.as<uint32_t>() + 2 * F, colS.as<uint64_t>(), CH, nseg, lstartS.as<uint32_t>(),
+                     estartS.as<uint64_t>(), istartS.as<uint32_t>(), listS.as<uint32_t>(), G, stream);
     HWBRJ_CHECK(hipEventRecord(ev_[5], stream));
     ProbeParams pp{};
     pp.g               = g;

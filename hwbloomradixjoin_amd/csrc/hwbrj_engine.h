@@ -52,6 +52,7 @@ class Engine {
     // S side
     DevBuf poolS, metaS, usedS, wgqcS, wgqeS, wgqoS, lstartS, estartS, istartS, listS;
     DevBuf slices, bitmap, rjoin, rqs, surv, survcnt, survoff, dense, small, dbgP, dbgJ, dbgS;
+    DevBuf colR, colS;  // per-partition totals from k_plan: u64 elements [F], then u32 chunks [F]
 };
 
 Engine* engine_for_current_device();

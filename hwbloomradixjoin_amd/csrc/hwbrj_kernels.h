@@ -80,12 +80,15 @@ void   launch_probe_global(const uint2* S, uint64_t n, const Geometry& g, const 
 size_t scatter_lds_bytes(uint32_t log2F);
 enum { SIDE_R = 0, SIDE_S = 1 };  // which relation a scatter partitions (kernel name only)
 void   launch_scatter(const ScatterParams& p, int src, int side, uint32_t grid, hipStream_t st);
+// k_plan: per-(wg, q) list offsets + per-partition chunk / element totals (colc, cole);
+// k_list_fill: scans the totals into list / element / item starts [F + 1] and fills the lists.
 void   launch_list_fill(const uint32_t* meta, const uint32_t* wg_used, uint64_t cap,
-                        uint32_t log2F, const uint32_t* wgq_off, const uint32_t* list_start,
-                        uint32_t* list, uint32_t grid, hipStream_t st);
-void   launch_plan(const uint32_t* wgq_chunks, const uint32_t* wgq_elems, uint32_t G,
-                   uint32_t log2F, uint32_t CH, uint32_t nseg, uint32_t* wgq_off,
-                   uint32_t* list_start, uint64_t* elem_start, uint32_t* item_start,
+                        uint32_t log2F, const uint32_t* wgq_off, const uint32_t* colc,
+                        const uint64_t* cole, uint32_t CH, uint32_t nseg, uint32_t* list_start,
+                        uint64_t* elem_start, uint32_t* item_start, uint32_t* list, uint32_t grid,
+                        hipStream_t st);
+bool   launch_plan(const uint32_t* wgq_chunks, const uint32_t* wgq_elems, uint32_t G,
+                   uint32_t log2F, uint32_t* wgq_off, uint32_t* colc, uint64_t* cole,
                    hipStream_t st);
 uint32_t probe_chunks_per_item();
 size_t   probe_lds_bytes(const Geometry& g, uint32_t* stage_cap);

@@ -644,71 +644,57 @@ constexpr uint32_t kNoEntry    = 0xFFFFFFFFu;
 
 __device__ __forceinline__ uint32_t list_count(uint32_t e) { return (((e >> kListIdBits) - 1u) & 31u) + 1u; }
 
-// One block. Column-wise exclusive scan of the scatter's (workgroup x partition) matrices gives
-// every (wg, q) its offset inside q's chunk list; then list_start = excl-scan(chunks),
-// elem_start = excl-scan(elements), item_start = excl-scan(ceil(chunks / CH) * nseg) over q.
+// Column-wise exclusive scan of the scatter's (workgroup x partition) matrices: every (wg, q) gets
+// its offset inside q's chunk list, and every partition its chunk / element totals. A block takes
+// 64 partitions (lanes) x 16 row groups (waves): every row is loaded by an independent load, so the
+// scan costs one memory latency instead of one per workgroup row.
+constexpr uint32_t kPlanMaxRG = 32;  // rows per wave: G <= 16 * 32 scatter workgroups
+
 __global__ __launch_bounds__(1024) void k_plan(const uint32_t* __restrict__ wgq_chunks,
                                                const uint32_t* __restrict__ wgq_elems, uint32_t G,
-                                               uint32_t log2F, uint32_t CH, uint32_t nseg,
-                                               uint32_t* __restrict__ wgq_off, uint32_t* list_start,
-                                               uint64_t* elem_start, uint32_t* item_start) {
-    __shared__ uint32_t sc[1024];
-    __shared__ uint32_t si[1024];
-    __shared__ uint64_t se[1024];
+                                               uint32_t log2F, uint32_t* __restrict__ wgq_off,
+                                               uint32_t* __restrict__ colc,
+                                               uint64_t* __restrict__ cole) {
+    __shared__ uint32_t tc[16][64];
+    __shared__ uint64_t te[16][64];
     const uint32_t F = 1u << log2F;
-    const uint32_t t = threadIdx.x;
-    uint32_t c = 0, it = 0;
-    uint64_t e = 0;
-    if (t < F) {
-        uint32_t wg = 0;
-        for (; wg + 8 <= G; wg += 8) {
-            uint32_t cc[8], ee[8];
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint32_t col = blockIdx.x * 64 + lane;
+    const bool     okc = col < F;
+    const uint32_t RG  = (G + 15) / 16;
+    const uint32_t r0  = min(G, w * RG), r1 = min(G, r0 + RG);
+    uint32_t       pre[kPlanMaxRG];
+    uint32_t       c = 0;
+    uint64_t       e = 0;
 #pragma unroll
-            for (int j = 0; j < 8; j++) {
-                cc[j] = wgq_chunks[(wg + j) * F + t];
-                ee[j] = wgq_elems[(wg + j) * F + t];
-            }
-#pragma unroll
-            for (int j = 0; j < 8; j++) {
-                wgq_off[(wg + j) * F + t] = c;
-                c += cc[j];
-                e += ee[j];
-            }
-        }
-        for (; wg < G; wg++) {
-            wgq_off[wg * F + t] = c;
-            c += wgq_chunks[wg * F + t];
-            e += wgq_elems[wg * F + t];
-        }
-        it = ((c + CH - 1) / CH) * nseg;
+    for (uint32_t j = 0; j < kPlanMaxRG; j++) {
+        const uint32_t r  = r0 + j;
+        const bool     ok = okc && r < r1;
+        const uint32_t cc = ok ? wgq_chunks[(uint64_t) r * F + col] : 0u;
+        const uint32_t ee = ok ? wgq_elems[(uint64_t) r * F + col] : 0u;
+        pre[j] = c;
+        c += cc;
+        e += ee;
     }
-    sc[t] = c;
-    si[t] = it;
-    se[t] = e;
+    tc[w][lane] = c;
+    te[w][lane] = e;
     __syncthreads();
-    for (uint32_t off = 1; off < 1024; off <<= 1) {  // Hillis-Steele inclusive scan
-        uint32_t ac = 0, ai = 0;
-        uint64_t ae = 0;
-        if (t >= off) {
-            ac = sc[t - off];
-            ai = si[t - off];
-            ae = se[t - off];
+    uint32_t base = 0;
+    for (uint32_t v = 0; v < w; v++) base += tc[v][lane];
+#pragma unroll
+    for (uint32_t j = 0; j < kPlanMaxRG; j++) {
+        const uint32_t r = r0 + j;
+        if (okc && r < r1) wgq_off[(uint64_t) r * F + col] = base + pre[j];
+    }
+    if (w == 0 && okc) {
+        uint32_t tcs = 0;
+        uint64_t tes = 0;
+        for (int v = 0; v < 16; v++) {
+            tcs += tc[v][lane];
+            tes += te[v][lane];
         }
-        __syncthreads();
-        sc[t] += ac;
-        si[t] += ai;
-        se[t] += ae;
-        __syncthreads();
-    }
-    if (t < F) {
-        list_start[t + 1] = sc[t];
-        item_start[t + 1] = si[t];
-        elem_start[t + 1] = se[t];
-    }
-    if (t == 0) {
-        list_start[0] = 0;
-        item_start[0] = 0;
-        elem_start[0] = 0;
+        colc[col] = tcs;
+        cole[col] = tes;
     }
 }
 
@@ -724,7 +710,12 @@ __global__ __launch_bounds__(kLfThreads) void k_list_fill(const uint32_t* __rest
                                                           const uint32_t* __restrict__ wg_used,
                                                           uint64_t cap, uint32_t log2F,
                                                           const uint32_t* __restrict__ wgq_off,
-                                                          const uint32_t* __restrict__ list_start,
+                                                          const uint32_t* __restrict__ colc,
+                                                          const uint64_t* __restrict__ cole,
+                                                          uint32_t CH, uint32_t nseg,
+                                                          uint32_t* __restrict__ list_start,
+                                                          uint64_t* __restrict__ elem_start,
+                                                          uint32_t* __restrict__ item_start,
                                                           uint32_t* __restrict__ list) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const uint32_t F    = 1u << log2F;
@@ -736,9 +727,46 @@ __global__ __launch_bounds__(kLfThreads) void k_list_fill(const uint32_t* __rest
     uint32_t*      wtot = cur + F;            // [16] wave totals of the scan
     const uint32_t tid  = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t wg   = blockIdx.x;
-    for (uint32_t q = tid; q < F; q += kLfThreads) {
-        cur[q] = list_start[q] + wgq_off[wg * F + q];
-        cnt[q] = 0;
+    {
+        // exclusive scans over the F <= 1024 partitions of the column totals (k_plan): list starts
+        // (every block), element and probe-item starts (block 0 publishes all three)
+        __shared__ uint32_t sc_c[16], sc_i[16];
+        __shared__ uint64_t sc_e[16];
+        const uint32_t c  = tid < F ? colc[tid] : 0u;
+        const uint32_t it = ((c + CH - 1) / CH) * nseg;
+        const uint64_t e  = tid < F ? cole[tid] : 0ull;
+        uint32_t ic = wave_incl_scan(c), ii = wave_incl_scan(it);
+        uint64_t ie = e;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint64_t t = __shfl_up(ie, off, 64);
+            if ((int) lane >= off) ie += t;
+        }
+        if (lane == 63) {
+            sc_c[wave] = ic;
+            sc_i[wave] = ii;
+            sc_e[wave] = ie;
+        }
+        __syncthreads();
+        for (uint32_t v = 0; v < wave; v++) {
+            ic += sc_c[v];
+            ii += sc_i[v];
+            ie += sc_e[v];
+        }
+        if (tid < F) {
+            cur[tid] = ic - c + wgq_off[wg * F + tid];
+            cnt[tid] = 0;
+            if (wg == 0) {
+                list_start[tid + 1] = ic;
+                item_start[tid + 1] = ii;
+                elem_start[tid + 1] = ie;
+            }
+        }
+        if (wg == 0 && tid == 0) {
+            list_start[0] = 0;
+            item_start[0] = 0;
+            elem_start[0] = 0;
+        }
     }
     __syncthreads();
     const uint64_t region = (uint64_t) wg * cap;
@@ -1442,18 +1470,21 @@ void launch_scatter(const ScatterParams& p, int src, int side, uint32_t grid, hi
 }
 
 void launch_list_fill(const uint32_t* meta, const uint32_t* wg_used, uint64_t cap, uint32_t log2F,
-                      const uint32_t* wgq_off, const uint32_t* list_start, uint32_t* list,
-                      uint32_t grid, hipStream_t st) {
+                      const uint32_t* wgq_off, const uint32_t* colc, const uint64_t* cole,
+                      uint32_t CH, uint32_t nseg, uint32_t* list_start, uint64_t* elem_start,
+                      uint32_t* item_start, uint32_t* list, uint32_t grid, hipStream_t st) {
     const size_t lds = (kLfBatch + kLfBatch / 2 + 3 * (1u << log2F) + 16) * sizeof(uint32_t);
     (void) hipFuncSetAttribute((const void*) &k_list_fill, hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds);
-    k_list_fill<<<grid, kLfThreads, lds, st>>>(meta, wg_used, cap, log2F, wgq_off, list_start, list);
+    k_list_fill<<<grid, kLfThreads, lds, st>>>(meta, wg_used, cap, log2F, wgq_off, colc, cole, CH,
+                                               nseg, list_start, elem_start, item_start, list);
 }
 
-void launch_plan(const uint32_t* wgq_chunks, const uint32_t* wgq_elems, uint32_t G, uint32_t log2F,
-                 uint32_t CH, uint32_t nseg, uint32_t* wgq_off, uint32_t* list_start,
-                 uint64_t* elem_start, uint32_t* item_start, hipStream_t st) {
-    k_plan<<<1, 1024, 0, st>>>(wgq_chunks, wgq_elems, G, log2F, CH, nseg, wgq_off, list_start,
-                               elem_start, item_start);
+bool launch_plan(const uint32_t* wgq_chunks, const uint32_t* wgq_elems, uint32_t G, uint32_t log2F,
+                 uint32_t* wgq_off, uint32_t* colc, uint64_t* cole, hipStream_t st) {
+    if (G > 16 * kPlanMaxRG) return false;
+    const uint32_t F = 1u << log2F;
+    k_plan<<<(F + 63) / 64, 1024, 0, st>>>(wgq_chunks, wgq_elems, G, log2F, wgq_off, colc, cole);
+    return true;
 }
 
 size_t slice_lds_bytes(const Geometry& g) {
