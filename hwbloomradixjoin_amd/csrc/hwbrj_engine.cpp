@@ -242,7 +242,7 @@ Engine::~Engine() { release(); }
 void Engine::release() {
     for (DevBuf* b : {&poolR, &metaR, &usedR, &wgqcR, &wgqeR, &wgqoR, &lstartR, &estartR, &istartR,
                       &listR, &poolS, &metaS, &usedS, &wgqcS, &wgqeS, &wgqoS, &lstartS, &estartS,
-                      &istartS, &listS, &slices, &bitmap, &rjoin, &rqs, &surv, &survcnt, &survoff,
+                      &istartS, &listS, &slices, &bitmap, &rjoin, &rrun, &surv, &survcnt, &survoff,
                       &dense, &small, &colR, &colS})
         b->release();
     have_filter_ = false;
@@ -290,7 +290,9 @@ int Engine::run(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     ok &= poolS.ensure(LS * 128) && metaS.ensure(LS * 4) && listS.ensure(LS * 4);
     ok &= usedS.ensure(G * 4) && wgqcS.ensure(GF * 4) && wgqeS.ensure(GF * 4) && wgqoS.ensure(GF * 4);
     ok &= lstartS.ensure((F + 1) * 4) && estartS.ensure((F + 1) * 8) && istartS.ensure((F + 1) * 4);
-    ok &= rjoin.ensure(nR * 4) && rqs.ensure((NJ + 1) * 8ull);
+    const uint64_t BSW = build_chunks_per_sweep(), SLOT = build_sweep_slot();
+    const uint64_t sweeps_max = LR / BSW + F + 1;  // build sweeps over all R partitions
+    ok &= rjoin.ensure(sweeps_max * SLOT * 4) && rrun.ensure(2 * sweeps_max * NSUB * 4);
     ok &= surv.ensure(nseg * LS * 128) && survcnt.ensure(items_max * NSUB * 4) &&
           survoff.ensure(items_max * NSUB * 4);
     ok &= small.ensure(64) && colR.ensure(F * 12) && colS.ensure(F * 12);  // u64 elems | u32 chunks
@@ -330,7 +332,7 @@ int Engine::run(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     launch_plan(wgqcR.as<uint32_t>(), wgqeR.as<uint32_t>(), G, g.log2F, wgqoR.as<uint32_t>(),
                 colR.as<uint32_t>() + 2 * F, colR.as<uint64_t>(), stream);
     launch_list_fill(metaR.as<uint32_t>(), usedR.as<uint32_t>(), capR, g.log2F, wgqoR.as<uint32_t>(),
-                     colR.as<uint32_t>() + 2 * F, colR.as<uint64_t>(), CH, 1, lstartR.as<uint32_t>(),
+                     colR.as<uint32_t>() + 2 * F, colR.as<uint64_t>(), (uint32_t) BSW, 1, lstartR.as<uint32_t>(),
                      estartR.as<uint64_t>(), istartR.as<uint32_t>(), listR.as<uint32_t>(), G, stream);
     HWBRJ_CHECK(hipEventRecord(ev_[2], stream));
     BuildParams bp{};
@@ -341,8 +343,10 @@ int Engine::run(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     bp.list_start = lstartR.as<uint32_t>();
     bp.elem_start = estartR.as<uint64_t>();
     bp.slices     = slice_mode ? slices.as<uint32_t>() : nullptr;
-    bp.qs_off     = rqs.as<uint64_t>();
-    bp.out_codes  = rjoin.as<uint32_t>();
+    bp.sweep_start = istartR.as<uint32_t>();  // (R items = build sweeps)
+    bp.out_codes   = rjoin.as<uint32_t>();
+    bp.run_cnt     = rrun.as<uint32_t>();
+    bp.run_off     = rrun.as<uint32_t>() + sweeps_max * NSUB;
     launch_build(bp, F, stream);
     HWBRJ_CHECK(hipEventRecord(ev_[3], stream));
     // ---------------------------------------------------------------- S: pass-1 (+ probe)
@@ -406,7 +410,10 @@ int Engine::run(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     // -------------------------------------------------------------------------- join
     JoinParams jp{};
     jp.r_codes         = rjoin.as<uint32_t>();
-    jp.r_off           = rqs.as<uint64_t>();
+    jp.r_sweep_start   = istartR.as<uint32_t>();
+    jp.r_cnt           = rrun.as<uint32_t>();
+    jp.r_off           = rrun.as<uint32_t>() + sweeps_max * NSUB;
+    jp.slot            = (uint32_t) SLOT;
     jp.surv            = surv.as<uint32_t>();
     jp.surv_cnt        = survcnt.as<uint32_t>();
     jp.surv_off        = survoff.as<uint32_t>();

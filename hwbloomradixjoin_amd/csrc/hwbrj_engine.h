@@ -51,7 +51,7 @@ class Engine {
     DevBuf poolR, metaR, usedR, wgqcR, wgqeR, wgqoR, lstartR, estartR, istartR, listR;
     // S side
     DevBuf poolS, metaS, usedS, wgqcS, wgqeS, wgqoS, lstartS, estartS, istartS, listS;
-    DevBuf slices, bitmap, rjoin, rqs, surv, survcnt, survoff, dense, small, dbgP, dbgJ, dbgS;
+    DevBuf slices, bitmap, rjoin, rrun, surv, survcnt, survoff, dense, small, dbgP, dbgJ, dbgS;
     DevBuf colR, colS;  // per-partition totals from k_plan: u64 elements [F], then u32 chunks [F]
 };
 

@@ -35,8 +35,10 @@ struct BuildParams {
     const uint32_t*  list_start;  // [F + 1]
     const uint64_t*  elem_start;  // [F + 1]
     uint32_t*        slices;      // [F][nseg][seg_words]
-    uint64_t*        qs_off;      // [F * NSUB + 1] start of each (q, sub) run in out_codes
-    uint32_t*        out_codes;   // R codes grouped by (q, sub)
+    const uint32_t*  sweep_start; // [F + 1] first build sweep of each partition
+    uint32_t*        out_codes;   // [sweeps][kBSlot]: each sweep's R codes sorted by sub
+    uint32_t*        run_cnt;     // [sweeps][NSUB] codes of each (sweep, sub) run
+    uint32_t*        run_off;     // [sweeps][NSUB] run offset inside the sweep's slot
 };
 
 struct ProbeParams {
@@ -57,8 +59,10 @@ struct ProbeParams {
 };
 
 struct JoinParams {
-    const uint32_t* r_codes;      // R codes grouped by (q, sub)
-    const uint64_t* r_off;        // [F * NSUB + 1]
+    const uint32_t* r_codes;      // build sweep slots (BuildParams::out_codes)
+    const uint32_t* r_sweep_start;  // [F + 1]
+    const uint32_t* r_cnt;        // [sweeps][NSUB]
+    const uint32_t* r_off;        // [sweeps][NSUB]
     const uint32_t* surv;         // survivor runs written by k_probe
     const uint32_t* surv_cnt;
     const uint32_t* surv_off;
@@ -66,6 +70,7 @@ struct JoinParams {
     const uint32_t* list_start;   // S lists [F + 1]
     uint64_t        surv_seg_stride;
     uint32_t        nseg, CH, log2NSUB, hash_shift;
+    uint32_t        slot;         // r_codes words per build sweep
     uint32_t        bitmap;       // 1: keys fit the direct-address bitmap (32 - hash_shift <= 18)
     uint64_t*       result;
     uint64_t*       dbg;          // dev-only: per-workgroup phase cycles (HWBRJ_DBG), or nullptr
@@ -93,6 +98,8 @@ bool   launch_plan(const uint32_t* wgq_chunks, const uint32_t* wgq_elems, uint32
 uint32_t probe_chunks_per_item();
 size_t   probe_lds_bytes(const Geometry& g, uint32_t* stage_cap);
 size_t slice_lds_bytes(const Geometry& g);
+uint32_t build_chunks_per_sweep();  // R chunks per k_build sweep
+uint32_t build_sweep_slot();        // out_codes words per k_build sweep
 void   launch_build(const BuildParams& p, uint32_t F, hipStream_t st);
 void   launch_probe(const ProbeParams& p, uint32_t grid, hipStream_t st);
 void   launch_join(const JoinParams& p, uint32_t jobs, hipStream_t st);

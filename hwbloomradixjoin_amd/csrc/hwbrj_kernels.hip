@@ -20,6 +20,7 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "hwbrj_common.h"
 #include "hwbrj_kernels.h"
@@ -882,12 +883,21 @@ __device__ __forceinline__ uint32_t sweep_word(const Sweep<NPQ>& S, int j, int t
     return t == 0 ? S.v[j].x : t == 1 ? S.v[j].y : t == 2 ? S.v[j].z : S.v[j].w;
 }
 
-constexpr int      kPQ    = 8;
-constexpr uint32_t kSweep = 128u * kPQ;
 
 // ======================================================================== K6: R build
-// One workgroup per partition q. Filter bits of R go into an LDS slice segment (ds_or), the slice
-// is written once (coalesced); then R codes are written grouped by sub-partition.
+// One workgroup per partition q, one pass over q's chunk list per slice segment. The list is
+// walked in groups of kBPQ sweeps (kBSweep chunks each); a group's list entries and chunks are
+// loaded while the previous group is processed:
+//   * every word sets its filter bits in the LDS slice segment (ds_or), the segment is written
+//     once at the end (bloom add, src/bloom_filter.c:73-132);
+//   * in the last segment's pass every sweep's codes are counting-sorted by join sub-partition in
+//     an LDS stage and written coalesced to the sweep's own kBSlot-word slot of out_codes, with a
+//     (sweep, sub) run table (pass-2 of R, src/parallel_radix_join_bloom.c:703-748). The join reads
+//     (q, sub) as the sub's runs in the slots of q's sweeps.
+constexpr int      kBPQ    = 4;               // sweeps per group (chunk quads per thread)
+constexpr uint32_t kBSweep = 128u;            // chunks per sweep (8 threads per chunk)
+constexpr uint32_t kBSlot  = kBSweep * 32u;   // out_codes words per sweep (4096)
+
 template <int KIND>
 __global__ __launch_bounds__(1024) void k_build(BuildParams P) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -897,73 +907,87 @@ __global__ __launch_bounds__(1024) void k_build(BuildParams P) {
     const uint32_t  segw   = slices ? g.seg_words : 0;  // multiple of 4
     uint32_t*       slice  = lds;
     uint32_t*       inv    = slice + segw;
-    uint32_t*       subh   = inv + 128;   // NSUB
-    uint64_t*       subc   = (uint64_t*) (subh + 64);  // NSUB (8-byte aligned: segw, 128, 64 even)
+    uint32_t*       stage  = inv + 128;       // kBSlot
+    uint32_t*       cnt    = stage + kBSlot;  // 64: ranks of this sweep by sub
+    uint32_t*       offs   = cnt + 64;        // 65: exclusive offsets (+ total)
     const uint32_t  q      = blockIdx.x;
+    const int       tid    = threadIdx.x, lane = tid & 63;
     load_tab(inv, &P.tabs->inv[0][0]);
-    for (uint32_t i = threadIdx.x; i < NSUB; i += blockDim.x) subh[i] = 0;
+    if (tid < 64) cnt[tid] = 0;
     const uint32_t l0 = P.list_start[q], l1 = P.list_start[q + 1];
+    const uint32_t sw0  = P.sweep_start[q];
     const uint32_t nseg = slices ? g.nseg : 1;
+    constexpr uint32_t GRP = kBSweep * kBPQ;
     for (uint32_t seg = 0; seg < nseg; seg++) {
-        for (uint32_t i = threadIdx.x; i < segw; i += blockDim.x) slice[i] = 0;
+        for (uint32_t i = tid; i < segw; i += blockDim.x) slice[i] = 0;
         __syncthreads();
-        const bool last = seg + 1 == nseg;
-        for (uint32_t lb = l0; lb < l1; lb += kSweep) {
-            uint32_t      ent[kPQ];
-            Sweep<kPQ>    S;
-            load_list<kPQ>(P.list, lb, l1, ent);
-            load_chunks<kPQ>(P.pool, ent, S);
+        const bool  last = seg + 1 == nseg;
+        uint32_t    eA[kBPQ], eB[kBPQ];
+        Sweep<kBPQ> SA, SB;
+        if (l0 < l1) {
+            load_list_u<kBPQ>(P.list, l0, l1, eA);
+            load_chunks_u<kBPQ>(P.pool, eA, l0, l1, SA);
+        }
+        for (uint32_t lb = l0; lb < l1; lb += GRP) {
+            const uint32_t nb = min(lb + GRP, l1 - 1u);  // next group (re-reads the last entry past the end)
+            const uint32_t ne = min(nb + GRP, l1);
+            load_list_u<kBPQ>(P.list, nb, ne, eB);
+            load_chunks_u<kBPQ>(P.pool, eB, nb, ne, SB);
 #pragma unroll
-            for (int j = 0; j < kPQ; j++) {
+            for (int jj = 0; jj < kBPQ; jj++) {
+                const uint32_t sb = lb + (uint32_t) jj * kBSweep;  // first list position of the sweep
+                if (sb >= l1) break;  // uniform
+                uint32_t c[4], rk[4];
 #pragma unroll
                 for (int t = 0; t < 4; t++) {
-                    if ((uint32_t) t >= S.n[j]) continue;
-                    const uint32_t w = sweep_word(S, j, t);
-                    if (slices) {
+                    const bool     ok = (uint32_t) t < SA.n[jj];
+                    const uint32_t w  = sweep_word(SA, jj, t);
+                    if (slices && ok) {
                         const Loc L = locate<KIND>(w, g, inv);
                         if (L.seg == seg) apply_bits<KIND, true>(L, g, slice);
                     }
-                    if (last) {
-                        const uint32_t c = decode_k<KIND>(w, q, g.log2F);
-                        atomicAdd(&subh[(c >> g.sub_shift) & (NSUB - 1u)], 1u);
-                    }
+                    c[t]  = decode_k<KIND>(w, q, g.log2F);
+                    rk[t] = 0xFFFFFFFFu;
+                    if (last && ok) rk[t] = atomicAdd(&cnt[(c[t] >> g.sub_shift) & (NSUB - 1u)], 1u);
                 }
+                if (!last) continue;
+                const uint32_t sw = sw0 + (sb - l0) / kBSweep;
+                __syncthreads();  // B1: every rank of the sweep taken
+                if (tid < 64) {   // wave 0: run offsets and the (sweep, sub) run table
+                    const uint32_t cs   = (uint32_t) lane < NSUB ? cnt[lane] : 0u;
+                    const uint32_t incl = wave_incl_scan_dpp(cs);
+                    if ((uint32_t) lane < NSUB) {
+                        offs[lane] = incl - cs;
+                        const uint64_t r = (uint64_t) sw * NSUB + lane;
+                        P.run_cnt[r]     = cs;
+                        P.run_off[r]     = incl - cs;
+                        cnt[lane]        = 0;
+                    }
+                    if (lane == 63) offs[64] = incl;
+                }
+                __syncthreads();  // B2: offsets visible
+#pragma unroll
+                for (int t = 0; t < 4; t++)
+                    if (rk[t] != 0xFFFFFFFFu) stage[offs[(c[t] >> g.sub_shift) & (NSUB - 1u)] + rk[t]] = c[t];
+                __syncthreads();  // B3: the sweep is sorted
+                const uint32_t tot = offs[64];
+                uint32_t* __restrict__ dst = P.out_codes + (uint64_t) sw * kBSlot;
+                for (uint32_t i = tid; i < tot; i += blockDim.x) dst[i] = stage[i];
+            }
+#pragma unroll
+            for (int jj = 0; jj < kBPQ; jj++) {
+                SA.v[jj] = SB.v[jj];
+                SA.n[jj] = SB.n[jj];
+                eA[jj]   = eB[jj];
             }
         }
         __syncthreads();
         if (slices) {
             uint4*       dst = (uint4*) (P.slices + ((uint64_t) q * g.nseg + seg) * segw);
             const uint4* src = (const uint4*) slice;
-            for (uint32_t i = threadIdx.x; i < segw / 4; i += blockDim.x) dst[i] = src[i];
+            for (uint32_t i = tid; i < segw / 4; i += blockDim.x) dst[i] = src[i];
         }
         __syncthreads();
-    }
-    if (threadIdx.x == 0) {
-        uint64_t run = P.elem_start[q];
-        for (uint32_t s = 0; s < NSUB; s++) {
-            P.qs_off[(uint64_t) q * NSUB + s] = run;
-            subc[s] = run;
-            run += subh[s];
-        }
-        if (q == gridDim.x - 1) P.qs_off[(uint64_t) gridDim.x * NSUB] = run;
-    }
-    __syncthreads();
-    for (uint32_t lb = l0; lb < l1; lb += kSweep) {
-        uint32_t   ent[kPQ];
-        Sweep<kPQ> S;
-        load_list<kPQ>(P.list, lb, l1, ent);
-        load_chunks<kPQ>(P.pool, ent, S);
-#pragma unroll
-        for (int j = 0; j < kPQ; j++) {
-#pragma unroll
-            for (int t = 0; t < 4; t++) {
-                if ((uint32_t) t >= S.n[j]) continue;
-                const uint32_t c   = decode_k<KIND>(sweep_word(S, j, t), q, g.log2F);
-                const uint32_t s   = (c >> g.sub_shift) & (NSUB - 1u);
-                const uint64_t pos = atomicAdd((unsigned long long*) &subc[s], 1ull);
-                P.out_codes[pos]   = c;
-            }
-        }
     }
 }
 
@@ -1258,8 +1282,6 @@ constexpr uint32_t kJoinWords   = 1u << (kJoinBmLog2 - 5);  // 8192 LDS words (3
 constexpr uint32_t kJoinLog2T   = 13;                  // hash path: 8192 slots in the same words
 constexpr uint32_t kJoinT       = 1u << kJoinLog2T;
 constexpr uint32_t kJoinPiece   = kJoinT / 2;
-constexpr int      kJoinRB      = 16;                  // R codes per thread per batch
-constexpr int      kJoinRuns    = 4;                   // survivor runs in flight per wave
 constexpr uint32_t kJoinDesc    = kJoinThreads;        // run descriptors per batch
 constexpr uint32_t kEmpty       = 0xFFFFFFFFu;  // codes of one job share their low hash_shift >= 1
                                                 // bits, so (code >> hash_shift) never equals it
@@ -1284,22 +1306,65 @@ __device__ __forceinline__ void join_insert(uint32_t* keys, uint32_t v) {
 
 __global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
     __shared__ __attribute__((aligned(16))) uint32_t tab[kJoinWords];  // bitmap or hash table
-    __shared__ uint64_t dbase[kJoinDesc];  // survivor run start (words) of each item in the batch
+    __shared__ uint64_t dbase[kJoinDesc];  // run starts (words) of a batch: S survivor runs
     __shared__ uint32_t dcnt[kJoinDesc];
+    __shared__ uint64_t rbase[kJoinDesc];  // R runs (one per build sweep of q)
+    __shared__ uint32_t rcnt[kJoinDesc];
+    __shared__ uint32_t pend[kJoinDesc + 1];  // hash path: piece boundaries inside an R batch
     __shared__ uint64_t wsum[kJoinWaves];
-    __shared__ uint32_t dupflag;
+    __shared__ uint32_t dupflag, npieces;
     const uint32_t NSUB = 1u << P.log2NSUB;
     const uint32_t job  = blockIdx.x, q = job >> P.log2NSUB, s = job & (NSUB - 1u);
-    const uint64_t r0 = P.r_off[job], r1 = P.r_off[job + 1];
+    const uint32_t w0 = P.r_sweep_start[q], w1 = P.r_sweep_start[q + 1];
     const uint32_t i0 = P.item_start[q], i1 = P.item_start[q + 1];
-    if (r1 == r0 || i1 == i0) return;
+    if (w1 == w0 || i1 == i0) return;
     const uint32_t lq0 = P.list_start[q];
     const uint32_t npc = (i1 - i0) / P.nseg;  // probe pieces of q (items are segment-major)
     const uint32_t sh  = P.hash_shift;
     const int      tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     uint64_t       cnt = 0;
-    // counts the survivors of (q, s) against the table: bitmap (BM) or hash table
-    auto probe_runs = [&](bool BM) {
+    // Every word of runs [da, db) of a descriptor batch through op(word): a wave per run, RUNS runs
+    // in flight per wave with WPL words per lane each; longer runs finish in a tail loop.
+    auto walk = [&](auto runs_c, auto wpl_c, const uint32_t* data, const uint32_t* nc,
+                    const uint64_t* nb, uint32_t da, uint32_t db, auto&& op) {
+        constexpr int RUNS = decltype(runs_c)::value, WPL = decltype(wpl_c)::value;
+        for (uint32_t d = da + wave; d < db; d += kJoinWaves * RUNS) {
+            uint32_t v[RUNS][WPL], n[RUNS];
+#pragma unroll
+            for (int r = 0; r < RUNS; r++) {
+                const uint32_t dd = d + r * kJoinWaves;
+                n[r]              = dd < db ? nc[dd] : 0u;
+                const uint64_t bb = dd < db ? nb[dd] : 0ull;
+#pragma unroll
+                for (int j = 0; j < WPL; j++) {
+                    const uint32_t o = lane + 64u * j;
+                    v[r][j]          = o < n[r] ? data[bb + o] : 0u;
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < RUNS; r++) {
+#pragma unroll
+                for (int j = 0; j < WPL; j++)
+                    if (lane + 64u * j < n[r]) op(v[r][j] >> sh);
+                if (n[r] > 64u * WPL) {
+                    const uint64_t bb = nb[d + r * kJoinWaves];
+                    for (uint32_t o = 64u * WPL + lane; o < n[r]; o += 64) op(data[bb + o] >> sh);
+                }
+            }
+        }
+    };
+#ifndef HWBRJ_JRR
+#define HWBRJ_JRR 4
+#define HWBRJ_JRW 4
+#define HWBRJ_JSR 8
+#define HWBRJ_JSW 2
+#endif
+    using RR = std::integral_constant<int, HWBRJ_JRR>;  // R runs in flight per wave
+    using RW = std::integral_constant<int, HWBRJ_JRW>;  // R words per lane per run
+    using SR = std::integral_constant<int, HWBRJ_JSR>;  // survivor runs in flight per wave
+    using SW = std::integral_constant<int, HWBRJ_JSW>;
+    // the survivors of (q, s), batch by batch, against the table: bitmap (BM) or hash table
+    auto probe_survivors = [&](bool BM) {
         for (uint32_t d0 = i0; d0 < i1; d0 += kJoinDesc) {
             const uint32_t nd = min(kJoinDesc, i1 - d0);
             __syncthreads();  // previous descriptors consumed
@@ -1313,72 +1378,70 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
                              P.surv_off[(uint64_t) it * NSUB + s];
             }
             __syncthreads();
-            for (uint32_t d = wave; d < nd; d += kJoinWaves * kJoinRuns) {
-                uint32_t v[kJoinRuns][2], n[kJoinRuns];
-#pragma unroll
-                for (int r = 0; r < kJoinRuns; r++) {
-                    const uint32_t dd = d + r * kJoinWaves;
-                    n[r]              = dd < nd ? dcnt[dd] : 0u;
-                    const uint64_t bb = dd < nd ? dbase[dd] : 0ull;
-#pragma unroll
-                    for (int j = 0; j < 2; j++) {
-                        const uint32_t o = lane + 64u * j;
-                        v[r][j]          = o < n[r] ? P.surv[bb + o] : 0u;
-                    }
-                }
-#pragma unroll
-                for (int r = 0; r < kJoinRuns; r++) {
-#pragma unroll
-                    for (int j = 0; j < 2; j++) {
-                        if (lane + 64u * j >= n[r]) continue;
-                        const uint32_t x = v[r][j] >> sh;
-                        cnt += BM ? (tab[x >> 5] >> (x & 31u)) & 1u : join_count(tab, x);
-                    }
-                    if (n[r] > 128) {  // long run (e.g. no filter): tail
-                        const uint64_t bb = dbase[d + r * kJoinWaves];
-                        for (uint32_t o = 128 + lane; o < n[r]; o += 64) {
-                            const uint32_t x = P.surv[bb + o] >> sh;
-                            cnt += BM ? (tab[x >> 5] >> (x & 31u)) & 1u : join_count(tab, x);
-                        }
-                    }
-                }
-            }
+            if (BM) walk(SR{}, SW{}, P.surv, dcnt, dbase, 0, nd, [&](uint32_t x) { cnt += (tab[x >> 5] >> (x & 31u)) & 1u; });
+            else walk(SR{}, SW{}, P.surv, dcnt, dbase, 0, nd, [&](uint32_t x) { cnt += join_count(tab, x); });
         }
     };
+    // R run descriptors of a batch
+    auto load_r = [&](uint32_t d0, uint32_t nd) {
+        __syncthreads();  // previous R descriptors consumed
+        uint32_t c = 0;
+        if ((uint32_t) tid < nd) {
+            const uint64_t r = (uint64_t) (d0 + tid) * NSUB + s;
+            c                = P.r_cnt[r];
+            rcnt[tid]        = c;
+            rbase[tid]       = (uint64_t) (d0 + tid) * P.slot + P.r_off[r];
+        }
+        (void) c;
+        __syncthreads();
+    };
     bool hashed = !P.bitmap;
-    if (!hashed) {
+    if (!hashed) {  // every R key sets bit v; a bit already set means a duplicate key
         for (uint32_t i = tid; i < kJoinWords / 4; i += kJoinThreads) ((uint4*) tab)[i] = make_uint4(0, 0, 0, 0);
         if (tid == 0) dupflag = 0;
-        __syncthreads();
         uint32_t dup = 0;
-        for (uint64_t b = r0 + tid; b < r1; b += (uint64_t) kJoinThreads * kJoinRB) {
-            uint32_t c[kJoinRB];
-#pragma unroll
-            for (int j = 0; j < kJoinRB; j++) {
-                const uint64_t i = b + (uint64_t) j * kJoinThreads;
-                c[j]             = i < r1 ? P.r_codes[i] : 0u;
-            }
-#pragma unroll
-            for (int j = 0; j < kJoinRB; j++) {
-                if (b + (uint64_t) j * kJoinThreads >= r1) continue;
-                const uint32_t x = c[j] >> sh, bit = 1u << (x & 31u);
+        for (uint32_t d0 = w0; d0 < w1; d0 += kJoinDesc) {
+            const uint32_t nd = min(kJoinDesc, w1 - d0);
+            load_r(d0, nd);
+            walk(RR{}, RW{}, P.r_codes, rcnt, rbase, 0, nd, [&](uint32_t x) {
+                const uint32_t bit = 1u << (x & 31u);
                 dup |= atomicOr(&tab[x >> 5], bit) & bit;
-            }
+            });
         }
         if (dup) dupflag = 1;
         __syncthreads();
         hashed = dupflag != 0;  // uniform
-        if (!hashed) probe_runs(true);
+        if (!hashed) probe_survivors(true);
     }
-    if (hashed) {  // duplicate R keys (or keys too wide for the bitmap): counting hash table
-        for (uint64_t rb = r0; rb < r1; rb += kJoinPiece) {
-            const uint64_t re = min(r1, rb + kJoinPiece);
+    if (hashed) {  // duplicate R keys (or keys too wide for the bitmap): counting hash table over
+                   // pieces of consecutive R runs holding <= kJoinPiece keys (a run has <= slot)
+        for (uint32_t d0 = w0; d0 < w1; d0 += kJoinDesc) {
+            const uint32_t nd = min(kJoinDesc, w1 - d0);
+            load_r(d0, nd);
+            if (tid == 0) {
+                uint32_t np = 0, acc = 0;
+                pend[0] = 0;
+                for (uint32_t d = 0; d < nd; d++) {
+                    if (acc + rcnt[d] > kJoinPiece && acc > 0) {
+                        pend[++np] = d;
+                        acc        = 0;
+                    }
+                    acc += rcnt[d];
+                }
+                pend[++np] = nd;
+                npieces    = np;
+            }
             __syncthreads();
-            for (uint32_t i = tid; i < kJoinT / 4; i += kJoinThreads)
-                ((uint4*) tab)[i] = make_uint4(kEmpty, kEmpty, kEmpty, kEmpty);
-            __syncthreads();
-            for (uint64_t i = rb + tid; i < re; i += kJoinThreads) join_insert(tab, P.r_codes[i] >> sh);
-            probe_runs(false);  // (starts with a barrier: the table is complete)
+            const uint32_t np = npieces;
+            for (uint32_t pc = 0; pc < np; pc++) {
+                const uint32_t da = pend[pc], db = pend[pc + 1];
+                __syncthreads();
+                for (uint32_t i = tid; i < kJoinT / 4; i += kJoinThreads)
+                    ((uint4*) tab)[i] = make_uint4(kEmpty, kEmpty, kEmpty, kEmpty);
+                __syncthreads();
+                walk(RR{}, RW{}, P.r_codes, rcnt, rbase, da, db, [&](uint32_t x) { join_insert(tab, x); });
+                probe_survivors(false);  // (starts with a barrier: the table is complete)
+            }
         }
     }
     cnt = wave_sum_u64(cnt);
@@ -1489,8 +1552,11 @@ bool launch_plan(const uint32_t* wgq_chunks, const uint32_t* wgq_elems, uint32_t
 
 size_t slice_lds_bytes(const Geometry& g) {
     const bool slices = g.mode == MODE_SLICE_BLOCK || g.mode == MODE_SLICE_BASIC;
-    return ((slices ? g.seg_words : 0) + 128 + 64 + 2 * 64 + 4) * sizeof(uint32_t);
+    return ((slices ? g.seg_words : 0) + 128 + kBSlot + 64 + 65) * sizeof(uint32_t);
 }
+
+uint32_t build_chunks_per_sweep() { return kBSweep; }
+uint32_t build_sweep_slot() { return kBSlot; }
 
 int consumer_kind(const Geometry& g) {
     if (g.mode == MODE_SLICE_BASIC) return KIND_BASIC_K1;
