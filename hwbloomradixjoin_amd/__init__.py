@@ -17,7 +17,7 @@ import numpy as np
 
 __all__ = [
     "BASIC", "BLOCKED", "SECTORIZED", "BloomFilterArgs", "Relation", "Result", "Stats",
-    "BPRO", "PRO", "BPRH", "BPRHO", "BRJ", "PRH", "PRHO", "RJ", "assert_args", "join_device", "generate_device", "generate_device_range",
+    "BPRO", "PRO", "join_materialize_device", "set_materialize", "BPRH", "BPRHO", "BRJ", "PRH", "PRHO", "RJ", "assert_args", "join_device", "generate_device", "generate_device_range",
     "generate_host", "nonunique_threshold", "create_relation_nonunique",
     "create_relation_nonunique_from_pk", "create_relation_fk_from_pk", "create_relation_zipf",
     "rand_stream", "reference_relations",
@@ -88,6 +88,14 @@ def lib() -> ctypes.CDLL:
         L.hwbrj_join_device.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
                                         ctypes.c_uint64, ctypes.POINTER(_BloomArgs),
                                         ctypes.c_void_p, ctypes.POINTER(_Stats)]
+        L.hwbrj_join_materialize_device.restype = ctypes.c_int
+        L.hwbrj_join_materialize_device.argtypes = [
+            ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64,
+            ctypes.POINTER(_BloomArgs), ctypes.c_void_p, ctypes.c_uint64,
+            ctypes.POINTER(ctypes.c_uint64), ctypes.c_void_p, ctypes.POINTER(_Stats),
+            ctypes.POINTER(ctypes.c_double)]
+        L.hwbrj_set_materialize.restype = None
+        L.hwbrj_set_materialize.argtypes = [ctypes.c_int]
         L.hwbrj_generate_device.restype = ctypes.c_int
         L.hwbrj_generate_device.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
                                             ctypes.c_uint64, ctypes.c_uint64, ctypes.c_double,
@@ -159,9 +167,71 @@ class BloomFilterArgs:
 
 @dataclass
 class Result:
-    """src/types.h:59-63 (count-only: resultlist is NULL in the reference's default build)."""
+    """src/types.h:59-63. `pairs` holds the materialized {R.payload, S.payload} result
+    (JOIN_RESULT_MATERIALIZE, see set_materialize), else None (the reference's default build)."""
     totalresults: int
     nthreads: int
+    pairs: Optional[np.ndarray] = None
+
+
+class _TupleBuffer(ctypes.Structure):  # src/tuple_buffer.h:27-30
+    pass
+
+
+_TupleBuffer._fields_ = [("tuples", ctypes.POINTER(_Tuple)), ("next", ctypes.POINTER(_TupleBuffer))]
+
+
+class _ChainedTupleBuffer(ctypes.Structure):  # src/tuple_buffer.h:32-40
+    _fields_ = [("buf", ctypes.POINTER(_TupleBuffer)), ("readcursor", ctypes.POINTER(_TupleBuffer)),
+                ("writecursor", ctypes.POINTER(_TupleBuffer)), ("writepos", ctypes.c_uint32),
+                ("readpos", ctypes.c_uint32), ("readlen", ctypes.c_uint32),
+                ("numbufs", ctypes.c_uint32)]
+
+
+class _ThreadResult(ctypes.Structure):  # src/types.h:51-56
+    _fields_ = [("nresults", ctypes.c_int64), ("results", ctypes.c_void_p),
+                ("threadid", ctypes.c_uint32)]
+
+
+_CB_TUPLES = 1024 * 1024  # CHAINEDBUFF_NUMTUPLESPERBUF
+
+
+def _take_result(r) -> Result:
+    """Copy a result_t (and its chained result buffers, if materialized) and free it."""
+    libc = ctypes.CDLL(None)
+    res = r.contents
+    pairs = None
+    if res.resultlist:
+        tl = ctypes.cast(res.resultlist, ctypes.POINTER(_ThreadResult))
+        parts = []
+        for t in range(res.nthreads):
+            cb = ctypes.cast(tl[t].results, ctypes.POINTER(_ChainedTupleBuffer)).contents
+            n, b, first = tl[t].nresults, cb.buf, True
+            while b and n > 0:  # cb_begin / cb_read_next order: newest buffer first
+                take = min(n, cb.writepos if first else _CB_TUPLES)
+                a = np.ctypeslib.as_array(ctypes.cast(b.contents.tuples, ctypes.POINTER(ctypes.c_int32)),
+                                          shape=(take * 2,))
+                parts.append(a.reshape(-1, 2).copy())
+                n -= take
+                b, first = b.contents.next, False
+            addr = ctypes.cast(cb.buf, ctypes.c_void_p).value
+            while addr:  # (plain addresses: a ctypes field view would read freed memory)
+                b = ctypes.cast(addr, ctypes.POINTER(_TupleBuffer)).contents
+                nxt = ctypes.cast(b.next, ctypes.c_void_p).value
+                libc.free(ctypes.cast(b.tuples, ctypes.c_void_p))
+                libc.free(ctypes.c_void_p(addr))
+                addr = nxt
+            libc.free(ctypes.c_void_p(tl[t].results))
+        libc.free(ctypes.cast(res.resultlist, ctypes.c_void_p))
+        pairs = np.concatenate(parts) if parts else np.empty((0, 2), dtype=np.int32)
+    out = Result(res.totalresults, res.nthreads, pairs)
+    libc.free(r)
+    return out
+
+
+def set_materialize(on: bool) -> None:
+    """Materialize {R.payload, S.payload} pairs in BPRO/PRO results (JOIN_RESULT_MATERIALIZE)."""
+    lib().hwbrj_set_materialize(1 if on else 0)
 
 
 @dataclass
@@ -212,27 +282,20 @@ def assert_args(args: BloomFilterArgs) -> bool:
 def BPRO(relR: Relation, relS: Relation, nthreads: int, args: BloomFilterArgs) -> Result:
     """src/parallel_radix_join_bloom.c:1781-1787 on the MI355X (prints the reference's lines)."""
     a = args._c()
-    r = lib().BPRO(ctypes.byref(relR._c), ctypes.byref(relS._c), int(nthreads), ctypes.byref(a))
-    out = Result(r.contents.totalresults, r.contents.nthreads)
-    ctypes.CDLL(None).free(r)
-    return out
+    return _take_result(lib().BPRO(ctypes.byref(relR._c), ctypes.byref(relS._c), int(nthreads),
+                                   ctypes.byref(a)))
 
 
 def PRO(relR: Relation, relS: Relation, nthreads: int) -> Result:
     """src/parallel_radix_join.c:1697-1700 (no filter) on the MI355X."""
-    r = lib().PRO(ctypes.byref(relR._c), ctypes.byref(relS._c), int(nthreads))
-    out = Result(r.contents.totalresults, r.contents.nthreads)
-    ctypes.CDLL(None).free(r)
-    return out
+    return _take_result(lib().PRO(ctypes.byref(relR._c), ctypes.byref(relS._c), int(nthreads)))
 
 
 def _run(name: str, relR: Relation, relS: Relation, nthreads: int, args=None) -> Result:
     fn = getattr(lib(), name)
     r = (fn(ctypes.byref(relR._c), ctypes.byref(relS._c), int(nthreads), ctypes.byref(args._c()))
          if args is not None else fn(ctypes.byref(relR._c), ctypes.byref(relS._c), int(nthreads)))
-    out = Result(r.contents.totalresults, r.contents.nthreads)
-    ctypes.CDLL(None).free(r)
-    return out
+    return _take_result(r)
 
 
 def BPRH(relR, relS, nthreads, args):
@@ -279,6 +342,26 @@ def join_device(R, S, args: Optional[BloomFilterArgs] = None, stream=None) -> St
                                  ctypes.byref(a) if a is not None else None, sp, ctypes.byref(st))
     _err(rc, "hwbrj_join_device")
     return Stats(**{n: getattr(st, n) for n, _ in _Stats._fields_})
+
+
+def join_materialize_device(R, S, args: Optional[BloomFilterArgs] = None, stream=None):
+    """(Stats, pairs): the join of device tensors R, S with its result materialized as a (n, 2)
+    int32 GPU tensor of {R.payload, S.payload} pairs, unordered (JOIN_RESULT_MATERIALIZE)."""
+    import torch
+    st = join_device(R, S, args, stream)
+    out = torch.empty((max(st.matches, 1), 2), dtype=torch.int32, device=R.device)
+    a = args._c() if args is not None else None
+    sp = ctypes.c_void_p(stream.cuda_stream) if stream is not None else None
+    n = ctypes.c_uint64()
+    st2 = _Stats()
+    ms = ctypes.c_double()
+    rc = lib().hwbrj_join_materialize_device(_ptr(R), R.shape[0], _ptr(S), S.shape[0],
+                                             ctypes.byref(a) if a is not None else None,
+                                             _ptr(out), out.shape[0], ctypes.byref(n), sp,
+                                             ctypes.byref(st2), ctypes.byref(ms))
+    _err(rc, "hwbrj_join_materialize_device")
+    stats = Stats(**{f: getattr(st2, f) for f, _ in _Stats._fields_})
+    return stats, out[: n.value], ms.value
 
 
 def generate_device(out, nthreads: int, maxid: int, threshold: int, selectivity: float,

@@ -59,6 +59,39 @@ int hwbrj_join_device(const tuple_t* d_R, uint64_t nR, const tuple_t* d_S, uint6
     return e->run((const uint2*) d_R, nR, (const uint2*) d_S, nS, args, (hipStream_t) stream, stats);
 }
 
+int hwbrj_join_materialize_device(const tuple_t* d_R, uint64_t nR, const tuple_t* d_S, uint64_t nS,
+                                  const bloom_filter_args_t* args, tuple_t* d_out,
+                                  uint64_t capacity, uint64_t* n_out, void* stream,
+                                  hwbrj_stats_t* stats, double* ms_materialize) {
+    Engine* e = engine_for_current_device();
+    if (!e) {
+        set_last_error("no HIP device");
+        return 10;
+    }
+    hwbrj_stats_t st;
+    int rc = e->run((const uint2*) d_R, nR, (const uint2*) d_S, nS, args, (hipStream_t) stream, &st);
+    if (rc) return rc;
+    if (stats) *stats = st;
+    uint64_t n = 0;
+    if ((uint64_t) st.matches > capacity) {
+        if (n_out) *n_out = (uint64_t) st.matches;
+        set_last_error("output capacity below the match count (*n_out holds the count)");
+        return 7;
+    }
+    rc = e->materialize((const uint2*) d_R, nR, (const uint2*) d_S, nS, (uint2*) d_out, capacity, &n,
+                        (hipStream_t) stream, ms_materialize);
+    if (rc) return rc;
+    if (n_out) *n_out = n;
+    if (n != (uint64_t) st.matches) {
+        set_last_error("materialized pairs differ from the counted matches");
+        return 8;
+    }
+    return 0;
+}
+
+static int g_materialize = -1;  // -1: from HWBRJ_MATERIALIZE
+void hwbrj_set_materialize(int on) { g_materialize = on ? 1 : 0; }
+
 int hwbrj_generate_device(tuple_t* d_out, uint64_t n, uint32_t nthreads, uint64_t maxid,
                           uint64_t threshold, double selectivity, uint64_t seed, void* stream) {
     Engine* e = engine_for_current_device();
@@ -161,6 +194,79 @@ static void print_timing(uint64_t total_cyc, uint64_t build_cyc, uint64_t part_c
     fflush(stdout);
 }
 
+// src/tuple_buffer.h:27-126: the reference's chained result buffers. The newest buffer is the
+// head (cb->buf, `writepos` tuples); older, full buffers of CHAINEDBUFF_NUMTUPLESPERBUF follow
+// through `next`, so cb_begin / cb_read_next walk every pair.
+namespace {
+constexpr uint32_t kCbTuples = 1024 * 1024;  // CHAINEDBUFF_NUMTUPLESPERBUF
+struct TupleBuffer {
+    tuple_t*     tuples;
+    TupleBuffer* next;
+};
+struct ChainedTupleBuffer {
+    TupleBuffer* buf;
+    TupleBuffer* readcursor;
+    TupleBuffer* writecursor;
+    uint32_t     writepos, readpos, readlen, numbufs;
+};
+
+ChainedTupleBuffer* chained_from(const tuple_t* pairs, uint64_t n) {
+    ChainedTupleBuffer* cb   = (ChainedTupleBuffer*) calloc(1, sizeof(ChainedTupleBuffer));
+    TupleBuffer*        head = nullptr;
+    uint64_t            off  = 0;
+    do {
+        const uint64_t c = n - off < kCbTuples ? n - off : kCbTuples;
+        TupleBuffer*   b = (TupleBuffer*) malloc(sizeof(TupleBuffer));
+        if (posix_memalign((void**) &b->tuples, 64, sizeof(tuple_t) * kCbTuples)) b->tuples = nullptr;
+        if (!b->tuples) {
+            set_last_error("out of host memory (result buffers)");
+            return nullptr;
+        }
+        if (c) memcpy(b->tuples, pairs + off, c * sizeof(tuple_t));
+        b->next      = head;
+        head         = b;
+        cb->writepos = (uint32_t) c;
+        cb->numbufs++;
+        off += c;
+    } while (off < n);
+    cb->buf = cb->readcursor = cb->writecursor = head;
+    return cb;
+}
+}  // namespace
+
+// JOIN_RESULT_MATERIALIZE (src/parallel_radix_join_bloom.c:1450-1472): resultlist[t] of every
+// worker; here all pairs are thread 0's, the others hold empty buffers.
+static threadresult_t* materialize_to_host(const tuple_t* dR, uint64_t nR, const tuple_t* dS,
+                                           uint64_t nS, const bloom_filter_args_t* args,
+                                           uint64_t matches, int nthreads) {
+    (void) args;
+    tuple_t* dout = nullptr;
+    if (hipMalloc((void**) &dout, (matches ? matches : 1) * sizeof(tuple_t)) != hipSuccess) {
+        set_last_error("hipMalloc of the result pairs failed");
+        fatal("BPRO");
+    }
+    Engine*  e = engine_for_current_device();
+    uint64_t n = 0;
+    if (!e || e->materialize((const uint2*) dR, nR, (const uint2*) dS, nS, (uint2*) dout, matches, &n,
+                             nullptr, nullptr) != 0 || n != matches)
+        fatal("BPRO (materialize)");
+    std::vector<tuple_t> host(matches ? matches : 1);
+    if (matches && hipMemcpy(host.data(), dout, matches * sizeof(tuple_t), hipMemcpyDeviceToHost) != hipSuccess) {
+        set_last_error("D2H of the result pairs failed");
+        fatal("BPRO");
+    }
+    (void) hipFree(dout);
+    const int       T    = nthreads > 0 ? nthreads : 1;
+    threadresult_t* tres = (threadresult_t*) calloc(T, sizeof(threadresult_t));
+    for (int t = 0; t < T; t++) {
+        tres[t].threadid = (uint32_t) t;
+        tres[t].nresults = t == 0 ? (int64_t) matches : 0;
+        tres[t].results  = chained_from(host.data(), t == 0 ? matches : 0);
+        if (!tres[t].results) fatal("BPRO");
+    }
+    return tres;
+}
+
 static result_t* run_host_join(relation_t* relR, relation_t* relS, int nthreads,
                                bloom_filter_args_t* args) {
     int ndev = 0;
@@ -188,6 +294,9 @@ static result_t* run_host_join(relation_t* relR, relation_t* relS, int nthreads,
     const uint64_t c0 = __rdtsc();
     if (hwbrj_join_device(dR, nR, dS, nS, args, nullptr, &st) != 0) fatal("BPRO");
     const uint64_t c1 = __rdtsc();
+    const bool mat = g_materialize == 1 || (g_materialize < 0 && getenv("HWBRJ_MATERIALIZE"));
+    threadresult_t* tres = nullptr;
+    if (mat) tres = materialize_to_host(dR, nR, dS, nS, args, (uint64_t) st.matches, nthreads);
     (void) hipFree(dR);
     (void) hipFree(dS);
     if (args) fprintf(stdout, "S-tuples after filter: %d\n", (int) st.filtered);  // :1253
@@ -209,7 +318,7 @@ static result_t* run_host_join(relation_t* relR, relation_t* relS, int nthreads,
         fatal("BPRO");
     }
     res->totalresults = st.matches;
-    res->resultlist   = nullptr;
+    res->resultlist   = tres;
     res->nthreads     = nthreads;
     return res;
 }

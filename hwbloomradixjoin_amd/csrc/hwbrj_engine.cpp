@@ -243,7 +243,7 @@ void Engine::release() {
     for (DevBuf* b : {&poolR, &metaR, &usedR, &wgqcR, &wgqeR, &wgqoR, &lstartR, &estartR, &istartR,
                       &listR, &poolS, &metaS, &usedS, &wgqcS, &wgqeS, &wgqoS, &lstartS, &estartS,
                       &istartS, &listS, &slices, &bitmap, &rjoin, &rrun, &surv, &survcnt, &survoff,
-                      &dense, &small, &colR, &colS})
+                      &dense, &small, &colR, &colS, &mtab, &mcount})
         b->release();
     have_filter_ = false;
 }
@@ -506,6 +506,35 @@ int Engine::export_filter(uint8_t* host_out, uint64_t nbytes) {
     HWBRJ_CHECK(hipStreamSynchronize(own_stream_));
     HWBRJ_CHECK(hipMemcpy(host_out, tmp.p, nbytes, hipMemcpyDeviceToHost));
     tmp.release();
+    return 0;
+}
+
+int Engine::materialize(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS, uint2* out,
+                        uint64_t cap, uint64_t* n, hipStream_t stream, double* ms) {
+    HWBRJ_CHECK(hipSetDevice(device_));
+    if (!stream) stream = own_stream_;
+    uint64_t T = 2;
+    while (T < 2 * nR) T <<= 1;
+    if (!mtab.ensure(T * 8) || !mcount.ensure(8)) {
+        set_last_error("hipMalloc failed (materialization table)");
+        return 4;
+    }
+    HWBRJ_CHECK(hipMemsetAsync(mtab.p, 0, T * 8, stream));
+    HWBRJ_CHECK(hipMemsetAsync(mcount.p, 0, 8, stream));
+    HWBRJ_CHECK(hipEventRecord(ev_[0], stream));
+    if (nR) launch_mat_build(dR, nR, mtab.as<unsigned long long>(), T - 1, stream);
+    if (nR && nS)
+        launch_mat_probe(dS, nS, dR, mtab.as<unsigned long long>(), T - 1, out, cap,
+                         mcount.as<unsigned long long>(), stream);
+    HWBRJ_CHECK(hipEventRecord(ev_[1], stream));
+    HWBRJ_CHECK(hipGetLastError());
+    HWBRJ_CHECK(hipEventSynchronize(ev_[1]));
+    HWBRJ_CHECK(hipMemcpy(n, mcount.p, 8, hipMemcpyDeviceToHost));
+    if (ms) {
+        float f = 0;
+        HWBRJ_CHECK(hipEventElapsedTime(&f, ev_[0], ev_[1]));
+        *ms = f;
+    }
     return 0;
 }
 

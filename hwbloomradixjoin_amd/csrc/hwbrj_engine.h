@@ -32,6 +32,9 @@ class Engine {
     int  run(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
              const bloom_filter_args_t* args, hipStream_t stream, hwbrj_stats_t* st);
     int  export_filter(uint8_t* host_out, uint64_t nbytes);
+    // (R.payload, S.payload) of every match into out[0, cap); *n = number of pairs.
+    int  materialize(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS, uint2* out,
+                     uint64_t cap, uint64_t* n, hipStream_t stream, double* ms);
     int  generate(uint2* d_out, uint64_t n, uint64_t offset, uint64_t count, uint32_t nthreads,
                   uint64_t maxid, uint64_t threshold, double selectivity, uint64_t seed,
                   hipStream_t stream);
@@ -53,6 +56,7 @@ class Engine {
     DevBuf poolS, metaS, usedS, wgqcS, wgqeS, wgqoS, lstartS, estartS, istartS, listS;
     DevBuf slices, bitmap, rjoin, rrun, surv, survcnt, survoff, dense, small, dbgP, dbgJ, dbgS;
     DevBuf colR, colS;  // per-partition totals from k_plan: u64 elements [F], then u32 chunks [F]
+    DevBuf mtab, mcount;  // materialization: R table, pair counter
 };
 
 Engine* engine_for_current_device();

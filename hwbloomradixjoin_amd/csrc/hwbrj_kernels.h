@@ -103,6 +103,12 @@ uint32_t build_sweep_slot();        // out_codes words per k_build sweep
 void   launch_build(const BuildParams& p, uint32_t F, hipStream_t st);
 void   launch_probe(const ProbeParams& p, uint32_t grid, hipStream_t st);
 void   launch_join(const JoinParams& p, uint32_t jobs, hipStream_t st);
+// result materialization (K12): R table build, S probe writing (R.payload, S.payload) pairs
+void   launch_mat_build(const uint2* R, uint64_t n, unsigned long long* tab, uint64_t mask,
+                        hipStream_t st);
+void   launch_mat_probe(const uint2* S, uint64_t n, const uint2* R, const unsigned long long* tab,
+                        uint64_t mask, uint2* out, uint64_t cap, unsigned long long* count,
+                        hipStream_t st);
 void   launch_export(const uint32_t* slices, const Geometry& g, uint32_t* out, uint64_t nwords,
                      hipStream_t st);
 

@@ -1481,6 +1481,79 @@ __global__ void k_export(const uint32_t* slices, Geometry g, uint32_t* out, uint
     }
 }
 
+// ================================================================ K12: result materialization
+// (R.payload, S.payload) pairs of every match, the reference's JOIN_RESULT_MATERIALIZE output
+// (src/parallel_radix_join_bloom.c:307-312: key = R rid, payload = S rid). A separate pass after
+// the counting pipeline (which fixes the output size): an open-addressing table of R
+// (entry = (row + 1) << 32 | key, 0 = empty, linear probing), then every S tuple walks its probe
+// sequence; a wave takes its output range with one atomic and every matching lane writes its
+// pairs there (a second walk, taken only by lanes that matched).
+__device__ __forceinline__ uint32_t mat_slot(uint32_t key, uint64_t mask) {
+    return (uint32_t) (mix32(key * 0x9E3779B1u + 0x7F4A7C15u) & mask);
+}
+
+__global__ __launch_bounds__(256) void k_mat_build(const uint2* __restrict__ R, uint64_t n,
+                                                    unsigned long long* __restrict__ tab,
+                                                    uint64_t mask) {
+    uint64_t       i      = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x;
+    const uint64_t stride = (uint64_t) gridDim.x * blockDim.x;
+    for (; i < n; i += stride) {
+        const uint32_t           key = R[i].x;
+        const unsigned long long e   = ((unsigned long long) (i + 1) << 32) | key;
+        uint64_t                 h   = mat_slot(key, mask);
+        while (atomicCAS(&tab[h], 0ull, e) != 0ull) h = (h + 1) & mask;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_mat_probe(const uint2* __restrict__ S, uint64_t n,
+                                                    const uint2* __restrict__ R,
+                                                    const unsigned long long* __restrict__ tab,
+                                                    uint64_t mask, uint2* __restrict__ out,
+                                                    uint64_t cap, unsigned long long* __restrict__ count) {
+    const int      lane   = threadIdx.x & 63;
+    const uint64_t stride = (uint64_t) gridDim.x * blockDim.x;
+    for (uint64_t i0 = blockIdx.x * (uint64_t) blockDim.x; i0 < n; i0 += stride) {  // uniform per wave
+        const uint64_t i   = i0 + threadIdx.x;
+        const bool     ok  = i < n;
+        const uint2    st  = ok ? S[i] : make_uint2(0, 0);
+        uint32_t       hit = 0;
+        if (ok) {
+            for (uint64_t h = mat_slot(st.x, mask);; h = (h + 1) & mask) {
+                const unsigned long long e = tab[h];
+                if (e == 0ull) break;
+                hit += (uint32_t) e == st.x;
+            }
+        }
+        const uint32_t incl = wave_incl_scan_dpp(hit);
+        const uint32_t tot  = __builtin_amdgcn_readlane(incl, 63);
+        if (tot == 0) continue;  // uniform
+        unsigned long long base = 0;
+        if (lane == 0) base = atomicAdd(count, (unsigned long long) tot);
+        base = ((unsigned long long) __builtin_amdgcn_readfirstlane((uint32_t) (base >> 32)) << 32) |
+               __builtin_amdgcn_readfirstlane((uint32_t) base);
+        if (hit) {
+            uint64_t o = base + incl - hit;
+            for (uint64_t h = mat_slot(st.x, mask);; h = (h + 1) & mask) {
+                const unsigned long long e = tab[h];
+                if (e == 0ull) break;
+                if ((uint32_t) e == st.x) {
+                    if (o < cap) out[o] = make_uint2(R[(e >> 32) - 1].y, st.y);  // (R rid, S rid)
+                    o++;
+                }
+            }
+        }
+    }
+}
+
+void launch_mat_build(const uint2* R, uint64_t n, unsigned long long* tab, uint64_t mask, hipStream_t st) {
+    k_mat_build<<<8192, 256, 0, st>>>(R, n, tab, mask);
+}
+
+void launch_mat_probe(const uint2* S, uint64_t n, const uint2* R, const unsigned long long* tab,
+                      uint64_t mask, uint2* out, uint64_t cap, unsigned long long* count, hipStream_t st) {
+    k_mat_probe<<<8192, 256, 0, st>>>(S, n, R, tab, mask, out, cap, count);
+}
+
 // ===================================================================== launch wrappers
 void launch_gen(uint2* out, uint64_t offset, uint64_t count, const GenPlan* d_plan, const Perm& perm,
                 hipStream_t st) {

@@ -117,6 +117,19 @@ typedef struct hwbrj_stats_t {
 int hwbrj_join_device(const tuple_t * d_R, uint64_t nR, const tuple_t * d_S, uint64_t nS,
                       const bloom_filter_args_t * args, void * stream, hwbrj_stats_t * stats);
 
+/* The join with result materialization (the reference's JOIN_RESULT_MATERIALIZE output,
+ * src/parallel_radix_join_bloom.c:307-312): d_out[i] = {R.payload, S.payload} of every match, in
+ * no particular order. Runs the counting join (stats) and then the pairs pass; capacity is in
+ * pairs. Returns 7 with *n_out = the match count when capacity is too small.
+ * ms_materialize (optional) receives the pairs pass's device time. */
+int hwbrj_join_materialize_device(const tuple_t * d_R, uint64_t nR, const tuple_t * d_S,
+                                  uint64_t nS, const bloom_filter_args_t * args, tuple_t * d_out,
+                                  uint64_t capacity, uint64_t * n_out, void * stream,
+                                  hwbrj_stats_t * stats, double * ms_materialize);
+/* Host BPRO/PRO (and the PRH/PRHO/RJ entries) fill result_t.resultlist with the reference's
+ * chained result buffers (src/tuple_buffer.h) when on (default: on iff HWBRJ_MATERIALIZE is set). */
+void hwbrj_set_materialize(int on);
+
 /* Fill d_out / out with the reference generator's key multiset (src/generator.c:304-415 with
  * `nthreads` generator threads) in a seeded permuted order; payload = row index. */
 int hwbrj_generate_device(tuple_t * d_out, uint64_t n, uint32_t nthreads, uint64_t maxid,

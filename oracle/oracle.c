@@ -411,6 +411,42 @@ orc_gen_zipf(orc_tuple_t * out, uint64_t n, unsigned int alphabet_size, double z
     return 0;
 }
 
+/* -------------------------------------------------- materialized join result */
+static int
+orc_key_cmp(const void * a, const void * b)
+{
+    const orc_tuple_t *x = a, *y = b;
+    return (x->key > y->key) - (x->key < y->key);
+}
+
+/* JOIN_RESULT_MATERIALIZE (src/parallel_radix_join_bloom.c:307-312): for every S tuple and every
+ * R tuple with an equal key, the pair {R.payload, S.payload}. Order-free restatement (sorted R,
+ * binary search); writes min(total, cap) pairs, returns the total (-1: out of memory). */
+int64_t
+orc_join_pairs(const orc_tuple_t * R, uint64_t nR, const orc_tuple_t * S, uint64_t nS,
+               orc_tuple_t * out, uint64_t cap)
+{
+    orc_tuple_t * r = malloc((nR ? nR : 1) * sizeof(orc_tuple_t));
+    if (!r) return -1;
+    memcpy(r, R, nR * sizeof(orc_tuple_t));
+    qsort(r, nR, sizeof(orc_tuple_t), orc_key_cmp);
+    int64_t n = 0;
+    for (uint64_t i = 0; i < nS; i++) {
+        uint64_t lo = 0, hi = nR;
+        while (lo < hi) {
+            uint64_t mid = (lo + hi) / 2;
+            if (r[mid].key < S[i].key) lo = mid + 1; else hi = mid;
+        }
+        for (uint64_t j = lo; j < nR && r[j].key == S[i].key; j++, n++)
+            if ((uint64_t) n < cap) {
+                out[n].key     = r[j].payload;
+                out[n].payload = S[i].payload;
+            }
+    }
+    free(r);
+    return n;
+}
+
 /* ------------------------------------------------------------- radix join */
 
 #define NUM_RADIX_BITS 10 /* src/prj_params.h:16 */

@@ -89,6 +89,11 @@ int64_t  orc_bpro(const orc_tuple_t * R, uint64_t nR, const orc_tuple_t * S, uin
                   int nthreads, int variant, uint64_t m, uint64_t k, uint64_t B, int use_bloom,
                   uint64_t * filtered, orc_timing_t * timing);
 
+/* src/parallel_radix_join_bloom.c:307-312 (JOIN_RESULT_MATERIALIZE): {R.payload, S.payload} of
+ * every match, order-free; writes min(total, cap) pairs, returns the total. */
+int64_t  orc_join_pairs(const orc_tuple_t * R, uint64_t nR, const orc_tuple_t * S, uint64_t nS,
+                        orc_tuple_t * out, uint64_t cap);
+
 /* Scalar helpers for tests (single-threaded, small inputs). */
 uint64_t orc_count_filtered(const orc_bloom_t * f, const int32_t * keys, uint64_t n);
 void     orc_bloom_add_all(orc_bloom_t * f, const int32_t * keys, uint64_t n);

@@ -63,8 +63,23 @@ def lib() -> ctypes.CDLL:
         L.orc_gen_zipf.restype = ctypes.c_int
         L.orc_gen_zipf.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint, ctypes.c_double,
                                    ctypes.c_uint32]
+        L.orc_join_pairs.restype = ctypes.c_int64
+        L.orc_join_pairs.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                     ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64]
         _L = L
     return _L
+
+
+def join_pairs(R: np.ndarray, S: np.ndarray) -> np.ndarray:
+    """(n, 2) int32 {R.payload, S.payload} of every match (JOIN_RESULT_MATERIALIZE), unordered."""
+    R = np.ascontiguousarray(R, dtype=np.int32)
+    S = np.ascontiguousarray(S, dtype=np.int32)
+    n = lib().orc_join_pairs(R.ctypes.data, R.shape[0], S.ctypes.data, S.shape[0], None, 0)
+    if n < 0:
+        raise MemoryError
+    out = np.empty((n, 2), dtype=np.int32)
+    lib().orc_join_pairs(R.ctypes.data, R.shape[0], S.ctypes.data, S.shape[0], out.ctypes.data, n)
+    return out
 
 
 def threshold(r_size: int, q: float, full_range: bool) -> int:

@@ -41,6 +41,9 @@ def test_struct_layouts_match_reference(hw):
     assert ctypes.sizeof(hw._Result) == 24
     assert ctypes.sizeof(hw._BloomArgs) == 32
     assert hw.BASIC == 0 and hw.BLOCKED == 1
+    # src/tuple_buffer.h:27-40 (chained result buffers of JOIN_RESULT_MATERIALIZE)
+    assert ctypes.sizeof(hw._TupleBuffer) == 16 and ctypes.sizeof(hw._ChainedTupleBuffer) == 40
+    assert ctypes.sizeof(hw._ThreadResult) == 24
 
 
 def test_host_hashes_match_reference_kats(hw):

@@ -286,3 +286,55 @@ def test_cli_end_to_end(hw):
     assert out.returncode == 0, out.stdout + out.stderr
     assert f"S-tuples after filter: {g['rows']['1024'][0]}" in out.stdout
     assert f"[INFO ] Results = {g['results']}. DONE." in out.stdout
+
+
+def _sorted_pairs(p):
+    p = np.asarray(p).reshape(-1, 2)
+    return p[np.lexsort((p[:, 1], p[:, 0]))]
+
+
+@pytest.mark.parametrize("case", ["pkfk", "dups", "nonunique", "edge"])
+def test_materialized_pairs_vs_oracle(hw, cuda, orc, gen3, case):
+    """JOIN_RESULT_MATERIALIZE: the multiset of {R.payload, S.payload} pairs equals the oracle's."""
+    rng = np.random.default_rng(11)
+    if case == "pkfk":
+        R = orc.relation(1000000, 2, 1000000, 1000000, 1.0, 1)
+        S = orc.relation(16000000, 2, INT_MAX, 1000000, 0.01, 2)
+    elif case == "dups":
+        Rk = np.concatenate([rng.integers(-3000, 3000, size=60000), [INT_MAX, -INT_MAX - 1, -1] * 3])
+        Sk = np.concatenate([rng.integers(-4000, 4000, size=500000), [INT_MAX, -INT_MAX - 1, -1] * 5])
+        R = np.stack([Rk, rng.integers(-2**31, 2**31, size=Rk.size)], 1).astype(np.int32)
+        S = np.stack([Sk, rng.integers(-2**31, 2**31, size=Sk.size)], 1).astype(np.int32)
+    elif case == "nonunique":
+        R, S = gen3[1]["nonunique"]
+    else:
+        R = np.array([[5, 1], [5, 2]], dtype=np.int32)
+        S = np.array([[5, 7], [6, 8], [5, 9]], dtype=np.int32)
+    for args in (hw.BloomFilterArgs(hw.BLOCKED, 1 << 24, 1, 1024), None):
+        st, pairs, _ = hw.join_materialize_device(to_dev(cuda, R), to_dev(cuda, S), args)
+        want = orc.join_pairs(R, S)
+        assert st.matches == want.shape[0] == pairs.shape[0]
+        assert np.array_equal(_sorted_pairs(pairs.cpu().numpy()), _sorted_pairs(want))
+
+
+def test_materialize_empty_sides(hw, cuda):
+    e = np.empty((0, 2), dtype=np.int32)
+    one = np.array([[1, 1]], dtype=np.int32)
+    for R, S in [(e, one), (one, e)]:
+        st, pairs, _ = hw.join_materialize_device(to_dev(cuda, R), to_dev(cuda, S), None)
+        assert st.matches == 0 and pairs.shape[0] == 0
+
+
+def test_bpro_materialized_result_list(hw, orc):
+    """Host BPRO with materialization fills result_t.resultlist with the reference's chained
+    buffers (src/tuple_buffer.h); the pairs equal the oracle's."""
+    R = hw.generate_host(300000, 2, 300000, 300000, 1.0, 5)
+    S = hw.generate_host(3000000, 2, INT_MAX, 300000, 0.5, 6)
+    hw.set_materialize(True)
+    try:
+        res = hw.BPRO(hw.Relation(R), hw.Relation(S), 4, hw.BloomFilterArgs(hw.BLOCKED, 1 << 22, 2, 512))
+    finally:
+        hw.set_materialize(False)
+    want = orc.join_pairs(R, S)
+    assert res.totalresults == want.shape[0] == res.pairs.shape[0] > 1024 * 1024
+    assert np.array_equal(_sorted_pairs(res.pairs), _sorted_pairs(want))
