@@ -20,7 +20,7 @@ __all__ = [
     "BPRO", "PRO", "join_materialize_device", "set_materialize", "BPRH", "BPRHO", "BRJ", "PRH", "PRHO", "RJ", "assert_args", "join_device", "generate_device", "generate_device_range",
     "generate_host", "nonunique_threshold", "create_relation_nonunique",
     "create_relation_nonunique_from_pk", "create_relation_fk_from_pk", "create_relation_zipf",
-    "rand_stream", "reference_relations",
+    "rand_stream", "reference_relations", "create_relation_zipf_device",
     "export_filter", "hash_crc", "hash_crapwow", "lib", "LIB_PATH", "shard_range",
 ]
 
@@ -121,6 +121,10 @@ def lib() -> ctypes.CDLL:
         L.hwbrj_create_relation_zipf.restype = ctypes.c_int
         L.hwbrj_create_relation_zipf.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
                                                  ctypes.c_double, ctypes.c_uint32, ctypes.c_int]
+        L.hwbrj_create_relation_zipf_device.restype = ctypes.c_int
+        L.hwbrj_create_relation_zipf_device.argtypes = [
+            ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_double, ctypes.c_uint32,
+            ctypes.c_double, ctypes.c_int, ctypes.c_void_p]
         L.hwbrj_rand_stream.restype = ctypes.c_int
         L.hwbrj_rand_stream.argtypes = [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint64]
         L.hwbrj_export_filter.restype = ctypes.c_int
@@ -432,6 +436,15 @@ def create_relation_zipf(n: int, alphabet_size: int, theta: float, seed: int,
     _err(lib().hwbrj_create_relation_zipf(out.ctypes.data, n, alphabet_size, theta, seed,
                                           host_threads), "hwbrj_create_relation_zipf")
     return out
+
+
+def create_relation_zipf_device(out, alphabet_size: int, theta: float, seed: int,
+                                selectivity: float = 1.0, host_threads: int = 0) -> None:
+    """The -z relation into a (n, 2) int32 GPU tensor (binary searches on the GPU). selectivity=1:
+    bit-exact create_relation_zipf; < 1: this build's selectivity extension (BASELINE config 5)."""
+    _err(lib().hwbrj_create_relation_zipf_device(_ptr(out), out.shape[0], alphabet_size, theta,
+                                                 seed, selectivity, host_threads, None),
+         "hwbrj_create_relation_zipf_device")
 
 
 def rand_stream(seed: int, n: int) -> np.ndarray:

@@ -76,6 +76,43 @@ static void knuth_shuffle(GlibcRand& g, tuple_t* rel, uint64_t n) {
     }
 }
 
+// gen_alphabet (genzipf.c:28-53: 1..size permuted by rand() after srand(seed)) and gen_zipf_lut
+// (:60-92: the two sequential sums of 1 / pow(i, theta); the pow terms are computed in parallel,
+// the sums in the reference's order). Leaves *g positioned for the stream. Returns the thread count.
+static int zipf_tables(GlibcRand* g, unsigned int size, double theta, uint32_t seed, int host_threads,
+                       std::vector<uint32_t>* alphabet, std::vector<double>* lut) {
+    g->seed(seed);
+    int T = host_threads > 0 ? host_threads : (int) std::thread::hardware_concurrency();
+    T     = std::max(1, std::min(T, 64));
+    alphabet->resize(size);
+    uint32_t* a = alphabet->data();
+    for (unsigned int i = 0; i < size; i++) a[i] = i + 1;
+    for (unsigned int i = size - 1; i > 0; i--) {
+        const unsigned int k   = (unsigned int) ((unsigned long) i * (unsigned long) g->next() /
+                                                 (unsigned long) 2147483647);
+        const uint32_t     tmp = a[i];
+        a[i]                   = a[k];
+        a[k]                   = tmp;
+    }
+    lut->resize(size);
+    double* l = lut->data();
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; t++)
+        th.emplace_back([=] {
+            const uint64_t b = (uint64_t) size * t / T, e = (uint64_t) size * (t + 1) / T;
+            for (uint64_t i = b; i < e; i++) l[i] = 1.0 / pow((double) (unsigned int) (i + 1), theta);
+        });
+    for (auto& x : th) x.join();
+    double scaling = 0.0;
+    for (unsigned int i = 0; i < size; i++) scaling += l[i];
+    double sum = 0.0;
+    for (unsigned int i = 0; i < size; i++) {
+        sum += l[i];
+        l[i] = sum / scaling;
+    }
+    return T;
+}
+
 }  // namespace hwbrj
 
 using namespace hwbrj;
@@ -169,40 +206,17 @@ int hwbrj_create_relation_zipf(tuple_t* out, uint64_t n, uint64_t alphabet_size,
         set_last_error("invalid arguments (alphabet and |S| must be in [1, 2^32))");
         return 2;
     }
-    const unsigned int size = (unsigned int) alphabet_size;
-    GlibcRand          g;
-    g.seed(seed);
-    int T = host_threads > 0 ? host_threads : (int) std::thread::hardware_concurrency();
-    T     = std::max(1, std::min(T, 64));
+    const unsigned int    size = (unsigned int) alphabet_size;
+    GlibcRand             g;
+    std::vector<uint32_t> alphabet;
+    std::vector<double>   lut;
+    const int             T = zipf_tables(&g, size, theta, seed, host_threads, &alphabet, &lut);
     auto par = [&](uint64_t total, auto&& fn) {
         std::vector<std::thread> th;
         for (int t = 0; t < T; t++)
             th.emplace_back([&, t] { fn(total * t / T, total * (t + 1) / T); });
         for (auto& x : th) x.join();
     };
-    // gen_alphabet (:28-53): 1..size, permuted by rand()
-    std::vector<uint32_t> alphabet(size);
-    for (unsigned int i = 0; i < size; i++) alphabet[i] = i + 1;
-    for (unsigned int i = size - 1; i > 0; i--) {
-        const unsigned int k   = (unsigned int) ((unsigned long) i * (unsigned long) g.next() /
-                                                 (unsigned long) 2147483647);
-        const uint32_t     tmp = alphabet[i];
-        alphabet[i]            = alphabet[k];
-        alphabet[k]            = tmp;
-    }
-    // gen_zipf_lut (:60-92): the two sequential sums of 1 / pow(i, theta); the pow terms are
-    // computed in parallel (same values), the sums in the reference's order.
-    std::vector<double> lut(size);
-    par(size, [&](uint64_t b, uint64_t e) {
-        for (uint64_t i = b; i < e; i++) lut[i] = 1.0 / pow((double) (unsigned int) (i + 1), theta);
-    });
-    double scaling = 0.0;
-    for (unsigned int i = 0; i < size; i++) scaling += lut[i];
-    double sum = 0.0;
-    for (unsigned int i = 0; i < size; i++) {
-        sum += lut[i];
-        lut[i] = sum / scaling;
-    }
     // the stream (:119-150): r = rand() / RAND_MAX, binary search, key = alphabet[pos]
     for (uint64_t i = 0; i < n; i++) out[i].key = g.next();
     par(n, [&](uint64_t b, uint64_t e) {
@@ -223,6 +237,66 @@ int hwbrj_create_relation_zipf(tuple_t* out, uint64_t n, uint64_t alphabet_size,
             out[i].payload = (int32_t) i;
         }
     });
+    return 0;
+}
+
+// The same Zipf relation generated into HBM (the binary searches run on the GPU; the rand() stream
+// is drawn on the host in order and shipped in chunks). selectivity < 1 is this build's extension
+// for BASELINE config 5 (the reference ignores -q under -z, src/main.c:457-466): floor(n (1 - q))
+// rows, chosen by a seeded permutation, get unique keys above the alphabet, so exactly the other
+// rows match. selectivity = 1 gives the reference's relation.
+int hwbrj_create_relation_zipf_device(tuple_t* d_out, uint64_t n, uint64_t alphabet_size,
+                                      double theta, uint32_t seed, double selectivity,
+                                      int host_threads, void* stream) {
+    if ((!d_out && n) || alphabet_size == 0 || alphabet_size > (uint64_t) UINT_MAX ||
+        n > (uint64_t) UINT_MAX || selectivity < 0 || selectivity > 1) {
+        set_last_error("invalid arguments (alphabet and |S| in [1, 2^32), q in [0, 1])");
+        return 2;
+    }
+    const uint64_t n_above = (uint64_t) ((double) n * (1 - selectivity));
+    if (alphabet_size + 1 + n_above > (uint64_t) INT_MAX) {
+        set_last_error("alphabet + unmatched keys exceed INT_MAX");
+        return 2;
+    }
+    hipStream_t st = (hipStream_t) stream;
+    GlibcRand             g;
+    std::vector<uint32_t> alphabet;
+    std::vector<double>   lut;
+    zipf_tables(&g, (unsigned int) alphabet_size, theta, seed, host_threads, &alphabet, &lut);
+    const uint64_t kChunk = 1ull << 26;
+    uint32_t* d_alpha = nullptr;
+    double*   d_lut   = nullptr;
+    int32_t*  d_rnd   = nullptr;
+    auto fail = [&](const char* what) {
+        set_last_error(what);
+        (void) hipFree(d_alpha);
+        (void) hipFree(d_lut);
+        (void) hipFree(d_rnd);
+        return 4;
+    };
+    if (hipMalloc((void**) &d_alpha, alphabet.size() * 4) != hipSuccess ||
+        hipMalloc((void**) &d_lut, lut.size() * 8) != hipSuccess ||
+        hipMalloc((void**) &d_rnd, kChunk * 4) != hipSuccess)
+        return fail("hipMalloc failed (zipf tables)");
+    if (hipMemcpy(d_alpha, alphabet.data(), alphabet.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(d_lut, lut.data(), lut.size() * 8, hipMemcpyHostToDevice) != hipSuccess)
+        return fail("H2D of the zipf tables failed");
+    std::vector<int32_t> rnd(std::min(n, kChunk));
+    const Perm           perm = make_perm(n ? n : 1, seed ^ 0x5A17F00Dull);
+    for (uint64_t r0 = 0; r0 < n; r0 += kChunk) {
+        const uint64_t c = std::min(kChunk, n - r0);
+        for (uint64_t i = 0; i < c; i++) rnd[i] = g.next();
+        if (hipStreamSynchronize(st) != hipSuccess ||  // the previous chunk's kernel read d_rnd
+            hipMemcpy(d_rnd, rnd.data(), c * 4, hipMemcpyHostToDevice) != hipSuccess)
+            return fail("H2D of the rand() stream failed");
+        launch_zipf(d_rnd, c, r0, d_lut, d_alpha, (uint32_t) alphabet_size, (uint2*) d_out + r0, n_above,
+                    (uint32_t) (alphabet_size + 1), perm, st);
+        if (hipGetLastError() != hipSuccess) return fail("zipf kernel launch failed");
+    }
+    if (hipStreamSynchronize(st) != hipSuccess) return fail("zipf kernel failed");
+    (void) hipFree(d_alpha);
+    (void) hipFree(d_lut);
+    (void) hipFree(d_rnd);
     return 0;
 }
 

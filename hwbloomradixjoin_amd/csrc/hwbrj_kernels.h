@@ -78,6 +78,9 @@ struct JoinParams {
 
 void   launch_gen(uint2* out, uint64_t offset, uint64_t count, const GenPlan* d_plan, const Perm& perm,
                   hipStream_t st);
+void   launch_zipf(const int32_t* rnd, uint64_t cnt, uint64_t row0, const double* lut,
+                   const uint32_t* alphabet, uint32_t size, uint2* out, uint64_t n_above,
+                   uint32_t above_base, const Perm& perm, hipStream_t st);
 void   launch_build_global(const uint2* R, uint64_t n, const Geometry& g, const CrcTables* tabs,
                            uint32_t* bm, hipStream_t st);
 void   launch_probe_global(const uint2* S, uint64_t n, const Geometry& g, const CrcTables* tabs,

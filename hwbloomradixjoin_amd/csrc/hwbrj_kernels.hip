@@ -150,6 +150,45 @@ __global__ void k_gen(uint2* out, uint64_t offset, uint64_t count, const GenPlan
     }
 }
 
+// Zipf stream on the device (src/genzipf.c:119-150): rnd holds the rand() draws of rows
+// [row0, row0 + cnt), each becomes alphabet[pos] by the reference's binary search over the CDF.
+// This build's selectivity extension: rows whose permuted index u < n_above get the unique
+// non-matching key above_base + u instead (n_above = 0: the reference's stream).
+__global__ void k_zipf(const int32_t* __restrict__ rnd, uint64_t cnt, uint64_t row0,
+                       const double* __restrict__ lut, const uint32_t* __restrict__ alphabet,
+                       uint32_t size, uint2* __restrict__ out, uint64_t n_above, uint32_t above_base,
+                       Perm perm) {
+    uint64_t       i      = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x;
+    const uint64_t stride = (uint64_t) gridDim.x * blockDim.x;
+    for (; i < cnt; i += stride) {
+        const double r     = ((double) rnd[i]) / 2147483647;
+        uint32_t     left  = 0, right = size - 1, pos;
+        if (lut[0] >= r) {
+            pos = 0;
+        } else {
+            while (right - left > 1) {
+                const uint32_t m = (left + right) / 2;
+                if (lut[m] < r) left = m;
+                else right = m;
+            }
+            pos = right;
+        }
+        const uint64_t row = row0 + i;
+        uint32_t       key = alphabet[pos];
+        if (n_above) {
+            const uint64_t u = perm_apply(perm, row);
+            if (u < n_above) key = above_base + (uint32_t) u;
+        }
+        out[i] = make_uint2(key, (uint32_t) row);
+    }
+}
+
+void launch_zipf(const int32_t* rnd, uint64_t cnt, uint64_t row0, const double* lut,
+                 const uint32_t* alphabet, uint32_t size, uint2* out, uint64_t n_above,
+                 uint32_t above_base, const Perm& perm, hipStream_t st) {
+    k_zipf<<<8192, 256, 0, st>>>(rnd, cnt, row0, lut, alphabet, size, out, n_above, above_base, perm);
+}
+
 // ============================================== K1/K2: global-bitmap fallback (MODE_GLOBAL)
 // Reference layout: bit b of the filter = bit (b & 31) of 32-bit word b >> 5 (== byte b >> 3,
 // bit b & 7 on little-endian, as bloom_filter.c addresses it).

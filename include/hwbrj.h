@@ -161,6 +161,13 @@ int      hwbrj_create_relation_fk_from_pk(tuple_t * out, uint64_t n, const tuple
                                           uint32_t seed);
 int      hwbrj_create_relation_zipf(tuple_t * out, uint64_t n, uint64_t alphabet_size,
                                     double theta, uint32_t seed, int host_threads);
+/* The -z relation generated straight into HBM (binary searches on the GPU): selectivity = 1 gives
+ * exactly hwbrj_create_relation_zipf's relation. selectivity < 1 is this build's extension for
+ * BASELINE config 5 (the reference ignores -q with -z): floor(n (1 - q)) rows chosen by a seeded
+ * permutation get unique keys above the alphabet. stream: hipStream_t or NULL. */
+int      hwbrj_create_relation_zipf_device(tuple_t * d_out, uint64_t n, uint64_t alphabet_size,
+                                           double theta, uint32_t seed, double selectivity,
+                                           int host_threads, void * stream);
 /* The first n values rand() returns after srand(seed) (test hook for the restatement). */
 int      hwbrj_rand_stream(uint32_t seed, int32_t * out, uint64_t n);
 
