@@ -82,7 +82,7 @@ enum Mode : int {
 
 enum Format : int {
     FMT_CODE   = 0,  // element word = code = crc32c(42, key)
-    FMT_PACKED = 1,  // blocked, k = 1, log2B <= log2F: (code >> log2F) | (bit-in-block << (32 - log2F))
+    FMT_PACKED = 1,  // blocked, log2B <= log2F: (code >> log2F) | (first bit-in-block << (32 - log2F))
 };
 
 struct Geometry {
@@ -116,6 +116,8 @@ enum Kind : int {
     KIND_BLOCK_PK1   = 1,  // blocked/sectorized, k = 1, packed words
     KIND_BLOCK       = 2,  // blocked/sectorized, code words, any k
     KIND_BASIC_K1    = 3,  // basic, k = 1
+    KIND_BLOCK_PKK   = 4,  // blocked/sectorized, k >= 2, packed words: the first bit is tested from
+                           // the word, the key (for the rest) is recovered only for those that pass
 };
 
 constexpr uint32_t kMaxLog2F     = 10;

@@ -176,7 +176,7 @@ bool plan_geometry(const bloom_filter_args_t* a, uint64_t nR, Geometry* g, std::
             g->nseg       = g->slice_bits / g->seg_bits;
             g->seg_words  = std::max<uint32_t>(4, g->seg_bits / 32);
         }
-        if (g->mode == MODE_SLICE_BLOCK && k == 1 && ilog2u(B) <= g->log2F) g->format = FMT_PACKED;
+        if (g->mode == MODE_SLICE_BLOCK && ilog2u(B) <= g->log2F) g->format = FMT_PACKED;
         if (g->mode == MODE_SLICE_BLOCK || g->mode == MODE_SLICE_BASIC) g->log2seg = ilog2u(g->seg_bits);
         if (a->variant != BASIC) {
             g->log2B    = ilog2u(B);

@@ -74,7 +74,11 @@ struct Loc {
 };
 
 template <int KIND>
-__device__ __forceinline__ Loc locate(uint32_t w, const Geometry& g, const uint32_t* inv) {
+__device__ __forceinline__ uint32_t decode_k(uint32_t w, uint32_t q, uint32_t log2F);
+
+// q: the element's partition (packed kinds recover the code from it).
+template <int KIND>
+__device__ __forceinline__ Loc locate(uint32_t w, const Geometry& g, const uint32_t* inv, uint32_t q) {
     Loc L;
     if (KIND == KIND_BASIC_K1) {
         const uint32_t key = code_key(inv, w);
@@ -86,10 +90,10 @@ __device__ __forceinline__ Loc locate(uint32_t w, const Geometry& g, const uint3
         return L;
     }
     uint32_t lb;
-    if (KIND == KIND_BLOCK_PK1) {
+    if (KIND == KIND_BLOCK_PK1 || KIND == KIND_BLOCK_PKK) {
         lb  = w & g.lbmask;           // (code >> log2F) & (nblocks/F - 1)
         L.h = w >> (32u - g.log2F);   // crapwow(key) & (B-1), stored by the scatter
-        L.y = 0;
+        L.y = KIND == KIND_BLOCK_PKK ? (code_key(inv, decode_k<KIND>(w, q, g.log2F)) + kSeed) & (g.B - 1u) : 0u;
     } else {
         const uint32_t key = code_key(inv, w);
         lb  = (w >> g.log2F) & g.lbmask;
@@ -135,7 +139,7 @@ __device__ __forceinline__ bool apply_bits(const Loc& L, const Geometry& g, uint
 
 template <int KIND>
 __device__ __forceinline__ uint32_t decode_k(uint32_t w, uint32_t q, uint32_t log2F) {
-    if (KIND == KIND_BLOCK_PK1) return (w << log2F) | q;  // log2F >= 3: (w << log2F) drops the h bits
+    if (KIND == KIND_BLOCK_PK1 || KIND == KIND_BLOCK_PKK) return (w << log2F) | q;  // drops the h bits
     return w;
 }
 
@@ -982,7 +986,7 @@ __global__ __launch_bounds__(1024) void k_build(BuildParams P) {
                     const bool     ok = (uint32_t) t < SA.n[jj];
                     const uint32_t w  = sweep_word(SA, jj, t);
                     if (slices && ok) {
-                        const Loc L = locate<KIND>(w, g, inv);
+                        const Loc L = locate<KIND>(w, g, inv, q);
                         if (L.seg == seg) apply_bits<KIND, true>(L, g, slice);
                     }
                     c[t]  = decode_k<KIND>(w, q, g.log2F);
@@ -1038,8 +1042,9 @@ __global__ __launch_bounds__(1024) void k_build(BuildParams P) {
 // the join reads them in place: surv_cnt[it][sub] / surv_off[it][sub] describe the runs.
 constexpr int      kPC      = 3;              // chunk quads per thread per item
 constexpr uint32_t kProbeCH = 128u * kPC;     // chunks per probe item (1024 threads, 8 per chunk)
-constexpr uint32_t kScrCap  = 128;            // compacted survivors per wave and item (LDS scratch)
-constexpr int      kDense   = kScrCap / 64;   // dense ranking rounds per wave
+// compacted survivors (first-bit candidates for KIND_BLOCK_PKK, whose rate is higher) per wave
+// and item in the LDS scratch, and the dense ranking rounds per wave
+template <int KIND> constexpr uint32_t scr_cap() { return KIND == KIND_BLOCK_PKK ? 256u : 128u; }
 
 __device__ __forceinline__ uint32_t find_q(const uint32_t* item_start, uint32_t F, uint32_t it) {
     uint32_t lo = 0, hi = F - 1;
@@ -1062,7 +1067,8 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
     const uint32_t  F      = 1u << g.log2F;
     const uint32_t  NSUB   = 1u << g.log2NSUB;
     constexpr bool  slices = KIND != KIND_PASS;
-    constexpr bool  onebit = KIND == KIND_BLOCK_PK1 || KIND == KIND_BASIC_K1;
+    constexpr bool  onebit = KIND == KIND_BLOCK_PK1 || KIND == KIND_BASIC_K1 || KIND == KIND_BLOCK_PKK;
+    constexpr bool  refine = KIND == KIND_BLOCK_PKK;  // onebit tests only the first bit: test the rest
     constexpr int   NW     = kPC * 4;   // words per thread per item
     const uint32_t  segw   = slices ? g.seg_words : 0;  // multiple of 4
     const uint32_t  scap   = P.stage_cap;               // survivor words per stage buffer
@@ -1071,6 +1077,8 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
     uint32_t*       inv    = slice + segw;
     uint32_t*       subc   = inv + 128;       // 3 x 128: per-sub counters (+64 dummies), by item
     uint32_t*       subow  = subc + 3 * 128;  // 16 waves x NSUB: each wave's copy of the offsets
+    constexpr uint32_t kScrCap = scr_cap<KIND>();
+    constexpr int      kDense  = kScrCap / 64;
     uint32_t*       scratch = subow + 16 * NSUB;  // 16 waves x (kScrCap + 64): compacted survivors
     uint32_t*       stage  = scratch + 16 * (kScrCap + 64);  // 2 x sstr, double-buffered by item
     const int       tid    = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -1176,10 +1184,10 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
 #pragma unroll
                 for (int i = 0; i < NW; i++) {
                     const uint32_t w = sweep_word(Sc, i >> 2, i & 3);
-                    if (KIND == KIND_BLOCK_PK1 && SEG1) {
+                    if ((KIND == KIND_BLOCK_PK1 || KIND == KIND_BLOCK_PKK) && SEG1) {
                         bb[i] = ((w & g.lbmask) << g.log2B) + (w >> (32u - g.log2F));
                     } else {
-                        const Loc L = locate<KIND>(w, g, inv);
+                        const Loc L = locate<KIND>(w, g, inv, q);
                         bb[i]       = L.base + L.h;
                     }
                     wv[i] = slice[bb[i] >> 5];
@@ -1188,7 +1196,7 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
                 for (int i = 0; i < NW; i++) {
                     const uint32_t w = sweep_word(Sc, i >> 2, i & 3);
                     uint32_t ok = (wv[i] >> (bb[i] & 31u)) & ((uint32_t) (i & 3) < Sc.n[i >> 2] ? 1u : 0u);
-                    if (!SEG1) ok &= locate<KIND>(w, g, inv).seg == seg ? 1u : 0u;
+                    if (!SEG1) ok &= locate<KIND>(w, g, inv, q).seg == seg ? 1u : 0u;
                     pass |= ok << i;
                     const uint64_t m   = __builtin_amdgcn_ballot_w64(ok != 0);
                     const uint32_t pre = __builtin_amdgcn_mbcnt_hi((uint32_t) (m >> 32),
@@ -1202,7 +1210,7 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
                 for (int i = 0; i < NW; i++) {
                     bool ok = (uint32_t) (i & 3) < Sc.n[i >> 2];
                     if (slices && ok) {
-                        const Loc L = locate<KIND>(sweep_word(Sc, i >> 2, i & 3), g, inv);
+                        const Loc L = locate<KIND>(sweep_word(Sc, i >> 2, i & 3), g, inv, q);
                         ok          = (SEG1 || L.seg == seg) && apply_bits<KIND, false>(L, g, slice);
                     }
                     pass |= (ok ? 1u : 0u) << i;
@@ -1212,18 +1220,34 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
             // ---- ranks inside the piece's sub runs
             const bool dense = nsv <= kScrCap;  // wave-uniform
             uint32_t   dc[kDense], dr[kDense];   // dense: code; rank << 16 | sub
+            bool       okd[kDense];              // dense: the entry survives
             uint32_t   rank2[NW / 2];            // word by word: two 16-bit ranks per register
             if (dense) {
 #pragma unroll
                 for (int k = 0; k < kDense; k++) {
                     const uint32_t j  = lane + 64u * k;
-                    const uint32_t c  = decode_k<KIND>(scr[j], q, g.log2F);
+                    const uint32_t w  = scr[j];
+                    const uint32_t c  = decode_k<KIND>(w, q, g.log2F);
                     const uint32_t s  = (c >> g.sub_shift) & (NSUB - 1u);
-                    const bool     ok = j < nsv;
-                    dc[k] = c;
+                    bool           ok = j < nsv;
+                    if (refine) ok = ok && apply_bits<KIND, false>(locate<KIND>(w, g, inv, q), g, slice);
+                    dc[k]  = c;
+                    okd[k] = ok;
                     dr[k] = s | (atomicAdd(&cnt[ok ? s : 64u + lane], 1u) << 16);  // dummies: 64..127
                 }
             } else {
+                if (refine) {  // too many first-bit candidates: the full test of every word
+                    pass = 0;
+#pragma unroll
+                    for (int i = 0; i < NW; i++) {
+                        bool ok = (uint32_t) (i & 3) < Sc.n[i >> 2];
+                        if (ok) {
+                            const Loc L = locate<KIND>(sweep_word(Sc, i >> 2, i & 3), g, inv, q);
+                            ok          = (SEG1 || L.seg == seg) && apply_bits<KIND, false>(L, g, slice);
+                        }
+                        pass |= (ok ? 1u : 0u) << i;
+                    }
+                }
 #pragma unroll
                 for (int i = 0; i < NW; i += 2) {
                     uint32_t r[2] = {0, 0};
@@ -1261,7 +1285,7 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
             if (dense) {
 #pragma unroll
                 for (int k = 0; k < kDense; k++) {
-                    const bool     ok = lane + 64u * k < nsv;
+                    const bool     ok = okd[k];
                     const uint32_t o  = subo[dr[k] & 0xFFFFu] + (dr[k] >> 16);
                     if (staged) stg[ok ? o : scap + lane] = dc[k];
                     else __builtin_amdgcn_raw_buffer_store_b32(dc[k], ro, ok ? o * 4 : 0x7FFFFFF0u, 0, 0);
@@ -1672,7 +1696,8 @@ uint32_t build_sweep_slot() { return kBSlot; }
 
 int consumer_kind(const Geometry& g) {
     if (g.mode == MODE_SLICE_BASIC) return KIND_BASIC_K1;
-    if (g.mode == MODE_SLICE_BLOCK) return g.format == FMT_PACKED ? KIND_BLOCK_PK1 : KIND_BLOCK;
+    if (g.mode == MODE_SLICE_BLOCK)
+        return g.format == FMT_PACKED ? (g.k == 1 ? KIND_BLOCK_PK1 : KIND_BLOCK_PKK) : KIND_BLOCK;
     return KIND_PASS;
 }
 
@@ -1697,6 +1722,7 @@ void launch_build(const BuildParams& p, uint32_t F, hipStream_t st) {
     const size_t lds = slice_lds_bytes(p.g);
     switch (consumer_kind(p.g)) {
         case KIND_BLOCK_PK1: return build_inst<KIND_BLOCK_PK1>(p, F, lds, st);
+        case KIND_BLOCK_PKK: return build_inst<KIND_BLOCK_PKK>(p, F, lds, st);
         case KIND_BLOCK: return build_inst<KIND_BLOCK>(p, F, lds, st);
         case KIND_BASIC_K1: return build_inst<KIND_BASIC_K1>(p, F, lds, st);
         default: return build_inst<KIND_PASS>(p, F, lds, st);
@@ -1707,7 +1733,8 @@ void launch_build(const BuildParams& p, uint32_t F, hipStream_t st) {
 size_t probe_lds_bytes(const Geometry& g, uint32_t* stage_cap) {
     const bool   slices = g.mode == MODE_SLICE_BLOCK || g.mode == MODE_SLICE_BASIC;
     const size_t NSUB   = (size_t) 1 << g.log2NSUB;
-    const size_t base   = ((slices ? g.seg_words : 0) + 128 + 3 * 128 + 16 * NSUB + 16 * (kScrCap + 64)) * sizeof(uint32_t);
+    const size_t scap   = consumer_kind(g) == KIND_BLOCK_PKK ? scr_cap<KIND_BLOCK_PKK>() : scr_cap<KIND_PASS>();
+    const size_t base   = ((slices ? g.seg_words : 0) + 128 + 3 * 128 + 16 * NSUB + 16 * (scap + 64)) * sizeof(uint32_t);
     // 2 buffers of cap words + 64 dummy slots each
     size_t cap = std::min<size_t>(kProbeCH * 32, (163840 - base) / 8 - 64) & ~(size_t) 3;
     if (stage_cap) *stage_cap = (uint32_t) cap;
@@ -1719,6 +1746,7 @@ void launch_probe(const ProbeParams& p0, uint32_t grid, hipStream_t st) {
     const size_t lds = probe_lds_bytes(p.g, &p.stage_cap);
     switch (consumer_kind(p.g)) {
         case KIND_BLOCK_PK1: return probe_inst<KIND_BLOCK_PK1>(p, grid, lds, st);
+        case KIND_BLOCK_PKK: return probe_inst<KIND_BLOCK_PKK>(p, grid, lds, st);
         case KIND_BLOCK: return probe_inst<KIND_BLOCK>(p, grid, lds, st);
         case KIND_BASIC_K1: return probe_inst<KIND_BASIC_K1>(p, grid, lds, st);
         default: return probe_inst<KIND_PASS>(p, grid, lds, st);
