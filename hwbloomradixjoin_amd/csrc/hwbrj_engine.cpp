@@ -243,7 +243,7 @@ void Engine::release() {
     for (DevBuf* b : {&poolR, &metaR, &usedR, &wgqcR, &wgqeR, &wgqoR, &lstartR, &estartR, &istartR,
                       &listR, &poolS, &metaS, &usedS, &wgqcS, &wgqeS, &wgqoS, &lstartS, &estartS,
                       &istartS, &listS, &slices, &bitmap, &rjoin, &rrun, &surv, &survcnt, &survoff,
-                      &dense, &small, &colR, &colS, &mtab, &mcount})
+                      &dense, &small, &colR, &colS, &mtab, &mcount, &jtask, &jparts})
         b->release();
     have_filter_ = false;
 }
@@ -296,6 +296,9 @@ int Engine::run(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     ok &= surv.ensure(nseg * LS * 128) && survcnt.ensure(items_max * NSUB * 4) &&
           survoff.ensure(items_max * NSUB * 4);
     ok &= small.ensure(64) && colR.ensure(F * 12) && colS.ensure(F * 12);  // u64 elems | u32 chunks
+    // jparts: nparts [NJ] | job_surv [NJ] | nextra; jtask: extra parts {job, part}
+    const bool jnew = jparts.bytes < (size_t) (2 * NJ + 1) * 4;
+    ok &= jtask.ensure((size_t) join_extra_tasks() * 8) && jparts.ensure((size_t) (2 * NJ + 1) * 4);
     if (slice_mode) ok &= slices.ensure((uint64_t) F * nseg * g.seg_words * 4);
     if (g.mode == MODE_GLOBAL) ok &= bitmap.ensure(((g.m + 31) / 32) * 4) && dense.ensure(nS * 4);
     if (!ok) {
@@ -306,8 +309,11 @@ int Engine::run(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     uint64_t* d_dcount   = small.as<uint64_t>() + 1;  // [1] dense survivor count (global mode)
     uint64_t* d_filtered = small.as<uint64_t>() + 2;  // [2] S-tuples after filter
 
-    // zeroing outside the timed region (the reference callocs before its timer, :1583, :1601)
+    // zeroing outside the timed region (the reference callocs before its timer, :1583, :1601);
+    // job_surv is left zero by every join's k_join_split, so it is cleared only when new
     HWBRJ_CHECK(hipMemsetAsync(small.p, 0, 64, stream));
+    if (jnew) HWBRJ_CHECK(hipMemsetAsync(jparts.p, 0, jparts.bytes, stream));
+    HWBRJ_CHECK(hipMemsetAsync(jparts.as<uint32_t>() + 2 * NJ, 0, 4, stream));
     if (g.mode == MODE_GLOBAL) HWBRJ_CHECK(hipMemsetAsync(bitmap.p, 0, bitmap.bytes, stream));
 
     ScatterParams sp{};
@@ -395,6 +401,7 @@ int Engine::run(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     pp.surv_cnt        = survcnt.as<uint32_t>();
     pp.surv_off        = survoff.as<uint32_t>();
     pp.filtered        = d_filtered;
+    pp.job_surv        = jparts.as<uint32_t>() + NJ;
     const size_t   pl_lds = probe_lds_bytes(g, nullptr);
     const uint32_t PG = (uint32_t) cus_ * (uint32_t) std::max<size_t>(1, std::min<size_t>(2, 163840 / pl_lds));
     const bool dbg_on = getenv("HWBRJ_DBG") != nullptr;  // dev-only phase stamps
@@ -427,7 +434,10 @@ int Engine::run(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     jp.bitmap          = (g.sub_shift > 0 && 32 - g.hash_shift <= 18) ? 1u : 0u;
     jp.result          = d_result;
     jp.dbg             = dbg_on ? dbgJ.as<uint64_t>() : nullptr;
-    launch_join(jp, NJ, stream);
+    jp.nparts          = jparts.as<uint32_t>();
+    jp.extra           = jtask.as<uint2>();
+    jp.nextra          = jparts.as<uint32_t>() + 2 * NJ;
+    launch_join(jp, NJ, jparts.as<uint32_t>() + NJ, stream);
     HWBRJ_CHECK(hipEventRecord(ev_[8], stream));
     HWBRJ_CHECK(hipGetLastError());
     HWBRJ_CHECK(hipEventSynchronize(ev_[8]));

@@ -57,6 +57,7 @@ class Engine {
     DevBuf slices, bitmap, rjoin, rrun, surv, survcnt, survoff, dense, small, dbgP, dbgJ, dbgS;
     DevBuf colR, colS;  // per-partition totals from k_plan: u64 elements [F], then u32 chunks [F]
     DevBuf mtab, mcount;  // materialization: R table, pair counter
+    DevBuf jtask, jparts;  // join task table; parts per job (+ the task count)
 };
 
 Engine* engine_for_current_device();

@@ -54,6 +54,7 @@ struct ProbeParams {
     uint32_t*        surv_cnt;    // [items][NSUB] survivors of each (item, sub) run
     uint32_t*        surv_off;    // [items][NSUB] run offset inside the item region
     uint64_t*        filtered;    // += survivors ("S-tuples after filter")
+    uint32_t*        job_surv;    // [F * NSUB] += survivors of each join job (zero on entry)
     uint32_t         stage_cap;   // survivor stage words (set by launch_probe)
     uint64_t*        dbg;         // dev-only: per-workgroup phase cycles (HWBRJ_DBG), or nullptr
 };
@@ -73,6 +74,10 @@ struct JoinParams {
     uint32_t        slot;         // r_codes words per build sweep
     uint32_t        bitmap;       // 1: keys fit the direct-address bitmap (32 - hash_shift <= 18)
     uint64_t*       result;
+    uint32_t        jobs;         // F * NSUB (set by launch_join)
+    uint32_t*       nparts;       // [jobs] parts of each job (k_join_split)
+    uint2*          extra;        // [join_extra_tasks()] {job, part} of the further parts
+    uint32_t*       nextra;       // parts requested beyond part 0 (zeroed before the join)
     uint64_t*       dbg;          // dev-only: per-workgroup phase cycles (HWBRJ_DBG), or nullptr
 };
 
@@ -105,7 +110,9 @@ uint32_t build_chunks_per_sweep();  // R chunks per k_build sweep
 uint32_t build_sweep_slot();        // out_codes words per k_build sweep
 void   launch_build(const BuildParams& p, uint32_t F, hipStream_t st);
 void   launch_probe(const ProbeParams& p, uint32_t grid, hipStream_t st);
-void   launch_join(const JoinParams& p, uint32_t jobs, hipStream_t st);
+// splits skewed jobs (job_surv: survivors per job from k_probe, cleared here) and runs the join
+void   launch_join(const JoinParams& p, uint32_t jobs, uint32_t* job_surv, hipStream_t st);
+uint32_t join_extra_tasks();
 // result materialization (K12): R table build, S probe writing (R.payload, S.payload) pairs
 void   launch_mat_build(const uint2* R, uint64_t n, unsigned long long* tab, uint64_t mask,
                         hipStream_t st);

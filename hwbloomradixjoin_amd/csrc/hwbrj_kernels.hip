@@ -1106,7 +1106,7 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
     // buffer stores whatever the counts (out-of-range ones are dropped), so the compiler never has
     // to wait for them (vmcnt counts stores on gfx9).
     constexpr uint32_t kNoItem = 0x80000000u;
-    uint32_t  prev_total = 0, prev_it = kNoItem, prev_buf = 0, subc_v = 0, subo_v = 0;
+    uint32_t  prev_total = 0, prev_it = kNoItem, prev_buf = 0, subc_v = 0, subo_v = 0, prev_q = 0;
     uint32_t* prev_out   = P.surv;
     auto copy_out = [&]() {
         const uint32_t nbytes = ((prev_total + 3u) & ~3u) * 4u;  // item region holds round_up(total, 4)
@@ -1122,6 +1122,10 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
         const auto rc = buf_rsrc(P.surv_cnt + (uint64_t) (prev_it & ~kNoItem) * NSUB, tb);
         const auto rf = buf_rsrc(P.surv_off + (uint64_t) (prev_it & ~kNoItem) * NSUB, tb);
         __builtin_amdgcn_raw_buffer_store_b32(subc_v, rc, tid * 4, 0, 0);
+        // survivors per join job (q, sub), for the join's skew split (every wave issues the one
+        // atomic; only wave 0's first NSUB lanes are in range)
+        const auto rj = buf_rsrc(P.job_surv + (uint64_t) prev_q * NSUB, tb);
+        __builtin_amdgcn_raw_ptr_buffer_atomic_add_i32((int) subc_v, rj, tid * 4, 0, 0);
         __builtin_amdgcn_raw_buffer_store_b32(subo_v, rf, tid * 4, 0, 0);
     };
     uint64_t filtered = 0;  // wave 0: survivors of this workgroup's items
@@ -1310,6 +1314,7 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
             prev_out   = out;
             prev_buf   = buf;
             prev_it    = rit0 + (p - p0);
+            prev_q     = q;
             nstep++;
             stamp(5);
         };
@@ -1367,6 +1372,37 @@ __device__ __forceinline__ void join_insert(uint32_t* keys, uint32_t v) {
     while (atomicCAS(&keys[h], kEmpty, v) != kEmpty) h = (h + 1u) & (kJoinT - 1u);
 }
 
+// Join tasks. A (q, sub) job whose survivors exceed kJoinTaskSurv (probe-side skew, e.g. the
+// hot keys of a Zipf S) is split into parts over q's probe items; every part rebuilds the job's
+// small R table and counts its share of the survivors. k_probe sums the survivors of every job
+// (job_surv); k_join_split gives part 0 of job j to workgroup j and appends the further parts to
+// a table read by kJoinExtra extra workgroups (first come, first served: the table bounds the
+// added parts). It also clears job_surv for the next join.
+constexpr uint32_t kJoinTaskSurv = 1u << 17;
+constexpr uint32_t kJoinExtra    = 2048;
+
+__global__ __launch_bounds__(256) void k_join_split(const uint32_t* __restrict__ item_start,
+                                                     uint32_t* __restrict__ job_surv,
+                                                     uint32_t log2NSUB, uint32_t NJ,
+                                                     uint32_t* __restrict__ nparts,
+                                                     uint2* __restrict__ extra, uint32_t* nextra) {
+    const uint32_t job = blockIdx.x * blockDim.x + threadIdx.x;  // one thread per job
+    if (job >= NJ) return;
+    const uint32_t q = job >> log2NSUB, items = item_start[q + 1] - item_start[q];
+    const uint32_t tot = job_surv[job];
+    job_surv[job]      = 0;
+    const uint32_t want = min(max((tot + kJoinTaskSurv - 1) / kJoinTaskSurv, 1u), max(items, 1u));
+    uint32_t       np   = 1;
+    if (want > 1) {
+        const uint32_t base = atomicAdd(nextra, want - 1);
+        if (base < kJoinExtra) {
+            np = 1 + min(want - 1, kJoinExtra - base);
+            for (uint32_t p = 1; p < np; p++) extra[base + p - 1] = make_uint2(job, p);
+        }
+    }
+    nparts[job] = np;
+}
+
 __global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
     __shared__ __attribute__((aligned(16))) uint32_t tab[kJoinWords];  // bitmap or hash table
     __shared__ uint64_t dbase[kJoinDesc];  // run starts (words) of a batch: S survivor runs
@@ -1377,12 +1413,23 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
     __shared__ uint64_t wsum[kJoinWaves];
     __shared__ uint32_t dupflag, npieces;
     const uint32_t NSUB = 1u << P.log2NSUB;
-    const uint32_t job  = blockIdx.x, q = job >> P.log2NSUB, s = job & (NSUB - 1u);
+    uint32_t       job = blockIdx.x, part = 0;  // workgroup j < jobs: part 0 of job j
+    if (blockIdx.x >= P.jobs) {                 // extra workgroups: further parts of skewed jobs
+        const uint32_t e = blockIdx.x - P.jobs;
+        if (e >= min(*P.nextra, kJoinExtra)) return;
+        const uint2 x = P.extra[e];
+        job           = x.x;
+        part          = x.y;
+    }
+    const uint32_t q = job >> P.log2NSUB, s = job & (NSUB - 1u);
     const uint32_t w0 = P.r_sweep_start[q], w1 = P.r_sweep_start[q + 1];
-    const uint32_t i0 = P.item_start[q], i1 = P.item_start[q + 1];
+    const uint32_t qi0 = P.item_start[q], qi1 = P.item_start[q + 1];  // q's items (segment-major)
+    const uint32_t np  = P.nparts[job];
+    const uint32_t i0  = qi0 + (uint32_t) ((uint64_t) (qi1 - qi0) * part / np);
+    const uint32_t i1  = qi0 + (uint32_t) ((uint64_t) (qi1 - qi0) * (part + 1) / np);
     if (w1 == w0 || i1 == i0) return;
     const uint32_t lq0 = P.list_start[q];
-    const uint32_t npc = (i1 - i0) / P.nseg;  // probe pieces of q (items are segment-major)
+    const uint32_t npc = (qi1 - qi0) / P.nseg;  // probe pieces of q
     const uint32_t sh  = P.hash_shift;
     const int      tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     uint64_t       cnt = 0;
@@ -1433,7 +1480,7 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
             __syncthreads();  // previous descriptors consumed
             if ((uint32_t) tid < nd) {
                 const uint32_t it    = d0 + tid;
-                const uint32_t local = it - i0;
+                const uint32_t local = it - qi0;
                 const uint32_t seg   = local / npc;
                 const uint32_t piece = local - seg * npc;
                 dcnt[tid]  = P.surv_cnt[(uint64_t) it * NSUB + s];
@@ -1755,9 +1802,15 @@ void launch_probe(const ProbeParams& p0, uint32_t grid, hipStream_t st) {
 
 uint32_t probe_chunks_per_item() { return kProbeCH; }
 
-void launch_join(const JoinParams& p, uint32_t jobs, hipStream_t st) {
-    k_join<<<jobs, kJoinThreads, 0, st>>>(p);
+void launch_join(const JoinParams& p0, uint32_t jobs, uint32_t* job_surv, hipStream_t st) {
+    JoinParams p = p0;
+    p.jobs       = jobs;
+    k_join_split<<<(jobs + 255) / 256, 256, 0, st>>>(p.item_start, job_surv, p.log2NSUB, jobs,
+                                                     p.nparts, p.extra, p.nextra);
+    k_join<<<jobs + kJoinExtra, kJoinThreads, 0, st>>>(p);
 }
+
+uint32_t join_extra_tasks() { return kJoinExtra; }
 
 void launch_export(const uint32_t* slices, const Geometry& g, uint32_t* out, uint64_t nwords,
                    hipStream_t st) {
