@@ -7,6 +7,7 @@
 #include "hwbrj_engine.h"
 
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -165,6 +166,8 @@ bool plan_geometry(const bloom_filter_args_t* a, uint64_t nR, Geometry* g, std::
             if (B >= 8 && m >= 32 && (m / B) <= 0xFFFFFFFFull) {
                 g->mode = MODE_SLICE_BLOCK;
                 F       = std::min<uint64_t>(std::min<uint64_t>(1024, m / B), m / 32);
+                if (const char* e = getenv("HWBRJ_DEV_MAXF"))  // dev-only experiments
+                    F = std::min<uint64_t>(F, strtoull(e, nullptr, 10));
             } else {
                 g->mode = MODE_GLOBAL;
             }
@@ -437,6 +440,8 @@ int Engine::run(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     jp.nparts          = jparts.as<uint32_t>();
     jp.extra           = jtask.as<uint2>();
     jp.nextra          = jparts.as<uint32_t>() + 2 * NJ;
+    if (const char* e = getenv("HWBRJ_DEV_JOIN_SPLIT"))  // tests: force the skew split
+        jp.split_surv = (uint32_t) strtoul(e, nullptr, 10);
     launch_join(jp, NJ, jparts.as<uint32_t>() + NJ, stream);
     HWBRJ_CHECK(hipEventRecord(ev_[8], stream));
     HWBRJ_CHECK(hipGetLastError());

@@ -78,6 +78,7 @@ struct JoinParams {
     uint32_t*       nparts;       // [jobs] parts of each job (k_join_split)
     uint2*          extra;        // [join_extra_tasks()] {job, part} of the further parts
     uint32_t*       nextra;       // parts requested beyond part 0 (zeroed before the join)
+    uint32_t        split_surv;   // survivors per join part (0: the default, kJoinTaskSurv)
     uint64_t*       dbg;          // dev-only: per-workgroup phase cycles (HWBRJ_DBG), or nullptr
 };
 

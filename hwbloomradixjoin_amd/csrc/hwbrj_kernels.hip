@@ -1383,7 +1383,7 @@ constexpr uint32_t kJoinExtra    = 2048;
 
 __global__ __launch_bounds__(256) void k_join_split(const uint32_t* __restrict__ item_start,
                                                      uint32_t* __restrict__ job_surv,
-                                                     uint32_t log2NSUB, uint32_t NJ,
+                                                     uint32_t log2NSUB, uint32_t NJ, uint32_t split,
                                                      uint32_t* __restrict__ nparts,
                                                      uint2* __restrict__ extra, uint32_t* nextra) {
     const uint32_t job = blockIdx.x * blockDim.x + threadIdx.x;  // one thread per job
@@ -1391,7 +1391,7 @@ __global__ __launch_bounds__(256) void k_join_split(const uint32_t* __restrict__
     const uint32_t q = job >> log2NSUB, items = item_start[q + 1] - item_start[q];
     const uint32_t tot = job_surv[job];
     job_surv[job]      = 0;
-    const uint32_t want = min(max((tot + kJoinTaskSurv - 1) / kJoinTaskSurv, 1u), max(items, 1u));
+    const uint32_t want = min(max((uint32_t) (((uint64_t) tot + split - 1) / split), 1u), max(items, 1u));
     uint32_t       np   = 1;
     if (want > 1) {
         const uint32_t base = atomicAdd(nextra, want - 1);
@@ -1805,7 +1805,8 @@ uint32_t probe_chunks_per_item() { return kProbeCH; }
 void launch_join(const JoinParams& p0, uint32_t jobs, uint32_t* job_surv, hipStream_t st) {
     JoinParams p = p0;
     p.jobs       = jobs;
-    k_join_split<<<(jobs + 255) / 256, 256, 0, st>>>(p.item_start, job_surv, p.log2NSUB, jobs,
+    const uint32_t split = p.split_surv ? p.split_surv : kJoinTaskSurv;
+    k_join_split<<<(jobs + 255) / 256, 256, 0, st>>>(p.item_start, job_surv, p.log2NSUB, jobs, split,
                                                      p.nparts, p.extra, p.nextra);
     k_join<<<jobs + kJoinExtra, kJoinThreads, 0, st>>>(p);
 }

@@ -338,3 +338,17 @@ def test_bpro_materialized_result_list(hw, orc):
     want = orc.join_pairs(R, S)
     assert res.totalresults == want.shape[0] == res.pairs.shape[0] > 1024 * 1024
     assert np.array_equal(_sorted_pairs(res.pairs), _sorted_pairs(want))
+
+
+@pytest.mark.parametrize("split", ["700", "5000"])
+def test_join_skew_split_forced(hw, cuda, orc, gen3, split, monkeypatch):
+    """The join's skew split (extra parts over a job's probe items) forced on every job: the counts
+    and materialized pairs still equal the oracle's (Zipf S; non-unique R takes the hash path)."""
+    monkeypatch.setenv("HWBRJ_DEV_JOIN_SPLIT", split)
+    for mode in ("zipf", "nonunique"):
+        R, S = gen3[1][mode]
+        S = S[:4000000]
+        for args in (hw.BloomFilterArgs(hw.BLOCKED, 1 << 24, 1, 1024), None):
+            st = hw.join_device(to_dev(cuda, R), to_dev(cuda, S), args)
+            res, filt, _ = orc.bpro(R, S, 8, 1 if args else 0, 1 << 24, 1, 1024, args is not None)
+            assert (st.filtered, st.matches) == (filt, res)
