@@ -10,10 +10,12 @@
 //                (bloom add, src/bloom_filter.c:73-132), and sub-partition R codes for the join
 //                (pass-2, :703-748).
 //   k_probe      per item (partition, chunk range): test S elements against the LDS slice
-//                (bloom contains, src/bloom_filter.c:92-141), compact survivors.
-//   k_surv_*     sub-partition survivors for the join (pass-2 of S).
-//   k_join       per (partition, sub): LDS open-addressing table of R codes, probe S codes, count
-//                equal keys (bucket_chaining_join, :259-329).
+//                (bloom contains, src/bloom_filter.c:92-141), write the survivors grouped by join
+//                sub-partition (pass-2 of S).
+//   k_join_split splits (partition, sub) jobs with skewed survivor counts into parts.
+//   k_join       per job part: LDS bitmap (or hash table) of the R codes of (partition, sub),
+//                survivors count equal keys (bucket_chaining_join, :259-329).
+//   k_mat_*      result materialization (JOIN_RESULT_MATERIALIZE): {R.payload, S.payload} pairs.
 // Keys travel as 32-bit "codes" = crc32c(42, key): a bijection of the key, so code equality is key
 // equality and the code's low bits ARE the bloom block index.
 #include <hip/hip_runtime.h>
@@ -1040,11 +1042,17 @@ __global__ __launch_bounds__(1024) void k_build(BuildParams P) {
 // item's list entries and chunks are loaded while the current one is tested. Survivors are
 // written into the item's own region grouped by join sub-partition (LDS counters + one scan), so
 // the join reads them in place: surv_cnt[it][sub] / surv_off[it][sub] describe the runs.
-constexpr int      kPC      = 3;              // chunk quads per thread per item
+#ifndef HWBRJ_PC
+#define HWBRJ_PC 3
+#endif
+#ifndef HWBRJ_SCR1
+#define HWBRJ_SCR1 128
+#endif
+constexpr int      kPC      = HWBRJ_PC;       // chunk quads per thread per item
 constexpr uint32_t kProbeCH = 128u * kPC;     // chunks per probe item (1024 threads, 8 per chunk)
 // compacted survivors (first-bit candidates for KIND_BLOCK_PKK, whose rate is higher) per wave
 // and item in the LDS scratch, and the dense ranking rounds per wave
-template <int KIND> constexpr uint32_t scr_cap() { return KIND == KIND_BLOCK_PKK ? 256u : 128u; }
+template <int KIND> constexpr uint32_t scr_cap() { return KIND == KIND_BLOCK_PKK ? 256u : (uint32_t) HWBRJ_SCR1; }
 
 __device__ __forceinline__ uint32_t find_q(const uint32_t* item_start, uint32_t F, uint32_t it) {
     uint32_t lo = 0, hi = F - 1;

@@ -108,7 +108,7 @@ typedef struct hwbrj_stats_t {
     double   ms_s_scatter;  /* S -> partitions (the dominant, HBM-bound kernel) */
     double   ms_s_index;
     double   ms_probe;      /* filter probe + survivor compaction */
-    double   ms_surv;       /* survivor sub-partitioning */
+    double   ms_surv;       /* survivor sub-partitioning: fused into the probe (k_probe), ~0 */
     double   ms_join;
 } hwbrj_stats_t;
 

@@ -15,8 +15,8 @@ from collections import defaultdict
 
 # dispatch order of one join (hwbrj_engine.cpp Engine::run) -> phase
 PHASE_OF = {"k_build_global": "build", "k_build": "build", "k_probe_global": "probe",
-            "k_probe": "probe", "k_surv_totals": "surv", "k_scan_u64": "surv",
-            "k_surv_scatter": "surv", "k_join": "join", "k_plan": "index", "k_list_fill": "index"}
+            "k_probe": "probe", "k_join_split": "join", "k_join": "join", "k_plan": "index",
+            "k_list_fill": "index", "k_mat_build": "materialize", "k_mat_probe": "materialize"}
 
 
 def one(path_glob):
