@@ -538,9 +538,13 @@ int Engine::materialize(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t 
     HWBRJ_CHECK(hipMemsetAsync(mcount.p, 0, 8, stream));
     HWBRJ_CHECK(hipEventRecord(ev_[0], stream));
     if (nR) launch_mat_build(dR, nR, mtab.as<unsigned long long>(), T - 1, stream);
-    if (nR && nS)
+    if (nR && nS) {
+        Geometry g = last_g_;  // the counting join's filter (materialize follows it)
+        if (!have_filter_) g.mode = MODE_NOBLOOM;
         launch_mat_probe(dS, nS, dR, mtab.as<unsigned long long>(), T - 1, out, cap,
-                         mcount.as<unsigned long long>(), stream);
+                         mcount.as<unsigned long long>(), g, slices.as<uint32_t>(),
+                         bitmap.as<uint32_t>(), d_tabs_, stream);
+    }
     HWBRJ_CHECK(hipEventRecord(ev_[1], stream));
     HWBRJ_CHECK(hipGetLastError());
     HWBRJ_CHECK(hipEventSynchronize(ev_[1]));

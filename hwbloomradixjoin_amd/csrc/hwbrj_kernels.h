@@ -117,9 +117,11 @@ uint32_t join_extra_tasks();
 // result materialization (K12): R table build, S probe writing (R.payload, S.payload) pairs
 void   launch_mat_build(const uint2* R, uint64_t n, unsigned long long* tab, uint64_t mask,
                         hipStream_t st);
+// g/slices/bm/tabs: the last join's filter, used as a pre-test (g.mode = MODE_NOBLOOM: none)
 void   launch_mat_probe(const uint2* S, uint64_t n, const uint2* R, const unsigned long long* tab,
                         uint64_t mask, uint2* out, uint64_t cap, unsigned long long* count,
-                        hipStream_t st);
+                        const Geometry& g, const uint32_t* slices, const uint32_t* bm,
+                        const CrcTables* tabs, hipStream_t st);
 void   launch_export(const uint32_t* slices, const Geometry& g, uint32_t* out, uint64_t nwords,
                      hipStream_t st);
 

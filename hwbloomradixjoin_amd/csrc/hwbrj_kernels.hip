@@ -1623,44 +1623,93 @@ __global__ __launch_bounds__(256) void k_mat_build(const uint2* __restrict__ R, 
     }
 }
 
+// The last join's filter as a pre-test (no false negatives, so it only skips table walks): the
+// reference bits of the key (src/bloom_filter.c:73-141) read from the partition slices (or the
+// global bitmap of MODE_GLOBAL).
+__device__ __forceinline__ bool mat_filter(uint32_t key, const Geometry& g, const uint32_t* slices,
+                                           const uint32_t* bm, const CrcTables* tabs) {
+    if (g.mode == MODE_NOBLOOM) return true;
+    const uint32_t code = key_code(&tabs->fwd[0][0], key);
+    if (g.mode == MODE_GLOBAL) return global_contains(key, code, g, bm);
+    const uint32_t F1 = (1u << g.log2F) - 1u;
+    auto bit = [&](uint32_t q, uint32_t sb) {  // bit sb of slice q
+        const uint32_t* w = slices + ((uint64_t) q * g.nseg + (sb >> g.log2seg)) * g.seg_words;
+        const uint32_t  o = sb & (g.seg_bits - 1u);
+        return (w[o >> 5] >> (o & 31u)) & 1u;
+    };
+    if (g.mode == MODE_SLICE_BASIC) {  // k = 1
+        const uint32_t b = mod_m(crapwow(kSeed, key), (uint32_t) g.m);
+        return bit(b & F1, b >> g.log2F);
+    }
+    const uint32_t q    = code & F1;
+    const uint32_t base = ((code >> g.log2F) & g.lbmask) << g.log2B;
+    const uint32_t mask = g.B - 1u;
+    uint32_t       h = crapwow(kSeed, key) & mask, y = (key + kSeed) & mask;
+    const uint32_t s0 = h >> g.log2secw;
+    for (uint32_t i = 0; i < g.k; i++) {
+        const uint32_t pos = g.variant == VAR_SECTORIZED
+                                 ? (((s0 + i) & g.nsecmask) << g.log2secw) | (h & ((1u << g.log2secw) - 1u))
+                                 : h;
+        if (!bit(q, base + pos)) return false;
+        h = (h + y) & mask;
+        y = (y + i + 1u) & mask;
+    }
+    return true;
+}
+
+constexpr uint32_t kMatBuf = 4096;  // pairs staged in LDS per workgroup before one output atomic
+
 __global__ __launch_bounds__(256) void k_mat_probe(const uint2* __restrict__ S, uint64_t n,
                                                     const uint2* __restrict__ R,
                                                     const unsigned long long* __restrict__ tab,
                                                     uint64_t mask, uint2* __restrict__ out,
-                                                    uint64_t cap, unsigned long long* __restrict__ count) {
-    const int      lane   = threadIdx.x & 63;
-    const uint64_t stride = (uint64_t) gridDim.x * blockDim.x;
-    for (uint64_t i0 = blockIdx.x * (uint64_t) blockDim.x; i0 < n; i0 += stride) {  // uniform per wave
-        const uint64_t i   = i0 + threadIdx.x;
-        const bool     ok  = i < n;
-        const uint2    st  = ok ? S[i] : make_uint2(0, 0);
-        uint32_t       hit = 0;
-        if (ok) {
-            for (uint64_t h = mat_slot(st.x, mask);; h = (h + 1) & mask) {
-                const unsigned long long e = tab[h];
-                if (e == 0ull) break;
-                hit += (uint32_t) e == st.x;
-            }
-        }
-        const uint32_t incl = wave_incl_scan_dpp(hit);
-        const uint32_t tot  = __builtin_amdgcn_readlane(incl, 63);
-        if (tot == 0) continue;  // uniform
-        unsigned long long base = 0;
-        if (lane == 0) base = atomicAdd(count, (unsigned long long) tot);
-        base = ((unsigned long long) __builtin_amdgcn_readfirstlane((uint32_t) (base >> 32)) << 32) |
-               __builtin_amdgcn_readfirstlane((uint32_t) base);
-        if (hit) {
-            uint64_t o = base + incl - hit;
-            for (uint64_t h = mat_slot(st.x, mask);; h = (h + 1) & mask) {
-                const unsigned long long e = tab[h];
-                if (e == 0ull) break;
-                if ((uint32_t) e == st.x) {
-                    if (o < cap) out[o] = make_uint2(R[(e >> 32) - 1].y, st.y);  // (R rid, S rid)
-                    o++;
+                                                    uint64_t cap, unsigned long long* __restrict__ count,
+                                                    Geometry g, const uint32_t* __restrict__ slices,
+                                                    const uint32_t* __restrict__ bm,
+                                                    const CrcTables* __restrict__ tabs) {
+    // Pairs are staged in LDS and appended to `out` with one atomic per flush (a single global
+    // counter taken per wave serialises at the L2); a burst beyond the stage takes one atomic per
+    // pair.
+    __shared__ uint2              buf[kMatBuf];
+    __shared__ uint32_t           nbuf;
+    __shared__ unsigned long long obase;
+    const uint64_t e0 = n * blockIdx.x / gridDim.x, e1 = n * (blockIdx.x + 1) / gridDim.x;
+    if (threadIdx.x == 0) nbuf = 0;
+    __syncthreads();
+    auto flush = [&]() {
+        const uint32_t c = min(nbuf, kMatBuf);
+        if (threadIdx.x == 0) obase = c ? atomicAdd(count, (unsigned long long) c) : 0ull;
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < c; i += blockDim.x)
+            if (obase + i < cap) out[obase + i] = buf[i];
+        __syncthreads();
+        if (threadIdx.x == 0) nbuf = 0;
+        __syncthreads();
+    };
+    for (uint64_t t0 = e0; t0 < e1; t0 += blockDim.x) {
+        const uint64_t i  = t0 + threadIdx.x;
+        if (i < e1) {
+            const uint2 st = S[i];
+            if (mat_filter(st.x, g, slices, bm, tabs)) {
+                for (uint64_t h = mat_slot(st.x, mask);; h = (h + 1) & mask) {
+                    const unsigned long long e = tab[h];
+                    if (e == 0ull) break;
+                    if ((uint32_t) e != st.x) continue;
+                    const uint2    pr   = make_uint2(R[(e >> 32) - 1].y, st.y);  // (R rid, S rid)
+                    const uint32_t slot = atomicAdd(&nbuf, 1u);
+                    if (slot < kMatBuf) {
+                        buf[slot] = pr;
+                    } else {  // burst beyond the stage
+                        const unsigned long long o = atomicAdd(count, 1ull);
+                        if (o < cap) out[o] = pr;
+                    }
                 }
             }
         }
+        __syncthreads();
+        if (nbuf >= kMatBuf / 2) flush();  // uniform (read after the barrier)
     }
+    flush();
 }
 
 void launch_mat_build(const uint2* R, uint64_t n, unsigned long long* tab, uint64_t mask, hipStream_t st) {
@@ -1668,8 +1717,10 @@ void launch_mat_build(const uint2* R, uint64_t n, unsigned long long* tab, uint6
 }
 
 void launch_mat_probe(const uint2* S, uint64_t n, const uint2* R, const unsigned long long* tab,
-                      uint64_t mask, uint2* out, uint64_t cap, unsigned long long* count, hipStream_t st) {
-    k_mat_probe<<<8192, 256, 0, st>>>(S, n, R, tab, mask, out, cap, count);
+                      uint64_t mask, uint2* out, uint64_t cap, unsigned long long* count,
+                      const Geometry& g, const uint32_t* slices, const uint32_t* bm,
+                      const CrcTables* tabs, hipStream_t st) {
+    k_mat_probe<<<2048, 256, 0, st>>>(S, n, R, tab, mask, out, cap, count, g, slices, bm, tabs);
 }
 
 // ===================================================================== launch wrappers

@@ -18,3 +18,6 @@ for i in range(3):
     print(f"q={q} count-join {st.ms_total:.3f} ms + pairs pass {ms:.3f} ms, pairs {pairs.shape[0]} "
           f"(= matches: {ok}, keys equal: {chk})", flush=True)
     del pairs
+# the R table build alone (one S tuple)
+st, pairs, ms = hw.join_materialize_device(dR, dS[:1], args)
+print(f"R table build + 1-tuple probe: {ms:.3f} ms", flush=True)
