@@ -311,7 +311,7 @@ __global__ __launch_bounds__(1024) void k_probe_global(const uint2* S, uint64_t 
 constexpr int      kScThreads = 1024;
 #ifndef HWBRJ_SC_E
 #define HWBRJ_SC_E 8
-#define HWBRJ_SC_K 3
+#define HWBRJ_SC_K 2
 #endif
 #ifndef HWBRJ_SC_PRE
 #define HWBRJ_SC_PRE 1
@@ -554,7 +554,10 @@ __device__ __forceinline__ void scatter_body(const ScatterParams& P) {
             uint32_t x, idx;
             elem(R, base, j, x, idx);
             sc_word_lds0<SRC, MODE, FMT>(x, P.g, crc_tab, w[j], q[j]);
-            if ((j & 1) == 1) __builtin_amdgcn_sched_barrier(0);  // bound the CRC reads in flight
+#ifndef HWBRJ_SC_SB
+#define HWBRJ_SC_SB 2
+#endif
+            if ((j % HWBRJ_SC_SB) == HWBRJ_SC_SB - 1) __builtin_amdgcn_sched_barrier(0);  // bound the CRC reads in flight
         }
         if (!full) {
 #pragma unroll
