@@ -752,7 +752,10 @@ __global__ __launch_bounds__(1024) void k_plan(const uint32_t* __restrict__ wgq_
 // batches of kLfBatch, counting-sorted by partition in LDS and written out as contiguous runs per
 // partition, so the list stores are coalesced.
 constexpr uint32_t kLfThreads = 1024;
-constexpr uint32_t kLfPer     = 16;
+#ifndef HWBRJ_LFPER
+#define HWBRJ_LFPER 24
+#endif
+constexpr uint32_t kLfPer     = HWBRJ_LFPER;
 constexpr uint32_t kLfBatch   = kLfThreads * kLfPer;
 
 __global__ __launch_bounds__(kLfThreads) void k_list_fill(const uint32_t* __restrict__ meta,
@@ -942,7 +945,10 @@ __device__ __forceinline__ uint32_t sweep_word(const Sweep<NPQ>& S, int j, int t
 //     an LDS stage and written coalesced to the sweep's own kBSlot-word slot of out_codes, with a
 //     (sweep, sub) run table (pass-2 of R, src/parallel_radix_join_bloom.c:703-748). The join reads
 //     (q, sub) as the sub's runs in the slots of q's sweeps.
-constexpr int      kBPQ    = 4;               // sweeps per group (chunk quads per thread)
+#ifndef HWBRJ_BPQ
+#define HWBRJ_BPQ 2
+#endif
+constexpr int      kBPQ    = HWBRJ_BPQ;       // sweeps per group (chunk quads per thread)
 constexpr uint32_t kBSweep = 128u;            // chunks per sweep (8 threads per chunk)
 constexpr uint32_t kBSlot  = kBSweep * 32u;   // out_codes words per sweep (4096)
 
@@ -1234,8 +1240,10 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
             }
             // ---- ranks inside the piece's sub runs
             const bool dense = nsv <= kScrCap;  // wave-uniform
-            uint32_t   dc[kDense], dr[kDense];   // dense: code; rank << 16 | sub
-            bool       okd[kDense];              // dense: the entry survives
+            // dense: rank << 16 | sub of scratch entry lane + 64 k (kNoRank: not a survivor); the
+            // code itself is re-read from the wave's scratch after the barrier (fewer live VGPRs)
+            constexpr uint32_t kNoRank = 0xFFFFFFFFu;
+            uint32_t   dr[kDense];
             uint32_t   rank2[NW / 2];            // word by word: two 16-bit ranks per register
             if (dense) {
 #pragma unroll
@@ -1246,9 +1254,8 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
                     const uint32_t s  = (c >> g.sub_shift) & (NSUB - 1u);
                     bool           ok = j < nsv;
                     if (refine) ok = ok && apply_bits<KIND, false>(locate<KIND>(w, g, inv, q), g, slice);
-                    dc[k]  = c;
-                    okd[k] = ok;
-                    dr[k] = s | (atomicAdd(&cnt[ok ? s : 64u + lane], 1u) << 16);  // dummies: 64..127
+                    const uint32_t r = atomicAdd(&cnt[ok ? s : 64u + lane], 1u);  // dummies: 64..127
+                    dr[k]            = ok ? (s | (r << 16)) : kNoRank;
                 }
             } else {
                 if (refine) {  // too many first-bit candidates: the full test of every word
@@ -1300,10 +1307,11 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
             if (dense) {
 #pragma unroll
                 for (int k = 0; k < kDense; k++) {
-                    const bool     ok = okd[k];
+                    const bool     ok = dr[k] != kNoRank;
+                    const uint32_t c  = decode_k<KIND>(scr[lane + 64u * k], q, g.log2F);
                     const uint32_t o  = subo[dr[k] & 0xFFFFu] + (dr[k] >> 16);
-                    if (staged) stg[ok ? o : scap + lane] = dc[k];
-                    else __builtin_amdgcn_raw_buffer_store_b32(dc[k], ro, ok ? o * 4 : 0x7FFFFFF0u, 0, 0);
+                    if (staged) stg[ok ? o : scap + lane] = c;
+                    else __builtin_amdgcn_raw_buffer_store_b32(c, ro, ok ? o * 4 : 0x7FFFFFF0u, 0, 0);
                 }
             } else if (staged) {  // LDS stage (copied out coalesced at the next piece)
 #pragma unroll
