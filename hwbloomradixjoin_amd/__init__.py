@@ -71,6 +71,13 @@ def lib() -> ctypes.CDLL:
             raise ImportError(f"{LIB_PATH} is missing: run `python -c 'import __graft_entry__ as g; "
                               "g.build()'` (the MI355X HIP library is required; there is no CPU "
                               "fallback)")
+        # torch-ROCm ships its own HIP runtime. If libhwbrj.so (linked against /opt/rocm's) is
+        # loaded first, torch's later device init leaves this library's runtime with no devices
+        # ("no ROCm-capable device"); loading torch's libraries first makes the two coexist.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = ctypes.CDLL(LIB_PATH)
         L.BPRO.restype = ctypes.POINTER(_Result)
         L.BPRO.argtypes = [ctypes.POINTER(_Relation), ctypes.POINTER(_Relation), ctypes.c_int,

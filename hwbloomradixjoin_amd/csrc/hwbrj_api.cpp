@@ -52,10 +52,7 @@ uint32_t hwbrj_hash_crapwow(uint32_t seed, int32_t key) { return crapwow(seed, (
 int hwbrj_join_device(const tuple_t* d_R, uint64_t nR, const tuple_t* d_S, uint64_t nS,
                       const bloom_filter_args_t* args, void* stream, hwbrj_stats_t* stats) {
     Engine* e = engine_for_current_device();
-    if (!e) {
-        set_last_error("no HIP device");
-        return 10;
-    }
+    if (!e) return 10;  // (last error set by engine_for_current_device)
     return e->run((const uint2*) d_R, nR, (const uint2*) d_S, nS, args, (hipStream_t) stream, stats);
 }
 
@@ -64,10 +61,7 @@ int hwbrj_join_materialize_device(const tuple_t* d_R, uint64_t nR, const tuple_t
                                   uint64_t capacity, uint64_t* n_out, void* stream,
                                   hwbrj_stats_t* stats, double* ms_materialize) {
     Engine* e = engine_for_current_device();
-    if (!e) {
-        set_last_error("no HIP device");
-        return 10;
-    }
+    if (!e) return 10;  // (last error set by engine_for_current_device)
     hwbrj_stats_t st;
     int rc = e->run((const uint2*) d_R, nR, (const uint2*) d_S, nS, args, (hipStream_t) stream, &st);
     if (rc) return rc;
@@ -95,10 +89,7 @@ void hwbrj_set_materialize(int on) { g_materialize = on ? 1 : 0; }
 int hwbrj_generate_device(tuple_t* d_out, uint64_t n, uint32_t nthreads, uint64_t maxid,
                           uint64_t threshold, double selectivity, uint64_t seed, void* stream) {
     Engine* e = engine_for_current_device();
-    if (!e) {
-        set_last_error("no HIP device");
-        return 10;
-    }
+    if (!e) return 10;  // (last error set by engine_for_current_device)
     return e->generate((uint2*) d_out, n, 0, n, nthreads, maxid, threshold, selectivity, seed,
                        (hipStream_t) stream);
 }
@@ -107,10 +98,7 @@ int hwbrj_generate_device_range(tuple_t* d_out, uint64_t n, uint64_t offset, uin
                                 uint32_t nthreads, uint64_t maxid, uint64_t threshold,
                                 double selectivity, uint64_t seed, void* stream) {
     Engine* e = engine_for_current_device();
-    if (!e) {
-        set_last_error("no HIP device");
-        return 10;
-    }
+    if (!e) return 10;  // (last error set by engine_for_current_device)
     return e->generate((uint2*) d_out, n, offset, count, nthreads, maxid, threshold, selectivity,
                        seed, (hipStream_t) stream);
 }
@@ -142,10 +130,7 @@ int hwbrj_generate_host(tuple_t* out, uint64_t n, uint32_t nthreads, uint64_t ma
 
 int hwbrj_export_filter(uint8_t* host_out, uint64_t nbytes) {
     Engine* e = engine_for_current_device();
-    if (!e) {
-        set_last_error("no HIP device");
-        return 10;
-    }
+    if (!e) return 10;  // (last error set by engine_for_current_device)
     return e->export_filter(host_out, nbytes);
 }
 

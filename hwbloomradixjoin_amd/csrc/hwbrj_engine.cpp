@@ -583,8 +583,16 @@ static std::mutex g_mu;
 static Engine*    g_engines[64] = {};
 
 Engine* engine_for_current_device() {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+    int        dev = 0;
+    hipError_t e   = hipGetDevice(&dev);
+    if (e != hipSuccess) {  // a runtime not yet initialised in this library's HIP instance
+        (void) hipInit(0);
+        e = hipGetDevice(&dev);
+    }
+    if (e != hipSuccess || dev < 0 || dev >= 64) {
+        set_last_error(std::string("no HIP device (hipGetDevice: ") + hipGetErrorString(e) + ")");
+        return nullptr;
+    }
     std::lock_guard<std::mutex> lk(g_mu);
     if (!g_engines[dev]) g_engines[dev] = new Engine(dev);
     return g_engines[dev];

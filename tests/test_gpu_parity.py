@@ -100,6 +100,26 @@ def test_northstar_golden(hw, full_scale):
         assert int(np.unpackbits(bm).sum()) == row["popcount"]
 
 
+@pytest.mark.parametrize("world", [2, 8])
+def test_northstar_rank_shards_sum_to_golden(hw, full_scale, cuda, world):
+    """What every rank of `bench.py --gpus N` computes (strong scaling): the replicated R and the
+    rank's S range regenerated on the device (generate_device_range, shard_range); the per-rank
+    counts summed over ranks (the all_reduce) must be the single-GPU golden."""
+    g = GOLD["F4_northstar"]
+    R, _ = full_scale
+    nS = 1024000000
+    tot = [0, 0]
+    for rank in range(world):
+        lo, hi = hw.shard_range(nS, rank, world)
+        S = cuda.empty((hi - lo, 2), dtype=cuda.int32, device="cuda")
+        hw.generate_device_range(S, nS, lo, 2, INT_MAX, 128000000, g["q"], 54321)
+        st = hw.join_device(R, S, hw.BloomFilterArgs(hw.BLOCKED, g["m"], 1, g["B"]))
+        tot[0] += st.filtered
+        tot[1] += st.matches
+        del S
+    assert tuple(tot) == (g["k1_filtered"], g["results"])
+
+
 @pytest.mark.parametrize("row", GOLD["F1_published"],
                          ids=lambda r: f"{r['variant']}-q{r['q']}-m{r['m']}-k{r['k']}-B{r['B']}")
 def test_published_thesis_rows(hw, full_scale, row):
