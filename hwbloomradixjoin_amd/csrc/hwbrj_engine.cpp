@@ -298,7 +298,7 @@ int Engine::run(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     ok &= rjoin.ensure(sweeps_max * SLOT * 4) && rrun.ensure(2 * sweeps_max * NSUB * 4);
     ok &= surv.ensure(nseg * LS * 128) && survcnt.ensure(items_max * NSUB * 4) &&
           survoff.ensure(items_max * NSUB * 4);
-    ok &= small.ensure(64) && colR.ensure(F * 12) && colS.ensure(F * 12);  // u64 elems | u32 chunks
+    ok &= small.ensure(128 + 64 * 128) && colR.ensure(F * 12) && colS.ensure(F * 12);  // u64 elems | u32 chunks
     // jparts: nparts [NJ] | job_surv [NJ] | nextra; jtask: extra parts {job, part}
     const bool jnew = jparts.bytes < (size_t) (2 * NJ + 1) * 4;
     ok &= jtask.ensure((size_t) join_extra_tasks() * 8) && jparts.ensure((size_t) (2 * NJ + 1) * 4);
@@ -436,6 +436,7 @@ int Engine::run(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     jp.hash_shift      = g.hash_shift;
     jp.bitmap          = (g.sub_shift > 0 && 32 - g.hash_shift <= 18) ? 1u : 0u;
     jp.result          = d_result;
+    jp.jsum            = (uint64_t*) ((char*) small.p + 128);  // 64 partial sums, one per 128-B line
     jp.dbg             = dbg_on ? dbgJ.as<uint64_t>() : nullptr;
     jp.nparts          = jparts.as<uint32_t>();
     jp.extra           = jtask.as<uint2>();

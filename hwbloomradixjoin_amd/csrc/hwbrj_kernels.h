@@ -74,6 +74,7 @@ struct JoinParams {
     uint32_t        slot;         // r_codes words per build sweep
     uint32_t        bitmap;       // 1: keys fit the direct-address bitmap (32 - hash_shift <= 18)
     uint64_t*       result;
+    uint64_t*       jsum;         // kJoinSumSlots partial sums, one per 128-byte line (zeroed by k_join_split)
     uint32_t        jobs;         // F * NSUB (set by launch_join)
     uint32_t*       nparts;       // [jobs] parts of each job (k_join_split)
     uint2*          extra;        // [join_extra_tasks()] {job, part} of the further parts

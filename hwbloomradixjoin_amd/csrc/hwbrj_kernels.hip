@@ -1400,11 +1400,19 @@ __device__ __forceinline__ void join_insert(uint32_t* keys, uint32_t v) {
 constexpr uint32_t kJoinTaskSurv = 1u << 17;
 constexpr uint32_t kJoinExtra    = 2048;
 
+// Match counts: every join workgroup adds its count to one of kJoinSumSlots partial sums (each in
+// its own 128-byte line, so the ~16K adds are not serialised on one address); k_join_sum adds them
+// into the result.
+constexpr uint32_t kJoinSumSlots = 64;
+constexpr uint32_t kJoinSumStride = 16;  // u64 words per slot (128 bytes)
+
 __global__ __launch_bounds__(256) void k_join_split(const uint32_t* __restrict__ item_start,
                                                      uint32_t* __restrict__ job_surv,
                                                      uint32_t log2NSUB, uint32_t NJ, uint32_t split,
                                                      uint32_t* __restrict__ nparts,
-                                                     uint2* __restrict__ extra, uint32_t* nextra) {
+                                                     uint2* __restrict__ extra, uint32_t* nextra,
+                                                     uint64_t* __restrict__ jsum) {
+    if (blockIdx.x == 0 && threadIdx.x < kJoinSumSlots) jsum[threadIdx.x * kJoinSumStride] = 0;
     const uint32_t job = blockIdx.x * blockDim.x + threadIdx.x;  // one thread per job
     if (job >= NJ) return;
     const uint32_t q = job >> log2NSUB, items = item_start[q + 1] - item_start[q];
@@ -1525,7 +1533,105 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
         __syncthreads();
     };
     bool hashed = !P.bitmap;
-    if (!hashed) {  // every R key sets bit v; a bit already set means a duplicate key
+    bool done   = false;
+#ifndef HWBRJ_JFR
+#define HWBRJ_JFR 8  // fused path: R runs per wave
+#define HWBRJ_JFW 5  // fused path: R words per lane per run (runs average slot / NSUB words)
+#endif
+    constexpr int FR = HWBRJ_JFR, FW = HWBRJ_JFW;
+    const uint32_t nRd = w1 - w0, nSd = i1 - i0;
+#ifdef HWBRJ_NOJFUSE
+    if (false) {
+#else
+    if (!hashed && nRd <= (uint32_t) (kJoinWaves * FR) && nSd <= kJoinDesc) {
+#endif
+        // Fused bitmap path (every job of the north star): both descriptor sets in one phase, then
+        // the loads of all R runs and of the first survivor runs are issued before any is used, so
+        // a job costs two memory latencies (descriptors, data) instead of one per batch.
+        for (uint32_t i = tid; i < kJoinWords / 4; i += kJoinThreads) ((uint4*) tab)[i] = make_uint4(0, 0, 0, 0);
+        if (tid == 0) dupflag = 0;
+        if ((uint32_t) tid < nRd) {
+            const uint64_t r = (uint64_t) (w0 + tid) * NSUB + s;
+            rcnt[tid]        = P.r_cnt[r];
+            rbase[tid]       = (uint64_t) (w0 + tid) * P.slot + P.r_off[r];
+        }
+        if ((uint32_t) tid < nSd) {
+            const uint32_t it    = i0 + tid;
+            const uint32_t local = it - qi0;
+            const uint32_t seg   = local / npc;
+            const uint32_t piece = local - seg * npc;
+            dcnt[tid]  = P.surv_cnt[(uint64_t) it * NSUB + s];
+            dbase[tid] = (uint64_t) seg * P.surv_seg_stride + (uint64_t) (lq0 + piece * P.CH) * 32 +
+                         P.surv_off[(uint64_t) it * NSUB + s];
+        }
+        __syncthreads();
+        constexpr int FS = HWBRJ_JSR, FSW = HWBRJ_JSW;
+        uint32_t rv[FR][FW], rn[FR], sv[FS][FSW], sn[FS];
+#pragma unroll
+        for (int r = 0; r < FR; r++) {
+            const uint32_t dd = wave + r * kJoinWaves;
+            rn[r]             = dd < nRd ? rcnt[dd] : 0u;
+#ifdef HWBRJ_ABL_JNOR
+            rn[r] = 0;  // dev ablation (results invalid)
+#endif
+            const uint64_t bb = dd < nRd ? rbase[dd] : 0ull;
+#pragma unroll
+            for (int j = 0; j < FW; j++) {
+                const uint32_t o = lane + 64u * j;
+                rv[r][j]         = o < rn[r] ? P.r_codes[bb + o] : 0u;
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < FS; r++) {
+            const uint32_t dd = wave + r * kJoinWaves;
+            sn[r]             = dd < nSd ? dcnt[dd] : 0u;
+#ifdef HWBRJ_ABL_JNOS
+            sn[r] = 0;  // dev ablation (results invalid)
+#endif
+            const uint64_t bb = dd < nSd ? dbase[dd] : 0ull;
+#pragma unroll
+            for (int j = 0; j < FSW; j++) {
+                const uint32_t o = lane + 64u * j;
+                sv[r][j]         = o < sn[r] ? P.surv[bb + o] : 0u;
+            }
+        }
+        uint32_t dup = 0;
+        auto     set = [&](uint32_t x) {
+            const uint32_t bit = 1u << (x & 31u);
+            dup |= atomicOr(&tab[x >> 5], bit) & bit;
+        };
+#pragma unroll
+        for (int r = 0; r < FR; r++) {
+#pragma unroll
+            for (int j = 0; j < FW; j++)
+                if (lane + 64u * j < rn[r]) set(rv[r][j] >> sh);
+            if (rn[r] > 64u * FW) {  // (rare) longer run
+                const uint64_t bb = rbase[wave + r * kJoinWaves];
+                for (uint32_t o = 64u * FW + lane; o < rn[r]; o += 64) set(P.r_codes[bb + o] >> sh);
+            }
+        }
+        if (dup) dupflag = 1;
+        __syncthreads();
+        hashed = dupflag != 0;  // uniform
+        if (!hashed) {
+            auto test = [&](uint32_t x) { cnt += (tab[x >> 5] >> (x & 31u)) & 1u; };
+#pragma unroll
+            for (int r = 0; r < FS; r++) {
+#pragma unroll
+                for (int j = 0; j < FSW; j++)
+                    if (lane + 64u * j < sn[r]) test(sv[r][j] >> sh);
+                if (sn[r] > 64u * FSW) {
+                    const uint64_t bb = dbase[wave + r * kJoinWaves];
+                    for (uint32_t o = 64u * FSW + lane; o < sn[r]; o += 64) test(P.surv[bb + o] >> sh);
+                }
+            }
+#ifndef HWBRJ_ABL_JNOS
+            walk(SR{}, SW{}, P.surv, dcnt, dbase, (uint32_t) (kJoinWaves * FS), nSd, test);
+#endif
+            done = true;
+        }
+    }
+    if (!hashed && !done) {  // every R key sets bit v; a bit already set means a duplicate key
         for (uint32_t i = tid; i < kJoinWords / 4; i += kJoinThreads) ((uint4*) tab)[i] = make_uint4(0, 0, 0, 0);
         if (tid == 0) dupflag = 0;
         uint32_t dup = 0;
@@ -1579,8 +1685,14 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
     if (tid == 0) {
         uint64_t t = 0;
         for (int w = 0; w < kJoinWaves; w++) t += wsum[w];
-        if (t) atomicAdd((unsigned long long*) P.result, (unsigned long long) t);
+        if (t) atomicAdd((unsigned long long*) &P.jsum[(blockIdx.x % kJoinSumSlots) * kJoinSumStride],
+                         (unsigned long long) t);
     }
+}
+
+__global__ __launch_bounds__(64) void k_join_sum(const uint64_t* __restrict__ jsum, uint64_t* result) {
+    const uint64_t v = wave_sum_u64(jsum[threadIdx.x * kJoinSumStride]);
+    if (threadIdx.x == 0 && v) atomicAdd((unsigned long long*) result, (unsigned long long) v);
 }
 
 // ============================================== K11: export the filter in reference layout
@@ -1877,8 +1989,9 @@ void launch_join(const JoinParams& p0, uint32_t jobs, uint32_t* job_surv, hipStr
     p.jobs       = jobs;
     const uint32_t split = p.split_surv ? p.split_surv : kJoinTaskSurv;
     k_join_split<<<(jobs + 255) / 256, 256, 0, st>>>(p.item_start, job_surv, p.log2NSUB, jobs, split,
-                                                     p.nparts, p.extra, p.nextra);
+                                                     p.nparts, p.extra, p.nextra, p.jsum);
     k_join<<<jobs + kJoinExtra, kJoinThreads, 0, st>>>(p);
+    k_join_sum<<<1, kJoinSumSlots, 0, st>>>(p.jsum, p.result);
 }
 
 uint32_t join_extra_tasks() { return kJoinExtra; }
