@@ -5,7 +5,8 @@ One step = one full BPRO join (filter build + probe + both partition passes + jo
 HBM-resident synthetic relations with the reference generator's key multiset
 (src/generator.c:304-415): |R| = 128M, |S| = 1024M, q = 0.01, -b blocked, m = 2^30, k = 1,
 B = 1024 (the reference default, src/main.c:393). value = probe tuples (|S|) per second over the
-whole job.
+whole job. The K timed joins are enqueued back to back (hwbrj_join_device_async) and waited for
+once, as a pipeline of joins runs; the phase breakdown comes from K synchronous joins afterwards.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (N > 1)
@@ -112,20 +113,30 @@ def main():
     for _ in range(a.warmup):
         hw.join_device(dR, dS, args)
 
-    sums = {}
+    # timed region: K full joins enqueued back to back (hwbrj_join_device_async: no host round
+    # trip between them), then one wait for the last; counts of the last join are checked below
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(a.steps):
-        st = hw.join_device(dR, dS, args)
-        for f in ("ms_total", "ms_r_scatter", "ms_r_index", "ms_build", "ms_s_scatter",
-                  "ms_s_index", "ms_probe", "ms_surv", "ms_join"):
-            sums[f] = sums.get(f, 0.0) + getattr(st, f)
+        hw.join_device_async(dR, dS, args)
+    last = hw.join_wait()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    if (last.filtered, last.matches) != (st.filtered, st.matches):
+        raise SystemExit(f"timed join counts {last.filtered, last.matches} differ from the parity "
+                         f"run {st.filtered, st.matches}")
+
+    # per-phase device times (HIP events, one synchronous join each, after the timed region)
+    sums = {}
+    for _ in range(a.steps):
+        st = hw.join_device(dR, dS, args)
+        for f in ("ms_total", "ms_r_scatter", "ms_r_index", "ms_build", "ms_s_scatter",
+                  "ms_s_index", "ms_probe", "ms_surv", "ms_join"):
+            sums[f] = sums.get(f, 0.0) + getattr(st, f)
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

@@ -17,7 +17,7 @@ import numpy as np
 
 __all__ = [
     "BASIC", "BLOCKED", "SECTORIZED", "BloomFilterArgs", "Relation", "Result", "Stats",
-    "BPRO", "PRO", "join_materialize_device", "set_materialize", "BPRH", "BPRHO", "BRJ", "PRH", "PRHO", "RJ", "assert_args", "join_device", "generate_device", "generate_device_range",
+    "BPRO", "PRO", "join_materialize_device", "set_materialize", "BPRH", "BPRHO", "BRJ", "PRH", "PRHO", "RJ", "assert_args", "join_device", "join_device_async", "join_wait", "generate_device", "generate_device_range",
     "generate_host", "nonunique_threshold", "create_relation_nonunique",
     "create_relation_nonunique_from_pk", "create_relation_fk_from_pk", "create_relation_zipf",
     "rand_stream", "reference_relations", "create_relation_zipf_device",
@@ -92,6 +92,11 @@ def lib() -> ctypes.CDLL:
             getattr(L, nm).argtypes = L.PRO.argtypes
         L.assert_args.argtypes = [ctypes.POINTER(_BloomArgs)]
         L.hwbrj_join_device.restype = ctypes.c_int
+        L.hwbrj_join_device_async.restype = ctypes.c_int
+        L.hwbrj_join_device_async.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                              ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]
+        L.hwbrj_join_wait.restype = ctypes.c_int
+        L.hwbrj_join_wait.argtypes = [ctypes.c_void_p]
         L.hwbrj_join_device.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
                                         ctypes.c_uint64, ctypes.POINTER(_BloomArgs),
                                         ctypes.c_void_p, ctypes.POINTER(_Stats)]
@@ -340,12 +345,34 @@ def _ptr(t) -> int:
     return int(t.data_ptr())
 
 
-def join_device(R, S, args: Optional[BloomFilterArgs] = None, stream=None) -> Stats:
-    """Join device-resident torch int32 tensors of shape (N, 2) ({key, payload}) in HBM.
-    args=None runs PRO. `stream` is a torch.cuda.Stream (default: the library's own stream)."""
+def _check_rel(R, S):
     for name, t in (("R", R), ("S", S)):
         if not t.is_cuda or t.dtype.itemsize != 4 or (t.numel() and t.shape[-1] != 2) or not t.is_contiguous():
             raise ValueError(f"{name} must be a contiguous (N, 2) int32 tensor on the GPU")
+
+
+def join_device_async(R, S, args: Optional[BloomFilterArgs] = None, stream=None) -> None:
+    """Enqueue the join of device tensors R, S without waiting (hwbrj_join_device_async);
+    join_wait() returns the Stats of the last join enqueued on this device."""
+    _check_rel(R, S)
+    a = args._c() if args is not None else None
+    sp = ctypes.c_void_p(stream.cuda_stream) if stream is not None else None
+    _err(lib().hwbrj_join_device_async(_ptr(R), R.shape[0], _ptr(S), S.shape[0],
+                                       ctypes.byref(a) if a is not None else None, sp),
+         "hwbrj_join_device_async")
+
+
+def join_wait() -> Stats:
+    """Wait for the last enqueued join on this device and return its Stats."""
+    st = _Stats()
+    _err(lib().hwbrj_join_wait(ctypes.byref(st)), "hwbrj_join_wait")
+    return Stats(**{n: getattr(st, n) for n, _ in _Stats._fields_})
+
+
+def join_device(R, S, args: Optional[BloomFilterArgs] = None, stream=None) -> Stats:
+    """Join device-resident torch int32 tensors of shape (N, 2) ({key, payload}) in HBM.
+    args=None runs PRO. `stream` is a torch.cuda.Stream (default: the library's own stream)."""
+    _check_rel(R, S)
     st = _Stats()
     a = args._c() if args is not None else None
     sp = ctypes.c_void_p(stream.cuda_stream) if stream is not None else None

@@ -56,6 +56,19 @@ int hwbrj_join_device(const tuple_t* d_R, uint64_t nR, const tuple_t* d_S, uint6
     return e->run((const uint2*) d_R, nR, (const uint2*) d_S, nS, args, (hipStream_t) stream, stats);
 }
 
+int hwbrj_join_device_async(const tuple_t* d_R, uint64_t nR, const tuple_t* d_S, uint64_t nS,
+                            const bloom_filter_args_t* args, void* stream) {
+    Engine* e = engine_for_current_device();
+    if (!e) return 10;  // (last error set by engine_for_current_device)
+    return e->run_async((const uint2*) d_R, nR, (const uint2*) d_S, nS, args, (hipStream_t) stream);
+}
+
+int hwbrj_join_wait(hwbrj_stats_t* stats) {
+    Engine* e = engine_for_current_device();
+    if (!e) return 10;
+    return e->wait(stats);
+}
+
 int hwbrj_join_materialize_device(const tuple_t* d_R, uint64_t nR, const tuple_t* d_S, uint64_t nS,
                                   const bloom_filter_args_t* args, tuple_t* d_out,
                                   uint64_t capacity, uint64_t* n_out, void* stream,

@@ -259,6 +259,17 @@ static uint64_t region_cap(uint64_t n, uint32_t G, uint32_t F) {
 
 int Engine::run(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
                 const bloom_filter_args_t* args, hipStream_t stream, hwbrj_stats_t* st) {
+    const int rc = enqueue(dR, nR, dS, nS, args, stream, getenv("HWBRJ_DBG") != nullptr);
+    return rc ? rc : wait(st);
+}
+
+int Engine::run_async(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
+                      const bloom_filter_args_t* args, hipStream_t stream) {
+    return enqueue(dR, nR, dS, nS, args, stream, false);
+}
+
+int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
+                    const bloom_filter_args_t* args, hipStream_t stream, bool dbg) {
     HWBRJ_CHECK(hipSetDevice(device_));
     Geometry    g;
     std::string err;
@@ -376,7 +387,7 @@ int Engine::run(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     sp.wgq_chunks = wgqcS.as<uint32_t>();
     sp.wgq_elems  = wgqeS.as<uint32_t>();
     sp.cap        = capS;
-    const bool dbg_sc = getenv("HWBRJ_DBG") != nullptr;  // dev-only phase stamps
+    const bool dbg_sc = dbg;  // dev-only phase stamps (HWBRJ_DBG)
     if (dbg_sc) {
         ok &= dbgS.ensure((size_t) G * 64);
         HWBRJ_CHECK(hipMemsetAsync(dbgS.p, 0, dbgS.bytes, stream));
@@ -407,7 +418,7 @@ int Engine::run(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     pp.job_surv        = jparts.as<uint32_t>() + NJ;
     const size_t   pl_lds = probe_lds_bytes(g, nullptr);
     const uint32_t PG = (uint32_t) cus_ * (uint32_t) std::max<size_t>(1, std::min<size_t>(2, 163840 / pl_lds));
-    const bool dbg_on = getenv("HWBRJ_DBG") != nullptr;  // dev-only phase stamps
+    const bool dbg_on = dbg;  // dev-only phase stamps (HWBRJ_DBG)
     if (dbg_on) {
         ok &= dbgP.ensure((size_t) std::max<uint32_t>(PG, F) * 64) && dbgJ.ensure((size_t) F * 64);
         HWBRJ_CHECK(hipMemsetAsync(dbgP.p, 0, dbgP.bytes, stream));
@@ -446,9 +457,14 @@ int Engine::run(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     launch_join(jp, NJ, jparts.as<uint32_t>() + NJ, stream);
     HWBRJ_CHECK(hipEventRecord(ev_[8], stream));
     HWBRJ_CHECK(hipGetLastError());
-    HWBRJ_CHECK(hipEventSynchronize(ev_[8]));
+    pending_      = true;
+    pending_args_ = args != nullptr;
+    pending_nS_   = nS;
+    have_filter_  = args != nullptr;
+    last_g_       = g;
 
     if (dbg_on) {
+        HWBRJ_CHECK(hipEventSynchronize(ev_[8]));
         std::vector<uint64_t> hp(PG * 8), hj(F * 8);
         HWBRJ_CHECK(hipMemcpy(hp.data(), dbgP.p, hp.size() * 8, hipMemcpyDeviceToHost));
         HWBRJ_CHECK(hipMemcpy(hj.data(), dbgJ.p, hj.size() * 8, hipMemcpyDeviceToHost));
@@ -467,14 +483,27 @@ int Engine::run(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
         fprintf(stderr, "[dbg] probe cyc/WG: top %.0f test %.0f b1 %.0f scan+b2 %.0f write %.0f b3+copy %.0f\n",
                 sp_[0], sp_[1], sp_[2], sp_[3], sp_[4], sp_[5]);
     }
+    return 0;
+}
+
+int Engine::wait(hwbrj_stats_t* st) {
+    HWBRJ_CHECK(hipSetDevice(device_));
+    if (!pending_) {
+        set_last_error("no join has been enqueued");
+        return 6;
+    }
+    HWBRJ_CHECK(hipEventSynchronize(ev_[8]));
+    const Geometry& g = last_g_;
+    const uint32_t  F = 1u << g.log2F, NSUB = 1u << g.log2NSUB;
+    const uint32_t  nseg = (g.mode == MODE_SLICE_BLOCK || g.mode == MODE_SLICE_BASIC) ? g.nseg : 1;
+    const uint64_t* d_result   = small.as<uint64_t>();      // (see enqueue)
+    const uint64_t* d_filtered = small.as<uint64_t>() + 2;
     uint64_t matches = 0, filtered = 0;
     HWBRJ_CHECK(hipMemcpy(&matches, d_result, 8, hipMemcpyDeviceToHost));
     HWBRJ_CHECK(hipMemcpy(&filtered, d_filtered, 8, hipMemcpyDeviceToHost));
-    have_filter_ = args != nullptr;
-    last_g_      = g;
     if (st) {
         memset(st, 0, sizeof(*st));
-        st->filtered       = args ? filtered : nS;
+        st->filtered       = pending_args_ ? filtered : pending_nS_;
         st->matches        = (int64_t) matches;
         st->mode           = g.mode;
         st->format         = g.format;

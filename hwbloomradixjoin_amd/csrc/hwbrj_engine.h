@@ -31,6 +31,10 @@ class Engine {
     // Synchronous join of device-resident tuples. Returns 0 on success.
     int  run(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
              const bloom_filter_args_t* args, hipStream_t stream, hwbrj_stats_t* st);
+    // Enqueue only (wait = false in run): wait() then waits for the last enqueued join.
+    int  run_async(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
+                   const bloom_filter_args_t* args, hipStream_t stream);
+    int  wait(hwbrj_stats_t* st);
     int  export_filter(uint8_t* host_out, uint64_t nbytes);
     // (R.payload, S.payload) of every match into out[0, cap); *n = number of pairs.
     int  materialize(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS, uint2* out,
@@ -48,6 +52,12 @@ class Engine {
     hipEvent_t   ev_[10];
     bool         have_filter_ = false;
     Geometry     last_g_{};
+    // the last enqueued join (collected by wait)
+    bool         pending_      = false;
+    bool         pending_args_ = false;
+    uint64_t     pending_nS_   = 0;
+    int          enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
+                         const bloom_filter_args_t* args, hipStream_t stream, bool dbg);
     CrcTables*   d_tabs_ = nullptr;
     GenPlan*     d_plan_ = nullptr;
     // R side

@@ -116,6 +116,12 @@ typedef struct hwbrj_stats_t {
  * stream: a hipStream_t (NULL = the library's own stream). The call is synchronous. */
 int hwbrj_join_device(const tuple_t * d_R, uint64_t nR, const tuple_t * d_S, uint64_t nS,
                       const bloom_filter_args_t * args, void * stream, hwbrj_stats_t * stats);
+/* The same join, enqueued on `stream` without waiting (back-to-back joins then run without host
+ * gaps); the inputs must stay valid until it completes. hwbrj_join_wait() waits for the last join
+ * enqueued on this device and fills stats (counts and phase times of that join). */
+int hwbrj_join_device_async(const tuple_t * d_R, uint64_t nR, const tuple_t * d_S, uint64_t nS,
+                            const bloom_filter_args_t * args, void * stream);
+int hwbrj_join_wait(hwbrj_stats_t * stats);
 
 /* The join with result materialization (the reference's JOIN_RESULT_MATERIALIZE output,
  * src/parallel_radix_join_bloom.c:307-312): d_out[i] = {R.payload, S.payload} of every match, in

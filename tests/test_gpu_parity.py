@@ -216,6 +216,18 @@ def test_repeatable_and_buffer_reuse(hw, cuda, f3):
     assert small.matches <= 5000
 
 
+def test_async_joins_back_to_back(hw, cuda, f3):
+    """hwbrj_join_device_async x3 then hwbrj_join_wait: the last join's counts are the golden's."""
+    g = GOLD["F3_grid"]
+    R, S = f3
+    args = hw.BloomFilterArgs(hw.BLOCKED, g["m"], 1, 1024)
+    for _ in range(3):
+        hw.join_device_async(R, S, args)
+    st = hw.join_wait()
+    assert (st.filtered, st.matches) == (g["rows"]["1024"][0], g["results"])
+    assert st.ms_total > 0
+
+
 def test_generate_device_matches_host(hw, cuda):
     for (n, nthr, maxid, thr, q) in [(1000000, 2, 1000000, 1000000, 1.0), (3000001, 3, INT_MAX, 100000, 0.01)]:
         d = dev_rel(hw, cuda, n, maxid, thr, q, 9, nthr).cpu().numpy()
