@@ -962,12 +962,12 @@ __global__ __launch_bounds__(1024) void k_build(BuildParams P) {
     uint32_t*       slice  = lds;
     uint32_t*       inv    = slice + segw;
     uint32_t*       stage  = inv + 128;       // kBSlot
-    uint32_t*       cnt    = stage + kBSlot;  // 64: ranks of this sweep by sub
-    uint32_t*       offs   = cnt + 64;        // 65: exclusive offsets (+ total)
+    uint32_t*       cnt    = stage + kBSlot;  // 2 x 64: ranks of a sweep by sub (by sweep parity)
     const uint32_t  q      = blockIdx.x;
-    const int       tid    = threadIdx.x, lane = tid & 63;
+    const int       tid    = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     load_tab(inv, &P.tabs->inv[0][0]);
-    if (tid < 64) cnt[tid] = 0;
+    if (tid < 128) cnt[tid] = 0;
+    uint32_t nsw = 0;  // sweeps sorted so far (selects the counter buffer)
     const uint32_t l0 = P.list_start[q], l1 = P.list_start[q + 1];
     const uint32_t sw0  = P.sweep_start[q];
     const uint32_t nseg = slices ? g.nseg : 1;
@@ -996,35 +996,54 @@ __global__ __launch_bounds__(1024) void k_build(BuildParams P) {
                 for (int t = 0; t < 4; t++) {
                     const bool     ok = (uint32_t) t < SA.n[jj];
                     const uint32_t w  = sweep_word(SA, jj, t);
+#ifndef HWBRJ_ABL_BNOBITS
                     if (slices && ok) {
                         const Loc L = locate<KIND>(w, g, inv, q);
                         if (L.seg == seg) apply_bits<KIND, true>(L, g, slice);
                     }
+#endif
                     c[t]  = decode_k<KIND>(w, q, g.log2F);
                     rk[t] = 0xFFFFFFFFu;
-                    if (last && ok) rk[t] = atomicAdd(&cnt[(c[t] >> g.sub_shift) & (NSUB - 1u)], 1u);
+#ifndef HWBRJ_ABL_BNOSORT
+                    if (last && ok) rk[t] = atomicAdd(&cnt[(nsw & 1u) * 64 + ((c[t] >> g.sub_shift) & (NSUB - 1u))], 1u);
+#else
+                    if (ok && c[t] == 0x12345678u) P.out_codes[0] = c[t];  // dev ablation: keep the loads live
+#endif
                 }
+#ifdef HWBRJ_ABL_BNOSORT
+                if (last && (uint32_t) tid < NSUB) {  // dev ablation (results invalid): empty runs
+                    const uint64_t r = (uint64_t) (sw0 + (sb - l0) / kBSweep) * NSUB + tid;
+                    P.run_cnt[r]     = 0;
+                    P.run_off[r]     = 0;
+                }
+                continue;
+#endif
                 if (!last) continue;
                 const uint32_t sw = sw0 + (sb - l0) / kBSweep;
-                __syncthreads();  // B1: every rank of the sweep taken
-                if (tid < 64) {   // wave 0: run offsets and the (sweep, sub) run table
-                    const uint32_t cs   = (uint32_t) lane < NSUB ? cnt[lane] : 0u;
-                    const uint32_t incl = wave_incl_scan_dpp(cs);
+                __syncthreads();  // B1: every rank of the sweep taken (and the last sweep copied out)
+                // every wave: run offsets of the sweep (DPP scan over the NSUB counters), so no
+                // second barrier; wave 0 writes the (sweep, sub) run table and clears the other
+                // counter buffer (last read before this B1, next used after B3)
+                uint32_t* cb = cnt + (nsw & 1u) * 64;
+                const uint32_t cs   = (uint32_t) lane < NSUB ? cb[lane] : 0u;
+                const uint32_t incl = wave_incl_scan_dpp(cs);
+                const uint32_t tot  = __builtin_amdgcn_readlane(incl, 63);
+                if (wave == 0) {
                     if ((uint32_t) lane < NSUB) {
-                        offs[lane] = incl - cs;
                         const uint64_t r = (uint64_t) sw * NSUB + lane;
                         P.run_cnt[r]     = cs;
                         P.run_off[r]     = incl - cs;
-                        cnt[lane]        = 0;
                     }
-                    if (lane == 63) offs[64] = incl;
+                    cnt[((nsw & 1u) ^ 1u) * 64 + lane] = 0;
                 }
-                __syncthreads();  // B2: offsets visible
 #pragma unroll
-                for (int t = 0; t < 4; t++)
-                    if (rk[t] != 0xFFFFFFFFu) stage[offs[(c[t] >> g.sub_shift) & (NSUB - 1u)] + rk[t]] = c[t];
+                for (int t = 0; t < 4; t++) {
+                    const uint32_t sub = (c[t] >> g.sub_shift) & (NSUB - 1u);
+                    const uint32_t o   = (uint32_t) __shfl((int) (incl - cs), (int) sub, 64) + rk[t];
+                    if (rk[t] != 0xFFFFFFFFu) stage[o] = c[t];
+                }
+                nsw++;
                 __syncthreads();  // B3: the sweep is sorted
-                const uint32_t tot = offs[64];
                 uint32_t* __restrict__ dst = P.out_codes + (uint64_t) sw * kBSlot;
                 for (uint32_t i = tid; i < tot; i += blockDim.x) dst[i] = stage[i];
             }
@@ -1165,24 +1184,24 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
         const uint32_t rend = min(it1, qi0 + (seg + 1) * npc);  // end of this (q, seg) run
         const uint32_t p1   = p0 + (rend - it);
         const uint32_t rit0 = it;  // item index of piece p0
-        if (slices) {
-            __syncthreads();  // every wave is done with the previous slice
-            const uint4* src = (const uint4*) (P.slices + ((uint64_t) q * nseg + seg) * segw);
-            uint4*       dst = (uint4*) slice;
-            for (uint32_t i = tid; i < segw / 4; i += NT) dst[i] = src[i];
-            __syncthreads();
-        }
         auto lb_of = [&](uint32_t p) { return lq0 + p * kProbeCH; };
         auto le_of = [&](uint32_t p) { return min(lq1, lq0 + (p + 1) * kProbeCH); };
         uint32_t   eA[kPC], eB[kPC], eC[kPC];
         Sweep<kPC> SA, SB, SC;
-        {
+        {  // the run's first loads are issued before the slice copy, so the two latencies overlap
             const uint32_t pa = min(p0 + 1, p1 - 1), pb = min(p0 + 2, p1 - 1);
             load_list_u<kPC>(P.list, lb_of(p0), le_of(p0), eA);
             load_list_u<kPC>(P.list, lb_of(pa), le_of(pa), eB);
             load_list_u<kPC>(P.list, lb_of(pb), le_of(pb), eC);
             load_chunks_u<kPC>(P.pool, eA, lb_of(p0), le_of(p0), SA);
             load_chunks_u<kPC>(P.pool, eB, lb_of(pa), le_of(pa), SB);
+        }
+        if (slices) {
+            __syncthreads();  // every wave is done with the previous slice
+            const uint4* src = (const uint4*) (P.slices + ((uint64_t) q * nseg + seg) * segw);
+            uint4*       dst = (uint4*) slice;
+            for (uint32_t i = tid; i < segw / 4; i += NT) dst[i] = src[i];
+            __syncthreads();
         }
         // Sc: words of piece p (registers); en: list entries of p+2 -> Sl; enn <- list of p+3.
         auto step = [&](uint32_t p, Sweep<kPC>& Sc, Sweep<kPC>& Sl, const uint32_t (&en)[kPC],
@@ -1917,7 +1936,7 @@ bool launch_plan(const uint32_t* wgq_chunks, const uint32_t* wgq_elems, uint32_t
 
 size_t slice_lds_bytes(const Geometry& g) {
     const bool slices = g.mode == MODE_SLICE_BLOCK || g.mode == MODE_SLICE_BASIC;
-    return ((slices ? g.seg_words : 0) + 128 + kBSlot + 64 + 65) * sizeof(uint32_t);
+    return ((slices ? g.seg_words : 0) + 128 + kBSlot + 128) * sizeof(uint32_t);
 }
 
 uint32_t build_chunks_per_sweep() { return kBSweep; }
