@@ -80,12 +80,20 @@ def main():
     import torch
     import hwbloomradixjoin_amd as hw
 
+    # HWBRJ_BENCH_SHARED_GPU=1 (rehearsal only): ranks share the visible GPUs round-robin, with
+    # gloo for the few host-side collectives, so the N > 1 path runs on a one-GPU box
+    shared = os.environ.get("HWBRJ_BENCH_SHARED_GPU") == "1"
+    if shared:
+        local = local % torch.cuda.device_count()
     torch.cuda.set_device(local)
     hw.lib().hwbrj_set_device(local)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if shared:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     nR, nS_total = a.r_size, a.s_size
     if a.scaling == "strong":
@@ -106,7 +114,8 @@ def main():
 
     # one untimed parity run (counts reduced over ranks)
     st = hw.join_device(dR, dS, args)
-    counts = torch.tensor([st.filtered, st.matches], dtype=torch.int64, device="cuda")
+    cdev = "cpu" if shared else "cuda"  # where the count / time reductions live
+    counts = torch.tensor([st.filtered, st.matches], dtype=torch.int64, device=cdev)
     if dist:
         dist.all_reduce(counts)
     filtered, matches = (int(x) for x in counts.tolist())
@@ -138,7 +147,7 @@ def main():
                   "ms_s_index", "ms_probe", "ms_surv", "ms_join"):
             sums[f] = sums.get(f, 0.0) + getattr(st, f)
     if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 

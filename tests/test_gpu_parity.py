@@ -320,6 +320,28 @@ def test_cli_end_to_end(hw):
     assert f"[INFO ] Results = {g['results']}. DONE." in out.stdout
 
 
+def test_bench_two_ranks(hw):
+    """bench.py's N > 1 path end to end (torch.distributed.run, 2 ranks, S sharded, counts
+    all-reduced), rehearsed on one GPU: HWBRJ_BENCH_SHARED_GPU=1 puts both ranks on it with gloo."""
+    import socket
+    g = GOLD["F3_grid"]
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    root = os.path.dirname(HERE)
+    env = dict(os.environ, HWBRJ_BENCH_SHARED_GPU="1")
+    out = subprocess.run(["python", "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                          "--master-addr", "127.0.0.1", "--master-port", str(port),
+                          os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+                          "-r", str(g["r"]), "-s", str(g["s"]), "-m", str(g["m"])],
+                         capture_output=True, text=True, timeout=300, env=env, cwd=root)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-2000:]
+    line = json.loads([x for x in out.stdout.splitlines() if x.startswith("{")][-1])
+    assert line["n_gpus"] == 2
+    assert (line["parity"]["filtered"], line["parity"]["matches"]) == (g["rows"]["1024"][0], g["results"])
+
+
 def _sorted_pairs(p):
     p = np.asarray(p).reshape(-1, 2)
     return p[np.lexsort((p[:, 1], p[:, 0]))]
