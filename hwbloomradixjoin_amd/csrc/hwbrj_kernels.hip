@@ -1389,6 +1389,10 @@ constexpr uint32_t kJoinLog2T   = 13;                  // hash path: 8192 slots 
 constexpr uint32_t kJoinT       = 1u << kJoinLog2T;
 constexpr uint32_t kJoinPiece   = kJoinT / 2;
 constexpr uint32_t kJoinDesc    = kJoinThreads;        // run descriptors per batch
+#ifndef HWBRJ_JTU
+#define HWBRJ_JTU 8
+#endif
+constexpr uint32_t kJoinTailU   = HWBRJ_JTU;           // loads in flight per lane in a long run
 constexpr uint32_t kEmpty       = 0xFFFFFFFFu;  // codes of one job share their low hash_shift >= 1
                                                 // bits, so (code >> hash_shift) never equals it
 
@@ -1479,6 +1483,21 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
     const uint32_t sh  = P.hash_shift;
     const int      tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     uint64_t       cnt = 0;
+    // The words [from, n) of one run (long runs: high-selectivity survivors, large R runs), with
+    // kJoinTailU loads in flight per lane instead of one dependent load per iteration.
+    auto tail_run = [&](const uint32_t* data, uint64_t bb, uint32_t from, uint32_t n, auto&& op) {
+        for (uint32_t o = from + lane; o < n; o += 64u * kJoinTailU) {
+            uint32_t v[kJoinTailU];
+#pragma unroll
+            for (int u = 0; u < (int) kJoinTailU; u++) {
+                const uint32_t oo = o + 64u * u;
+                v[u]              = oo < n ? data[bb + oo] : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < (int) kJoinTailU; u++)
+                if (o + 64u * u < n) op(v[u] >> sh);
+        }
+    };
     // Every word of runs [da, db) of a descriptor batch through op(word): a wave per run, RUNS runs
     // in flight per wave with WPL words per lane each; longer runs finish in a tail loop.
     auto walk = [&](auto runs_c, auto wpl_c, const uint32_t* data, const uint32_t* nc,
@@ -1504,7 +1523,7 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
                     if (lane + 64u * j < n[r]) op(v[r][j] >> sh);
                 if (n[r] > 64u * WPL) {
                     const uint64_t bb = nb[d + r * kJoinWaves];
-                    for (uint32_t o = 64u * WPL + lane; o < n[r]; o += 64) op(data[bb + o] >> sh);
+                    tail_run(data, bb, 64u * WPL, n[r], op);
                 }
             }
         }
@@ -1626,7 +1645,7 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
                 if (lane + 64u * j < rn[r]) set(rv[r][j] >> sh);
             if (rn[r] > 64u * FW) {  // (rare) longer run
                 const uint64_t bb = rbase[wave + r * kJoinWaves];
-                for (uint32_t o = 64u * FW + lane; o < rn[r]; o += 64) set(P.r_codes[bb + o] >> sh);
+                tail_run(P.r_codes, bb, 64u * FW, rn[r], set);
             }
         }
         if (dup) dupflag = 1;
@@ -1641,7 +1660,7 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
                     if (lane + 64u * j < sn[r]) test(sv[r][j] >> sh);
                 if (sn[r] > 64u * FSW) {
                     const uint64_t bb = dbase[wave + r * kJoinWaves];
-                    for (uint32_t o = 64u * FSW + lane; o < sn[r]; o += 64) test(P.surv[bb + o] >> sh);
+                    tail_run(P.surv, bb, 64u * FSW, sn[r], test);
                 }
             }
 #ifndef HWBRJ_ABL_JNOS
