@@ -1115,8 +1115,9 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
     uint32_t*       subow  = subc + 3 * 128;  // 16 waves x NSUB: each wave's copy of the offsets
     constexpr uint32_t kScrCap = scr_cap<KIND>();
     constexpr int      kDense  = kScrCap / 64;
-    uint32_t*       scratch = subow + 16 * NSUB;  // 16 waves x (kScrCap + 64): compacted survivors
-    uint32_t*       stage  = scratch + 16 * (kScrCap + 64);  // 2 x sstr, double-buffered by item
+    uint32_t*       scratch = subow + 16 * NSUB;  // 16 waves x kScrCap: compacted survivors
+    uint32_t*       scrdum = scratch + 16 * kScrCap;  // 64 dummy slots shared by all waves
+    uint32_t*       stage  = scrdum + 64;             // 2 x sstr, double-buffered by item
     const int       tid    = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     load_tab(inv, &P.tabs->inv[0][0]);
     for (uint32_t i = tid; i < 3 * 128; i += NT) subc[i] = 0;
@@ -1213,7 +1214,7 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
             load_list_u<kPC>(P.list, lb_of(p3), le_of(p3), enn);
             stamp(0);
             uint32_t* cnt = subc + cb3 * 128;
-            uint32_t* scr = scratch + wave * (kScrCap + 64);
+            uint32_t* scr = scratch + wave * kScrCap;
             // ---- test. One-bit kinds: all slice reads first, then per word slot the pass bit, its
             // wave ballot and the compaction of the wave's survivors into its scratch (no exec
             // masking: non-survivors write a per-lane dummy slot).
@@ -1242,7 +1243,7 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
                     const uint32_t pre = __builtin_amdgcn_mbcnt_hi((uint32_t) (m >> 32),
                                                                    __builtin_amdgcn_mbcnt_lo((uint32_t) m, 0u));
                     const uint32_t at  = nsv + pre;
-                    scr[ok && at < kScrCap ? at : kScrCap + lane] = w;
+                    *(ok && at < kScrCap ? &scr[at] : &scrdum[lane]) = w;  // non-survivors: garbage slot
                     nsv += (uint32_t) __builtin_popcountll(m);
                 }
             } else {
@@ -2001,7 +2002,7 @@ size_t probe_lds_bytes(const Geometry& g, uint32_t* stage_cap) {
     const bool   slices = g.mode == MODE_SLICE_BLOCK || g.mode == MODE_SLICE_BASIC;
     const size_t NSUB   = (size_t) 1 << g.log2NSUB;
     const size_t scap   = consumer_kind(g) == KIND_BLOCK_PKK ? scr_cap<KIND_BLOCK_PKK>() : scr_cap<KIND_PASS>();
-    const size_t base   = ((slices ? g.seg_words : 0) + 128 + 3 * 128 + 16 * NSUB + 16 * (scap + 64)) * sizeof(uint32_t);
+    const size_t base   = ((slices ? g.seg_words : 0) + 128 + 3 * 128 + 16 * NSUB + 16 * scap + 64) * sizeof(uint32_t);
     // 2 buffers of cap words + 64 dummy slots each
     size_t cap = std::min<size_t>(kProbeCH * 32, (163840 - base) / 8 - 64) & ~(size_t) 3;
     if (stage_cap) *stage_cap = (uint32_t) cap;
