@@ -76,8 +76,9 @@ HWBRJ_HD uint32_t mix32(uint32_t x) {
 enum Mode : int {
     MODE_NOBLOOM      = 0,  // PRO: no filter
     MODE_SLICE_BLOCK  = 1,  // blocked/sectorized: S partitioned by block bits, probed from LDS slices
-    MODE_SLICE_BASIC  = 2,  // basic, k = 1: partitioned by crapwow bit-index bits, LDS slices
-    MODE_GLOBAL       = 3,  // basic k > 1 or B < 8: global atomics build + direct probe (fallback)
+    MODE_SLICE_BASIC  = 2,  // basic: partitioned by the first bit's index bits, LDS slices (k >= 2:
+                            // bits 2..k of the first-bit candidates from the global bitmap)
+    MODE_GLOBAL       = 3,  // basic k = 0 or B < 8: global atomics build + direct probe (fallback)
 };
 
 enum Format : int {
@@ -118,6 +119,8 @@ enum Kind : int {
     KIND_BASIC_K1    = 3,  // basic, k = 1
     KIND_BLOCK_PKK   = 4,  // blocked/sectorized, k >= 2, packed words: the first bit is tested from
                            // the word, the key (for the rest) is recovered only for those that pass
+    KIND_BASIC_KK    = 5,  // basic, k >= 2: the first bit from the LDS slice, bits 2..k of the
+                           // candidates from the global bitmap (slices = its transpose)
 };
 
 constexpr uint32_t kMaxLog2F     = 10;

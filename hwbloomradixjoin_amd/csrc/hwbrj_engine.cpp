@@ -156,7 +156,7 @@ bool plan_geometry(const bloom_filter_args_t* a, uint64_t nR, Geometry* g, std::
         }
         uint64_t F = 0;
         if (a->variant == BASIC) {
-            if (k == 1 && m >= 32) {
+            if (k >= 1 && m >= 32) {  // k >= 2: KIND_BASIC_KK (first bit sliced, the rest global)
                 g->mode = MODE_SLICE_BASIC;
                 F       = std::min<uint64_t>(1024, m / 32);
             } else {
@@ -314,7 +314,9 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     const bool jnew = jparts.bytes < (size_t) (2 * NJ + 1) * 4;
     ok &= jtask.ensure((size_t) join_extra_tasks() * 8) && jparts.ensure((size_t) (2 * NJ + 1) * 4);
     if (slice_mode) ok &= slices.ensure((uint64_t) F * nseg * g.seg_words * 4);
+    const bool basic_kk = g.mode == MODE_SLICE_BASIC && g.k > 1;  // global bitmap + sliced first bit
     if (g.mode == MODE_GLOBAL) ok &= bitmap.ensure(((g.m + 31) / 32) * 4) && dense.ensure(nS * 4);
+    if (basic_kk) ok &= bitmap.ensure(((g.m + 31) / 32) * 4);
     if (!ok) {
         set_last_error("hipMalloc failed (device memory)");
         return 4;
@@ -328,7 +330,7 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     HWBRJ_CHECK(hipMemsetAsync(small.p, 0, 64, stream));
     if (jnew) HWBRJ_CHECK(hipMemsetAsync(jparts.p, 0, jparts.bytes, stream));
     HWBRJ_CHECK(hipMemsetAsync(jparts.as<uint32_t>() + 2 * NJ, 0, 4, stream));
-    if (g.mode == MODE_GLOBAL) HWBRJ_CHECK(hipMemsetAsync(bitmap.p, 0, bitmap.bytes, stream));
+    if (g.mode == MODE_GLOBAL || basic_kk) HWBRJ_CHECK(hipMemsetAsync(bitmap.p, 0, bitmap.bytes, stream));
 
     ScatterParams sp{};
     sp.tabs = d_tabs_;
@@ -336,7 +338,7 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
 
     HWBRJ_CHECK(hipEventRecord(ev_[0], stream));
     // ---------------------------------------------------------------- R: pass-1 (+ filter)
-    if (g.mode == MODE_GLOBAL)
+    if (g.mode == MODE_GLOBAL || basic_kk)
         launch_build_global(dR, nR, g, d_tabs_, bitmap.as<uint32_t>(), stream);
     sp.src        = dR;
     sp.n          = nR;
@@ -368,6 +370,7 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     bp.run_cnt     = rrun.as<uint32_t>();
     bp.run_off     = rrun.as<uint32_t>() + sweeps_max * NSUB;
     launch_build(bp, F, stream);
+    if (basic_kk) launch_slices_from_bitmap(bitmap.as<uint32_t>(), g, slices.as<uint32_t>(), stream);
     HWBRJ_CHECK(hipEventRecord(ev_[3], stream));
     // ---------------------------------------------------------------- S: pass-1 (+ probe)
     if (g.mode == MODE_GLOBAL) {
@@ -410,6 +413,7 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     pp.list_start      = lstartS.as<uint32_t>();
     pp.item_start      = istartS.as<uint32_t>();
     pp.slices          = slice_mode ? slices.as<uint32_t>() : nullptr;
+    pp.bm              = basic_kk ? bitmap.as<uint32_t>() : nullptr;
     pp.surv            = surv.as<uint32_t>();
     pp.surv_seg_stride = LS * 32;
     pp.surv_cnt        = survcnt.as<uint32_t>();

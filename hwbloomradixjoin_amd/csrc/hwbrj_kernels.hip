@@ -82,9 +82,9 @@ __device__ __forceinline__ uint32_t decode_k(uint32_t w, uint32_t q, uint32_t lo
 template <int KIND>
 __device__ __forceinline__ Loc locate(uint32_t w, const Geometry& g, const uint32_t* inv, uint32_t q) {
     Loc L;
-    if (KIND == KIND_BASIC_K1) {
+    if (KIND == KIND_BASIC_K1 || KIND == KIND_BASIC_KK) {
         const uint32_t key = code_key(inv, w);
-        const uint32_t b   = mod_m(crapwow(kSeed, key), (uint32_t) g.m);  // add_basic, k = 1
+        const uint32_t b   = mod_m(crapwow(kSeed, key), (uint32_t) g.m);  // add_basic, first bit
         const uint32_t lb  = b >> g.log2F;
         L.seg  = lb >> g.log2seg;
         L.base = lb & (g.seg_bits - 1u);
@@ -111,7 +111,7 @@ __device__ __forceinline__ Loc locate(uint32_t w, const Geometry& g, const uint3
 // SET: add the key's bits (ds_or); otherwise test them (src/bloom_filter.c:73-111 per variant).
 template <int KIND, bool SET>
 __device__ __forceinline__ bool apply_bits(const Loc& L, const Geometry& g, uint32_t* slice) {
-    if (KIND == KIND_BASIC_K1 || KIND == KIND_BLOCK_PK1) {
+    if (KIND == KIND_BASIC_K1 || KIND == KIND_BASIC_KK || KIND == KIND_BLOCK_PK1) {
         const uint32_t b = L.base + L.h;
         if (SET) {
             atomicOr(slice + (b >> 5), 1u << (b & 31u));
@@ -143,6 +143,22 @@ template <int KIND>
 __device__ __forceinline__ uint32_t decode_k(uint32_t w, uint32_t q, uint32_t log2F) {
     if (KIND == KIND_BLOCK_PK1 || KIND == KIND_BLOCK_PKK) return (w << log2F) | q;  // drops the h bits
     return w;
+}
+
+// KIND_BASIC_KK: bits 2..k of add_basic (src/bloom_filter.c:73-111, the double-hashing sequence of
+// global_contains below) read from the global bitmap; bit 1 was tested from the LDS slice.
+__device__ __forceinline__ bool basic_rest(uint32_t code, const Geometry& g, const uint32_t* inv,
+                                           const uint32_t* __restrict__ bm) {
+    const uint32_t key = code_key(inv, code), msz = (uint32_t) g.m;
+    uint32_t       h = mod_m(crapwow(kSeed, key), msz), y = mod_m(key + kSeed, msz);
+    h = mod_m(h + y, msz);
+    y = mod_m(y + 1u, msz);
+    for (uint32_t i = 1; i < g.k; i++) {
+        if (!((bm[h >> 5] >> (h & 31u)) & 1u)) return false;
+        h = mod_m(h + y, msz);
+        y = mod_m(y + i + 1u, msz);
+    }
+    return true;
 }
 
 // ========================================================================= K0: generator
@@ -1080,7 +1096,9 @@ constexpr int      kPC      = HWBRJ_PC;       // chunk quads per thread per item
 constexpr uint32_t kProbeCH = 128u * kPC;     // chunks per probe item (1024 threads, 8 per chunk)
 // compacted survivors (first-bit candidates for KIND_BLOCK_PKK, whose rate is higher) per wave
 // and item in the LDS scratch, and the dense ranking rounds per wave
-template <int KIND> constexpr uint32_t scr_cap() { return KIND == KIND_BLOCK_PKK ? 256u : (uint32_t) HWBRJ_SCR1; }
+template <int KIND> constexpr uint32_t scr_cap() {
+    return KIND == KIND_BLOCK_PKK || KIND == KIND_BASIC_KK ? 256u : (uint32_t) HWBRJ_SCR1;
+}
 
 __device__ __forceinline__ uint32_t find_q(const uint32_t* item_start, uint32_t F, uint32_t it) {
     uint32_t lo = 0, hi = F - 1;
@@ -1103,8 +1121,10 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
     const uint32_t  F      = 1u << g.log2F;
     const uint32_t  NSUB   = 1u << g.log2NSUB;
     constexpr bool  slices = KIND != KIND_PASS;
-    constexpr bool  onebit = KIND == KIND_BLOCK_PK1 || KIND == KIND_BASIC_K1 || KIND == KIND_BLOCK_PKK;
-    constexpr bool  refine = KIND == KIND_BLOCK_PKK;  // onebit tests only the first bit: test the rest
+    constexpr bool  onebit = KIND == KIND_BLOCK_PK1 || KIND == KIND_BASIC_K1 || KIND == KIND_BLOCK_PKK ||
+                             KIND == KIND_BASIC_KK;
+    // onebit tests only the first bit: test the rest (basic: from the global bitmap)
+    constexpr bool  refine = KIND == KIND_BLOCK_PKK || KIND == KIND_BASIC_KK;
     constexpr int   NW     = kPC * 4;   // words per thread per item
     const uint32_t  segw   = slices ? g.seg_words : 0;  // multiple of 4
     const uint32_t  scap   = P.stage_cap;               // survivor words per stage buffer
@@ -1266,6 +1286,19 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
             uint32_t   dr[kDense];
             uint32_t   rank2[NW / 2];            // word by word: two 16-bit ranks per register
             if (dense) {
+                // KIND_BASIC_KK: the second bit of every slot's candidate is loaded from the global
+                // bitmap before any is tested (kDense loads in flight instead of one at a time)
+                uint32_t b2w[KIND == KIND_BASIC_KK ? kDense : 1], b2h[KIND == KIND_BASIC_KK ? kDense : 1];
+                if (KIND == KIND_BASIC_KK) {
+                    const uint32_t msz = (uint32_t) g.m;
+#pragma unroll
+                    for (int k = 0; k < kDense; k++) {
+                        const uint32_t j   = lane + 64u * k;
+                        const uint32_t key = code_key(inv, scr[j]);
+                        b2h[k] = mod_m(mod_m(crapwow(kSeed, key), msz) + mod_m(key + kSeed, msz), msz);
+                        b2w[k] = P.bm[j < nsv ? b2h[k] >> 5 : 0u];
+                    }
+                }
 #pragma unroll
                 for (int k = 0; k < kDense; k++) {
                     const uint32_t j  = lane + 64u * k;
@@ -1273,17 +1306,22 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
                     const uint32_t c  = decode_k<KIND>(w, q, g.log2F);
                     const uint32_t s  = (c >> g.sub_shift) & (NSUB - 1u);
                     bool           ok = j < nsv;
-                    if (refine) ok = ok && apply_bits<KIND, false>(locate<KIND>(w, g, inv, q), g, slice);
+                    if (KIND == KIND_BASIC_KK)
+                        ok = ok && ((b2w[k] >> (b2h[k] & 31u)) & 1u) && (g.k == 2 || basic_rest(w, g, inv, P.bm));
+                    else if (refine) ok = ok && apply_bits<KIND, false>(locate<KIND>(w, g, inv, q), g, slice);
                     const uint32_t r = atomicAdd(&cnt[ok ? s : 64u + lane], 1u);  // dummies: 64..127
                     dr[k]            = ok ? (s | (r << 16)) : kNoRank;
                 }
             } else {
                 if (refine) {  // too many first-bit candidates: the full test of every word
+                    const uint32_t pass1 = pass;
                     pass = 0;
 #pragma unroll
                     for (int i = 0; i < NW; i++) {
                         bool ok = (uint32_t) (i & 3) < Sc.n[i >> 2];
-                        if (ok) {
+                        if (KIND == KIND_BASIC_KK) {
+                            ok = ok && ((pass1 >> i) & 1u) && basic_rest(sweep_word(Sc, i >> 2, i & 3), g, inv, P.bm);
+                        } else if (ok) {
                             const Loc L = locate<KIND>(sweep_word(Sc, i >> 2, i & 3), g, inv, q);
                             ok          = (SEG1 || L.seg == seg) && apply_bits<KIND, false>(L, g, slice);
                         }
@@ -1761,6 +1799,33 @@ __global__ void k_export(const uint32_t* slices, Geometry g, uint32_t* out, uint
     }
 }
 
+// ===================================== K11b: basic k >= 2, partition slices from the global bitmap
+// Slice q bit lb = filter bit (lb << log2F) | q (k_export's inverse). The slices built by k_build
+// hold only the R keys' first bits; the reference tests bit 1 against every bit of the filter, so
+// the slices are replaced by this transpose of the global bitmap. q runs fastest, so a wave's 32
+// loads per output word touch two bitmap words each.
+__global__ void k_slices_from_bitmap(const uint32_t* __restrict__ bm, Geometry g,
+                                     uint32_t* __restrict__ slices) {
+    const uint32_t F1     = (1u << g.log2F) - 1u;
+    const uint64_t n      = (uint64_t) (F1 + 1u) * (g.slice_bits / 32u);
+    const uint64_t stride = (uint64_t) gridDim.x * blockDim.x;
+    for (uint64_t o = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x; o < n; o += stride) {
+        const uint32_t q = (uint32_t) o & F1, lb0 = (uint32_t) (o >> g.log2F) * 32u;
+        uint32_t       r = 0;
+#pragma unroll 8
+        for (uint32_t t = 0; t < 32; t++) {
+            const uint64_t gb = ((uint64_t) (lb0 + t) << g.log2F) | q;
+            r |= ((bm[gb >> 5] >> (uint32_t) (gb & 31u)) & 1u) << t;
+        }
+        const uint32_t seg = lb0 >> g.log2seg, off = lb0 & (g.seg_bits - 1u);
+        slices[((uint64_t) q * g.nseg + seg) * g.seg_words + (off >> 5)] = r;
+    }
+}
+
+void launch_slices_from_bitmap(const uint32_t* bm, const Geometry& g, uint32_t* slices, hipStream_t st) {
+    k_slices_from_bitmap<<<4096, 256, 0, st>>>(bm, g, slices);
+}
+
 // ================================================================ K12: result materialization
 // (R.payload, S.payload) pairs of every match, the reference's JOIN_RESULT_MATERIALIZE output
 // (src/parallel_radix_join_bloom.c:307-312: key = R rid, payload = S rid). A separate pass after
@@ -1799,9 +1864,15 @@ __device__ __forceinline__ bool mat_filter(uint32_t key, const Geometry& g, cons
         const uint32_t  o = sb & (g.seg_bits - 1u);
         return (w[o >> 5] >> (o & 31u)) & 1u;
     };
-    if (g.mode == MODE_SLICE_BASIC) {  // k = 1
-        const uint32_t b = mod_m(crapwow(kSeed, key), (uint32_t) g.m);
-        return bit(b & F1, b >> g.log2F);
+    if (g.mode == MODE_SLICE_BASIC) {  // bit b lives in slice b & F1 at b >> log2F
+        const uint32_t msz = (uint32_t) g.m;
+        uint32_t       h = mod_m(crapwow(kSeed, key), msz), y = mod_m(key + kSeed, msz);
+        for (uint32_t i = 0; i < g.k; i++) {
+            if (!bit(h & F1, h >> g.log2F)) return false;
+            h = mod_m(h + y, msz);
+            y = mod_m(y + i + 1u, msz);
+        }
+        return true;
     }
     const uint32_t q    = code & F1;
     const uint32_t base = ((code >> g.log2F) & g.lbmask) << g.log2B;
@@ -1963,7 +2034,7 @@ uint32_t build_chunks_per_sweep() { return kBSweep; }
 uint32_t build_sweep_slot() { return kBSlot; }
 
 int consumer_kind(const Geometry& g) {
-    if (g.mode == MODE_SLICE_BASIC) return KIND_BASIC_K1;
+    if (g.mode == MODE_SLICE_BASIC) return g.k == 1 ? KIND_BASIC_K1 : KIND_BASIC_KK;
     if (g.mode == MODE_SLICE_BLOCK)
         return g.format == FMT_PACKED ? (g.k == 1 ? KIND_BLOCK_PK1 : KIND_BLOCK_PKK) : KIND_BLOCK;
     return KIND_PASS;
@@ -1992,7 +2063,8 @@ void launch_build(const BuildParams& p, uint32_t F, hipStream_t st) {
         case KIND_BLOCK_PK1: return build_inst<KIND_BLOCK_PK1>(p, F, lds, st);
         case KIND_BLOCK_PKK: return build_inst<KIND_BLOCK_PKK>(p, F, lds, st);
         case KIND_BLOCK: return build_inst<KIND_BLOCK>(p, F, lds, st);
-        case KIND_BASIC_K1: return build_inst<KIND_BASIC_K1>(p, F, lds, st);
+        case KIND_BASIC_K1:
+        case KIND_BASIC_KK: return build_inst<KIND_BASIC_K1>(p, F, lds, st);  // (KK: first bits only)
         default: return build_inst<KIND_PASS>(p, F, lds, st);
     }
 }
@@ -2001,7 +2073,8 @@ void launch_build(const BuildParams& p, uint32_t F, hipStream_t st) {
 size_t probe_lds_bytes(const Geometry& g, uint32_t* stage_cap) {
     const bool   slices = g.mode == MODE_SLICE_BLOCK || g.mode == MODE_SLICE_BASIC;
     const size_t NSUB   = (size_t) 1 << g.log2NSUB;
-    const size_t scap   = consumer_kind(g) == KIND_BLOCK_PKK ? scr_cap<KIND_BLOCK_PKK>() : scr_cap<KIND_PASS>();
+    const int    kind   = consumer_kind(g);
+    const size_t scap   = kind == KIND_BLOCK_PKK || kind == KIND_BASIC_KK ? scr_cap<KIND_BLOCK_PKK>() : scr_cap<KIND_PASS>();
     const size_t base   = ((slices ? g.seg_words : 0) + 128 + 3 * 128 + 16 * NSUB + 16 * scap + 64) * sizeof(uint32_t);
     // 2 buffers of cap words + 64 dummy slots each
     size_t cap = std::min<size_t>(kProbeCH * 32, (163840 - base) / 8 - 64) & ~(size_t) 3;
@@ -2017,6 +2090,7 @@ void launch_probe(const ProbeParams& p0, uint32_t grid, hipStream_t st) {
         case KIND_BLOCK_PKK: return probe_inst<KIND_BLOCK_PKK>(p, grid, lds, st);
         case KIND_BLOCK: return probe_inst<KIND_BLOCK>(p, grid, lds, st);
         case KIND_BASIC_K1: return probe_inst<KIND_BASIC_K1>(p, grid, lds, st);
+        case KIND_BASIC_KK: return probe_inst<KIND_BASIC_KK>(p, grid, lds, st);
         default: return probe_inst<KIND_PASS>(p, grid, lds, st);
     }
 }
