@@ -156,7 +156,9 @@ bool plan_geometry(const bloom_filter_args_t* a, uint64_t nR, Geometry* g, std::
         }
         uint64_t F = 0;
         if (a->variant == BASIC) {
-            if (k >= 1 && m >= 32) {  // k >= 2: KIND_BASIC_KK (first bit sliced, the rest global)
+            // k >= 2: KIND_BASIC_KK, whose slice build partitions k * |R| bit positions (bounded by
+            // the scatter's chunk ids; beyond that the global fallback)
+            if (k >= 1 && m >= 32 && k * nR <= (1ull << 31)) {
                 g->mode = MODE_SLICE_BASIC;
                 F       = std::min<uint64_t>(1024, m / 32);
             } else {
@@ -246,7 +248,7 @@ void Engine::release() {
     for (DevBuf* b : {&poolR, &metaR, &usedR, &wgqcR, &wgqeR, &wgqoR, &lstartR, &estartR, &istartR,
                       &listR, &poolS, &metaS, &usedS, &wgqcS, &wgqeS, &wgqoS, &lstartS, &estartS,
                       &istartS, &listS, &slices, &bitmap, &rjoin, &rrun, &surv, &survcnt, &survoff,
-                      &dense, &small, &colR, &colS, &mtab, &mcount, &jtask, &jparts})
+                      &dense, &small, &bpos, &colR, &colS, &mtab, &mcount, &jtask, &jparts})
         b->release();
     have_filter_ = false;
 }
@@ -284,7 +286,10 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     const uint32_t CH         = probe_chunks_per_item();  // chunks per probe item
     const size_t   sc_lds     = scatter_lds_bytes(g.log2F);
     const uint32_t G          = (uint32_t) cus_ * (uint32_t) std::max<size_t>(1, std::min<size_t>(2, 163840 / sc_lds));
-    const uint64_t capR = region_cap(nR, G, F), capS = region_cap(nS, G, F);
+    // basic k >= 2: the S-side buffers first partition the R keys' k * |R| bit positions
+    const bool     basic_kk = g.mode == MODE_SLICE_BASIC && g.k > 1;
+    const uint64_t nRk      = basic_kk ? (uint64_t) g.k * nR : 0;
+    const uint64_t capR = region_cap(nR, G, F), capS = region_cap(std::max(nS, nRk), G, F);
     const uint64_t LR = (uint64_t) G * capR, LS = (uint64_t) G * capS;  // max chunks
     const uint64_t items_max = (LS / CH + F + 1) * nseg;
     // list entries hold a 27-bit chunk id (hwbrj_kernels.hip, K4); metas a 22-bit region offset
@@ -314,9 +319,8 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     const bool jnew = jparts.bytes < (size_t) (2 * NJ + 1) * 4;
     ok &= jtask.ensure((size_t) join_extra_tasks() * 8) && jparts.ensure((size_t) (2 * NJ + 1) * 4);
     if (slice_mode) ok &= slices.ensure((uint64_t) F * nseg * g.seg_words * 4);
-    const bool basic_kk = g.mode == MODE_SLICE_BASIC && g.k > 1;  // global bitmap + sliced first bit
     if (g.mode == MODE_GLOBAL) ok &= bitmap.ensure(((g.m + 31) / 32) * 4) && dense.ensure(nS * 4);
-    if (basic_kk) ok &= bitmap.ensure(((g.m + 31) / 32) * 4);
+    if (basic_kk) ok &= bpos.ensure(nRk * 4);
     if (!ok) {
         set_last_error("hipMalloc failed (device memory)");
         return 4;
@@ -330,7 +334,7 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     HWBRJ_CHECK(hipMemsetAsync(small.p, 0, 64, stream));
     if (jnew) HWBRJ_CHECK(hipMemsetAsync(jparts.p, 0, jparts.bytes, stream));
     HWBRJ_CHECK(hipMemsetAsync(jparts.as<uint32_t>() + 2 * NJ, 0, 4, stream));
-    if (g.mode == MODE_GLOBAL || basic_kk) HWBRJ_CHECK(hipMemsetAsync(bitmap.p, 0, bitmap.bytes, stream));
+    if (g.mode == MODE_GLOBAL) HWBRJ_CHECK(hipMemsetAsync(bitmap.p, 0, bitmap.bytes, stream));
 
     ScatterParams sp{};
     sp.tabs = d_tabs_;
@@ -338,7 +342,7 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
 
     HWBRJ_CHECK(hipEventRecord(ev_[0], stream));
     // ---------------------------------------------------------------- R: pass-1 (+ filter)
-    if (g.mode == MODE_GLOBAL || basic_kk)
+    if (g.mode == MODE_GLOBAL)
         launch_build_global(dR, nR, g, d_tabs_, bitmap.as<uint32_t>(), stream);
     sp.src        = dR;
     sp.n          = nR;
@@ -370,7 +374,29 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     bp.run_cnt     = rrun.as<uint32_t>();
     bp.run_off     = rrun.as<uint32_t>() + sweeps_max * NSUB;
     launch_build(bp, F, stream);
-    if (basic_kk) launch_slices_from_bitmap(bitmap.as<uint32_t>(), g, slices.as<uint32_t>(), stream);
+    if (basic_kk) {
+        // basic k >= 2: the k bit positions of every R key, partitioned by slice with the S-side
+        // scatter buffers (free until the S pass), then one LDS slice build per partition
+        launch_bitpos(dR, nR, g, bpos.as<uint32_t>(), stream);
+        sp.src        = bpos.p;
+        sp.n          = nRk;
+        sp.n_dev      = nullptr;
+        sp.pool       = poolS.as<uint32_t>();
+        sp.meta       = metaS.as<uint32_t>();
+        sp.wg_used    = usedS.as<uint32_t>();
+        sp.wgq_chunks = wgqcS.as<uint32_t>();
+        sp.wgq_elems  = wgqeS.as<uint32_t>();
+        sp.cap        = capS;
+        launch_scatter(sp, SRC_CODES, SIDE_R, G, stream);
+        launch_plan(wgqcS.as<uint32_t>(), wgqeS.as<uint32_t>(), G, g.log2F, wgqoS.as<uint32_t>(),
+                    colS.as<uint32_t>() + 2 * F, colS.as<uint64_t>(), stream);
+        launch_list_fill(metaS.as<uint32_t>(), usedS.as<uint32_t>(), capS, g.log2F, wgqoS.as<uint32_t>(),
+                         colS.as<uint32_t>() + 2 * F, colS.as<uint64_t>(), (uint32_t) BSW, 1,
+                         lstartS.as<uint32_t>(), estartS.as<uint64_t>(), istartS.as<uint32_t>(),
+                         listS.as<uint32_t>(), G, stream);
+        launch_slice_fill(poolS.as<uint32_t>(), listS.as<uint32_t>(), lstartS.as<uint32_t>(), g,
+                          slices.as<uint32_t>(), stream);
+    }
     HWBRJ_CHECK(hipEventRecord(ev_[3], stream));
     // ---------------------------------------------------------------- S: pass-1 (+ probe)
     if (g.mode == MODE_GLOBAL) {
@@ -413,7 +439,6 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     pp.list_start      = lstartS.as<uint32_t>();
     pp.item_start      = istartS.as<uint32_t>();
     pp.slices          = slice_mode ? slices.as<uint32_t>() : nullptr;
-    pp.bm              = basic_kk ? bitmap.as<uint32_t>() : nullptr;
     pp.surv            = surv.as<uint32_t>();
     pp.surv_seg_stride = LS * 32;
     pp.surv_cnt        = survcnt.as<uint32_t>();

@@ -65,6 +65,7 @@ class Engine {
     // S side
     DevBuf poolS, metaS, usedS, wgqcS, wgqeS, wgqoS, lstartS, estartS, istartS, listS;
     DevBuf slices, bitmap, rjoin, rrun, surv, survcnt, survoff, dense, small, dbgP, dbgJ, dbgS;
+    DevBuf bpos;        // basic k >= 2: R bit positions (k_bitpos)
     DevBuf colR, colS;  // per-partition totals from k_plan: u64 elements [F], then u32 chunks [F]
     DevBuf mtab, mcount;  // materialization: R table, pair counter
     DevBuf jtask, jparts;  // join task table; parts per job (+ the task count)

@@ -49,7 +49,6 @@ struct ProbeParams {
     const uint32_t*  list_start;  // [F + 1]
     const uint32_t*  item_start;  // [F + 1]
     const uint32_t*  slices;
-    const uint32_t*  bm;          // KIND_BASIC_KK: the global bitmap (bits 2..k), else nullptr
     uint32_t*        surv;        // item region at (seg * surv_seg_stride + list_pos * 32), by sub
     uint64_t         surv_seg_stride;
     uint32_t*        surv_cnt;    // [items][NSUB] survivors of each (item, sub) run
@@ -93,8 +92,11 @@ void   launch_build_global(const uint2* R, uint64_t n, const Geometry& g, const 
                            uint32_t* bm, hipStream_t st);
 void   launch_probe_global(const uint2* S, uint64_t n, const Geometry& g, const CrcTables* tabs,
                            const uint32_t* bm, uint32_t* out, uint64_t* out_count, hipStream_t st);
-// basic k >= 2: overwrite the partition slices with the transpose of the global bitmap
-void   launch_slices_from_bitmap(const uint32_t* bm, const Geometry& g, uint32_t* slices, hipStream_t st);
+// basic k >= 2: every R key's k bit positions (element j * n + i), then the slices from their
+// partitioned chunk lists
+void   launch_bitpos(const uint2* R, uint64_t n, const Geometry& g, uint32_t* out, hipStream_t st);
+void   launch_slice_fill(const uint32_t* pool, const uint32_t* list, const uint32_t* list_start,
+                         const Geometry& g, uint32_t* slices, hipStream_t st);
 size_t scatter_lds_bytes(uint32_t log2F);
 enum { SIDE_R = 0, SIDE_S = 1 };  // which relation a scatter partitions (kernel name only)
 void   launch_scatter(const ScatterParams& p, int src, int side, uint32_t grid, hipStream_t st);

@@ -145,16 +145,24 @@ __device__ __forceinline__ uint32_t decode_k(uint32_t w, uint32_t q, uint32_t lo
     return w;
 }
 
+// Basic filter bit b in the partition-slice layout (MODE_SLICE_BASIC): slice q = b & (F-1) holds
+// it at lb = b >> log2F. Returns the word; the bit inside it is lb & 31.
+__device__ __forceinline__ const uint32_t* basic_word(const uint32_t* slices, const Geometry& g, uint32_t b) {
+    const uint32_t lb = b >> g.log2F;
+    return slices + ((uint64_t) (b & ((1u << g.log2F) - 1u)) * g.nseg + (lb >> g.log2seg)) * g.seg_words +
+           ((lb & (g.seg_bits - 1u)) >> 5);
+}
+
 // KIND_BASIC_KK: bits 2..k of add_basic (src/bloom_filter.c:73-111, the double-hashing sequence of
-// global_contains below) read from the global bitmap; bit 1 was tested from the LDS slice.
+// global_contains below) read from the slices in HBM; bit 1 was tested from the LDS slice.
 __device__ __forceinline__ bool basic_rest(uint32_t code, const Geometry& g, const uint32_t* inv,
-                                           const uint32_t* __restrict__ bm) {
+                                           const uint32_t* __restrict__ slices) {
     const uint32_t key = code_key(inv, code), msz = (uint32_t) g.m;
     uint32_t       h = mod_m(crapwow(kSeed, key), msz), y = mod_m(key + kSeed, msz);
     h = mod_m(h + y, msz);
     y = mod_m(y + 1u, msz);
     for (uint32_t i = 1; i < g.k; i++) {
-        if (!((bm[h >> 5] >> (h & 31u)) & 1u)) return false;
+        if (!((*basic_word(slices, g, h) >> ((h >> g.log2F) & 31u)) & 1u)) return false;
         h = mod_m(h + y, msz);
         y = mod_m(y + i + 1u, msz);
     }
@@ -1296,7 +1304,7 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
                         const uint32_t j   = lane + 64u * k;
                         const uint32_t key = code_key(inv, scr[j]);
                         b2h[k] = mod_m(mod_m(crapwow(kSeed, key), msz) + mod_m(key + kSeed, msz), msz);
-                        b2w[k] = P.bm[j < nsv ? b2h[k] >> 5 : 0u];
+                        b2w[k] = *basic_word(P.slices, g, j < nsv ? b2h[k] : 0u);
                     }
                 }
 #pragma unroll
@@ -1307,7 +1315,8 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
                     const uint32_t s  = (c >> g.sub_shift) & (NSUB - 1u);
                     bool           ok = j < nsv;
                     if (KIND == KIND_BASIC_KK)
-                        ok = ok && ((b2w[k] >> (b2h[k] & 31u)) & 1u) && (g.k == 2 || basic_rest(w, g, inv, P.bm));
+                        ok = ok && ((b2w[k] >> ((b2h[k] >> g.log2F) & 31u)) & 1u) &&
+                             (g.k == 2 || basic_rest(w, g, inv, P.slices));
                     else if (refine) ok = ok && apply_bits<KIND, false>(locate<KIND>(w, g, inv, q), g, slice);
                     const uint32_t r = atomicAdd(&cnt[ok ? s : 64u + lane], 1u);  // dummies: 64..127
                     dr[k]            = ok ? (s | (r << 16)) : kNoRank;
@@ -1320,7 +1329,7 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
                     for (int i = 0; i < NW; i++) {
                         bool ok = (uint32_t) (i & 3) < Sc.n[i >> 2];
                         if (KIND == KIND_BASIC_KK) {
-                            ok = ok && ((pass1 >> i) & 1u) && basic_rest(sweep_word(Sc, i >> 2, i & 3), g, inv, P.bm);
+                            ok = ok && ((pass1 >> i) & 1u) && basic_rest(sweep_word(Sc, i >> 2, i & 3), g, inv, P.slices);
                         } else if (ok) {
                             const Loc L = locate<KIND>(sweep_word(Sc, i >> 2, i & 3), g, inv, q);
                             ok          = (SEG1 || L.seg == seg) && apply_bits<KIND, false>(L, g, slice);
@@ -1799,31 +1808,61 @@ __global__ void k_export(const uint32_t* slices, Geometry g, uint32_t* out, uint
     }
 }
 
-// ===================================== K11b: basic k >= 2, partition slices from the global bitmap
-// Slice q bit lb = filter bit (lb << log2F) | q (k_export's inverse). The slices built by k_build
-// hold only the R keys' first bits; the reference tests bit 1 against every bit of the filter, so
-// the slices are replaced by this transpose of the global bitmap. q runs fastest, so a wave's 32
-// loads per output word touch two bitmap words each.
-__global__ void k_slices_from_bitmap(const uint32_t* __restrict__ bm, Geometry g,
-                                     uint32_t* __restrict__ slices) {
-    const uint32_t F1     = (1u << g.log2F) - 1u;
-    const uint64_t n      = (uint64_t) (F1 + 1u) * (g.slice_bits / 32u);
+// ======================================== K11b: basic k >= 2, partition slices without atomics
+// The reference sets all k bits of every R key anywhere in the m-bit filter (add_basic,
+// src/bloom_filter.c:73-89). Here every bit position becomes an element (k_bitpos), the SWWC
+// scatter partitions the positions by their low log2F bits (the slice they belong to, SRC_CODES),
+// and one workgroup per partition ORs its positions into the slice in LDS (k_slice_fill).
+__global__ void k_bitpos(const uint2* __restrict__ R, uint64_t n, Geometry g, uint32_t* __restrict__ out) {
     const uint64_t stride = (uint64_t) gridDim.x * blockDim.x;
-    for (uint64_t o = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x; o < n; o += stride) {
-        const uint32_t q = (uint32_t) o & F1, lb0 = (uint32_t) (o >> g.log2F) * 32u;
-        uint32_t       r = 0;
-#pragma unroll 8
-        for (uint32_t t = 0; t < 32; t++) {
-            const uint64_t gb = ((uint64_t) (lb0 + t) << g.log2F) | q;
-            r |= ((bm[gb >> 5] >> (uint32_t) (gb & 31u)) & 1u) << t;
+    const uint32_t msz    = (uint32_t) g.m;
+    for (uint64_t i = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint32_t key = R[i].x;
+        uint32_t       h = mod_m(crapwow(kSeed, key), msz), y = mod_m(key + kSeed, msz);
+        for (uint32_t j = 0; j < g.k; j++) {  // element j * n + i: coalesced per bit
+            out[(uint64_t) j * n + i] = h;
+            h = mod_m(h + y, msz);
+            y = mod_m(y + j + 1u, msz);
         }
-        const uint32_t seg = lb0 >> g.log2seg, off = lb0 & (g.seg_bits - 1u);
-        slices[((uint64_t) q * g.nseg + seg) * g.seg_words + (off >> 5)] = r;
     }
 }
 
-void launch_slices_from_bitmap(const uint32_t* bm, const Geometry& g, uint32_t* slices, hipStream_t st) {
-    k_slices_from_bitmap<<<4096, 256, 0, st>>>(bm, g, slices);
+__global__ __launch_bounds__(1024) void k_slice_fill(const uint32_t* __restrict__ pool,
+                                                     const uint32_t* __restrict__ list,
+                                                     const uint32_t* __restrict__ list_start, Geometry g,
+                                                     uint32_t* __restrict__ slices) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const uint32_t q = blockIdx.x, segw = g.seg_words;
+    const uint32_t l0 = list_start[q], l1 = list_start[q + 1];
+    const uint64_t nw = (uint64_t) (l1 - l0) * 32u;
+    for (uint32_t seg = 0; seg < g.nseg; seg++) {
+        for (uint32_t i = threadIdx.x; i < segw; i += blockDim.x) lds[i] = 0;
+        __syncthreads();
+        for (uint64_t i = threadIdx.x; i < nw; i += blockDim.x) {  // 32 lanes per chunk, coalesced
+            const uint32_t e = list[l0 + (uint32_t) (i >> 5)];
+            if ((uint32_t) (i & 31u) >= list_count(e)) continue;
+            const uint32_t lb = pool[(uint64_t) (e & kListIdMask) * 32 + (i & 31u)] >> g.log2F;
+            if ((lb >> g.log2seg) != seg) continue;
+            const uint32_t off = lb & (g.seg_bits - 1u);
+            atomicOr(&lds[off >> 5], 1u << (off & 31u));
+        }
+        __syncthreads();
+        uint4*       dst = (uint4*) (slices + ((uint64_t) q * g.nseg + seg) * segw);
+        const uint4* src = (const uint4*) lds;
+        for (uint32_t i = threadIdx.x; i < segw / 4; i += blockDim.x) dst[i] = src[i];
+        __syncthreads();
+    }
+}
+
+void launch_bitpos(const uint2* R, uint64_t n, const Geometry& g, uint32_t* out, hipStream_t st) {
+    k_bitpos<<<4096, 256, 0, st>>>(R, n, g, out);
+}
+
+void launch_slice_fill(const uint32_t* pool, const uint32_t* list, const uint32_t* list_start,
+                       const Geometry& g, uint32_t* slices, hipStream_t st) {
+    const size_t lds = (size_t) g.seg_words * 4;
+    (void) hipFuncSetAttribute((const void*) &k_slice_fill, hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds);
+    k_slice_fill<<<1u << g.log2F, 1024, lds, st>>>(pool, list, list_start, g, slices);
 }
 
 // ================================================================ K12: result materialization
@@ -2063,8 +2102,8 @@ void launch_build(const BuildParams& p, uint32_t F, hipStream_t st) {
         case KIND_BLOCK_PK1: return build_inst<KIND_BLOCK_PK1>(p, F, lds, st);
         case KIND_BLOCK_PKK: return build_inst<KIND_BLOCK_PKK>(p, F, lds, st);
         case KIND_BLOCK: return build_inst<KIND_BLOCK>(p, F, lds, st);
-        case KIND_BASIC_K1:
-        case KIND_BASIC_KK: return build_inst<KIND_BASIC_K1>(p, F, lds, st);  // (KK: first bits only)
+        case KIND_BASIC_K1: return build_inst<KIND_BASIC_K1>(p, F, lds, st);
+        case KIND_BASIC_KK: return build_inst<KIND_PASS>(p, F, lds, st);  // (KK: k_slice_fill sets the bits)
         default: return build_inst<KIND_PASS>(p, F, lds, st);
     }
 }
