@@ -49,6 +49,15 @@ def test_f3_grid(hw, f3, Bname):
         assert (st.filtered, st.matches) == (want, g["results"]), (Bname, k, st)
 
 
+def test_basic_multi_hash_takes_slice_path(hw, f3):
+    """Basic k >= 2 runs on the partition slices (MODE_SLICE_BASIC = 2, KIND_BASIC_KK), not the
+    global-bitmap fallback (mode 3)."""
+    g = GOLD["F3_grid"]
+    R, S = f3
+    for k in (2, 5):
+        assert hw.join_device(R, S, hw.BloomFilterArgs(hw.BASIC, g["m"], k, 1024)).mode == 2
+
+
 def test_f3_extra_and_pro(hw, cuda, f3):
     g = GOLD["F3_grid"]
     R, S = f3
@@ -155,7 +164,8 @@ def oracle_check(hw, cuda, orc, Rk, Sk, args, nthr=4):
 
 ARGS = [None, ("blocked", 1 << 20, 1, 1024), ("blocked", 1 << 22, 3, 512), ("basic", 1 << 20, 1, 0),
         ("basic", 1 << 20, 3, 0), ("sectorized", 1 << 20, 1, 1024), ("sectorized", 1 << 22, 4, 512),
-        ("blocked", 1 << 16, 2, 4), ("blocked", 1 << 31, 2, 512), ("blocked", 64, 1, 32)]
+        ("blocked", 1 << 16, 2, 4), ("blocked", 1 << 31, 2, 512), ("blocked", 64, 1, 32),
+        ("basic", 1 << 31, 2, 0), ("basic", 64, 3, 0)]
 
 
 def mk(hw, a):
