@@ -76,13 +76,14 @@ HWBRJ_HD uint32_t mix32(uint32_t x) {
 enum Mode : int {
     MODE_NOBLOOM      = 0,  // PRO: no filter
     MODE_SLICE_BLOCK  = 1,  // blocked/sectorized: S partitioned by block bits, probed from LDS slices
-    MODE_SLICE_BASIC  = 2,  // basic: partitioned by the first bit's index bits, LDS slices (k >= 2:
+    MODE_SLICE_BASIC  = 2,  // basic: partitioned by the first bit's index bits, element word = the key,
+                            // LDS slices (k >= 2:
                             // bits 2..k of the first-bit candidates from the global bitmap)
     MODE_GLOBAL       = 3,  // basic k = 0 or B < 8: global atomics build + direct probe (fallback)
 };
 
 enum Format : int {
-    FMT_CODE   = 0,  // element word = code = crc32c(42, key)
+    FMT_CODE   = 0,  // element word = code = crc32c(42, key) (MODE_SLICE_BASIC: the key)
     FMT_PACKED = 1,  // blocked, log2B <= log2F: (code >> log2F) | (first bit-in-block << (32 - log2F))
 };
 

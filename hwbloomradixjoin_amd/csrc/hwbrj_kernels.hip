@@ -83,7 +83,7 @@ template <int KIND>
 __device__ __forceinline__ Loc locate(uint32_t w, const Geometry& g, const uint32_t* inv, uint32_t q) {
     Loc L;
     if (KIND == KIND_BASIC_K1 || KIND == KIND_BASIC_KK) {
-        const uint32_t key = code_key(inv, w);
+        const uint32_t key = w;  // MODE_SLICE_BASIC words are the keys themselves
         const uint32_t b   = mod_m(crapwow(kSeed, key), (uint32_t) g.m);  // add_basic, first bit
         const uint32_t lb  = b >> g.log2F;
         L.seg  = lb >> g.log2seg;
@@ -155,9 +155,10 @@ __device__ __forceinline__ const uint32_t* basic_word(const uint32_t* slices, co
 
 // KIND_BASIC_KK: bits 2..k of add_basic (src/bloom_filter.c:73-111, the double-hashing sequence of
 // global_contains below) read from the slices in HBM; bit 1 was tested from the LDS slice.
-__device__ __forceinline__ bool basic_rest(uint32_t code, const Geometry& g, const uint32_t* inv,
+__device__ __forceinline__ bool basic_rest(uint32_t key, const Geometry& g, const uint32_t* inv,
                                            const uint32_t* __restrict__ slices) {
-    const uint32_t key = code_key(inv, code), msz = (uint32_t) g.m;
+    (void) inv;
+    const uint32_t msz = (uint32_t) g.m;
     uint32_t       h = mod_m(crapwow(kSeed, key), msz), y = mod_m(key + kSeed, msz);
     h = mod_m(h + y, msz);
     y = mod_m(y + 1u, msz);
@@ -402,8 +403,10 @@ __device__ __forceinline__ void sc_word_lds0(uint32_t x, const Geometry& g, cons
     const uint32_t code = crc_nib(tab, key);
 #endif
     if (MODE == MODE_SLICE_BASIC) {
+        // the partition is the first filter bit's slice, not a code digit, so the word carries
+        // the key itself: the join compares keys, and nothing downstream needs the CRC
         q = mod_m(crapwow(kSeed, key), (uint32_t) g.m) & F1;
-        w = code;
+        w = key;
     } else if (MODE == MODE_SLICE_BLOCK && FMT == FMT_PACKED) {
         q = code & F1;
 #ifdef HWBRJ_ABL_NOCRAP
@@ -1302,7 +1305,7 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
 #pragma unroll
                     for (int k = 0; k < kDense; k++) {
                         const uint32_t j   = lane + 64u * k;
-                        const uint32_t key = code_key(inv, scr[j]);
+                        const uint32_t key = scr[j];  // (the word is the key)
                         b2h[k] = mod_m(mod_m(crapwow(kSeed, key), msz) + mod_m(key + kSeed, msz), msz);
                         b2w[k] = *basic_word(P.slices, g, j < nsv ? b2h[k] : 0u);
                     }
