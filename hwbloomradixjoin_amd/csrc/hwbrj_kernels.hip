@@ -1297,17 +1297,35 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
             uint32_t   dr[kDense];
             uint32_t   rank2[NW / 2];            // word by word: two 16-bit ranks per register
             if (dense) {
-                // KIND_BASIC_KK: the second bit of every slot's candidate is loaded from the global
-                // bitmap before any is tested (kDense loads in flight instead of one at a time)
-                uint32_t b2w[KIND == KIND_BASIC_KK ? kDense : 1], b2h[KIND == KIND_BASIC_KK ? kDense : 1];
+                // KIND_BASIC_KK: bits 2..k of every slot's candidate from the slices in HBM, bit by
+                // bit, each bit loaded for all of the wave's live slots before any is tested
+                // (kDense loads in flight instead of one at a time); stops when no slot is live
+                constexpr int KD = KIND == KIND_BASIC_KK ? kDense : 1;
+                uint32_t      live[KD];
                 if (KIND == KIND_BASIC_KK) {
                     const uint32_t msz = (uint32_t) g.m;
+                    uint32_t       hh[KD], yy[KD], wv[KD];
 #pragma unroll
                     for (int k = 0; k < kDense; k++) {
                         const uint32_t j   = lane + 64u * k;
                         const uint32_t key = scr[j];  // (the word is the key)
-                        b2h[k] = mod_m(mod_m(crapwow(kSeed, key), msz) + mod_m(key + kSeed, msz), msz);
-                        b2w[k] = *basic_word(P.slices, g, j < nsv ? b2h[k] : 0u);
+                        const uint32_t y0  = mod_m(key + kSeed, msz);
+                        hh[k]   = mod_m(mod_m(crapwow(kSeed, key), msz) + y0, msz);  // bit 2
+                        yy[k]   = mod_m(y0 + 1u, msz);
+                        live[k] = j < nsv ? 1u : 0u;
+                    }
+                    for (uint32_t i = 1; i < g.k; i++) {
+#pragma unroll
+                        for (int k = 0; k < kDense; k++) wv[k] = live[k] ? *basic_word(P.slices, g, hh[k]) : 0u;
+                        uint32_t any = 0;
+#pragma unroll
+                        for (int k = 0; k < kDense; k++) {
+                            live[k] &= (wv[k] >> ((hh[k] >> g.log2F) & 31u)) & 1u;
+                            hh[k] = mod_m(hh[k] + yy[k], msz);
+                            yy[k] = mod_m(yy[k] + i + 1u, msz);
+                            any |= live[k];
+                        }
+                        if (__builtin_amdgcn_ballot_w64(any != 0) == 0) break;  // wave-uniform
                     }
                 }
 #pragma unroll
@@ -1318,8 +1336,7 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
                     const uint32_t s  = (c >> g.sub_shift) & (NSUB - 1u);
                     bool           ok = j < nsv;
                     if (KIND == KIND_BASIC_KK)
-                        ok = ok && ((b2w[k] >> ((b2h[k] >> g.log2F) & 31u)) & 1u) &&
-                             (g.k == 2 || basic_rest(w, g, inv, P.slices));
+                        ok = ok && live[k] != 0;
                     else if (refine) ok = ok && apply_bits<KIND, false>(locate<KIND>(w, g, inv, q), g, slice);
                     const uint32_t r = atomicAdd(&cnt[ok ? s : 64u + lane], 1u);  // dummies: 64..127
                     dr[k]            = ok ? (s | (r << 16)) : kNoRank;
