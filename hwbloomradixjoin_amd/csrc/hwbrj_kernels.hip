@@ -1858,13 +1858,29 @@ __global__ __launch_bounds__(1024) void k_slice_fill(const uint32_t* __restrict_
     for (uint32_t seg = 0; seg < g.nseg; seg++) {
         for (uint32_t i = threadIdx.x; i < segw; i += blockDim.x) lds[i] = 0;
         __syncthreads();
-        for (uint64_t i = threadIdx.x; i < nw; i += blockDim.x) {  // 32 lanes per chunk, coalesced
-            const uint32_t e = list[l0 + (uint32_t) (i >> 5)];
-            if ((uint32_t) (i & 31u) >= list_count(e)) continue;
-            const uint32_t lb = pool[(uint64_t) (e & kListIdMask) * 32 + (i & 31u)] >> g.log2F;
-            if ((lb >> g.log2seg) != seg) continue;
-            const uint32_t off = lb & (g.seg_bits - 1u);
-            atomicOr(&lds[off >> 5], 1u << (off & 31u));
+        // 32 lanes per chunk (coalesced); kFillU list entries, then kFillU words, in flight per thread
+        constexpr int kFillU = 8;
+        for (uint64_t i0 = threadIdx.x; i0 < nw; i0 += (uint64_t) blockDim.x * kFillU) {
+            uint32_t e[kFillU], v[kFillU], okm = 0;
+#pragma unroll
+            for (int u = 0; u < kFillU; u++) {
+                const uint64_t i = i0 + (uint64_t) u * blockDim.x;
+                e[u]             = i < nw ? list[l0 + (uint32_t) (i >> 5)] : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < kFillU; u++) {
+                const uint64_t i  = i0 + (uint64_t) u * blockDim.x;
+                const bool     ok = i < nw && (uint32_t) (i & 31u) < list_count(e[u]);
+                v[u]              = ok ? pool[(uint64_t) (e[u] & kListIdMask) * 32 + (i & 31u)] : 0u;
+                okm |= (ok ? 1u : 0u) << u;
+            }
+#pragma unroll
+            for (int u = 0; u < kFillU; u++) {
+                const uint32_t lb = v[u] >> g.log2F;
+                if (!((okm >> u) & 1u) || (lb >> g.log2seg) != seg) continue;
+                const uint32_t off = lb & (g.seg_bits - 1u);
+                atomicOr(&lds[off >> 5], 1u << (off & 31u));
+            }
         }
         __syncthreads();
         uint4*       dst = (uint4*) (slices + ((uint64_t) q * g.nseg + seg) * segw);
