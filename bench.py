@@ -53,22 +53,22 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=0,
                     help="S tuples in the CPU baseline run (0: the full |S|, the same workload)")
-    ap.add_argument("--cpu-threads", type=int, default=16)
-    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r01_pmc_traffic.json"))
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="port threads (0: every allowed CPU, capped by OMP_NUM_THREADS)")
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     return ap.parse_args()
 
 
-def phase_bytes(ph: str, nR: int, nS: int, filtered: int, m: int) -> float:
-    """Algorithmic bytes per launch of each pipeline phase (DESIGN.md "Roofline"): every input
-    tuple read once (8 B), every partitioned 4-byte word written once and read once."""
+def modeled_bytes(nR: int, nS: int, filtered: int, m: int, word_bytes: float) -> dict:
+    """Implementation bytes beyond the algorithmic 8-byte tuple reads (reported,
+    never in the headline): partition words written and read back, survivor codes, the filter."""
     return {
-        "r_scatter": 8.0 * nR + 4.0 * nR,
-        "build": 4.0 * nR + m / 8.0 + 4.0 * nR,
-        "s_scatter": 8.0 * nS + 4.0 * nS,
-        "probe": 4.0 * nS + 4.0 * filtered,
-        "surv": 8.0 * filtered,
-        "join": 4.0 * nR + 4.0 * filtered,
-    }.get(ph, 0.0)
+        "partition_words_R": 2.0 * 4.0 * nR,          # k_scatter_r writes, k_build reads
+        "partition_words_S": 2.0 * word_bytes * nS,   # k_scatter_s writes, k_probe reads
+        "join_codes_R": 2.0 * 4.0 * nR,               # k_build writes, k_join reads
+        "survivors": 2.0 * 4.0 * filtered,            # k_probe writes, k_join reads
+        "filter_slices": 2.0 * m / 8.0,               # k_build writes, k_probe loads
+    }
 
 
 def main():
@@ -122,19 +122,25 @@ def main():
     for _ in range(a.warmup):
         hw.join_device(dR, dS, args)
 
-    # timed region: K full joins enqueued back to back (hwbrj_join_device_async: no host round
-    # trip between them), then one wait for the last; counts of the last join are checked below
+    # Timed region: K full joins enqueued back to back on one stream (hwbrj_join_device_async: no
+    # host round trip between them), bracketed by barrier + synchronize; HIP events on that same
+    # stream give the device time of the K joins (the roofline's launch duration).
+    stream = torch.cuda.Stream()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    ev0.record(stream)
     for _ in range(a.steps):
-        hw.join_device_async(dR, dS, args)
+        hw.join_device_async(dR, dS, args, stream=stream)
+    ev1.record(stream)
     last = hw.join_wait()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    dev_ms = ev0.elapsed_time(ev1) / max(a.steps, 1)  # device ms per join on this rank
     if (last.filtered, last.matches) != (st.filtered, st.matches):
         raise SystemExit(f"timed join counts {last.filtered, last.matches} differ from the parity "
                          f"run {st.filtered, st.matches}")
@@ -147,9 +153,9 @@ def main():
                   "ms_s_index", "ms_probe", "ms_surv", "ms_join"):
             sums[f] = sums.get(f, 0.0) + getattr(st, f)
     if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
+        t = torch.tensor([elapsed, dev_ms], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed, dev_ms = (float(x) for x in t.tolist())
 
     if rank != 0:
         if dist:
@@ -158,24 +164,34 @@ def main():
 
     K = max(a.steps, 1)
     mean = {k: v / K for k, v in sums.items()}
-    phases = ["r_scatter", "build", "s_scatter", "probe", "surv", "join"]
-    dom = max(phases, key=lambda p: mean["ms_" + p])
-    local_filtered = st.filtered
-    bytes_dom = phase_bytes(dom, nR, nS, local_filtered, a.bloom_size if args else 0)
-    achieved = bytes_dom / (mean["ms_" + dom] * 1e-3) / 1e9
-    traffic = None
-    if os.path.exists(a.pmc_json):
-        try:
-            pm = json.load(open(a.pmc_json))
-            if pm.get("config_key") == [nR, nS, a.s_sel, a.bloom_filter, a.bloom_size,
-                                        a.bloom_hashes, a.bloom_block_size]:
-                traffic = pm.get("phases", {}).get(dom, {}).get("hbm_bytes")
-        except (OSError, ValueError):
-            traffic = None
-    roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "kernel": dom, "algorithmic_bytes": bytes_dom,
-                "kernel_ms": round(mean["ms_" + dom], 4)}
+    # Roofline: ALG_BYTES = sizeof(tuple_t) * (|R| + |S|), every input tuple read
+    # once; achieved = ALG_BYTES / t / (G * 8 TB/s) with t = the slowest rank's device time per join
+    # (HIP events over the timed region). Everything else the pipeline moves is modeled_bytes.
+    alg_bytes = 8.0 * (nR + nS_total) if a.scaling == "strong" else 8.0 * (nR + nS) * world
+    achieved = alg_bytes / (dev_ms * 1e-3) / 1e9
+    peak = HBM_PEAK_GBS * world
+    pm = load_pmc(a.pmc_json, [nR, nS, a.s_sel, a.bloom_filter, a.bloom_size, a.bloom_hashes,
+                               a.bloom_block_size]) if world == 1 else None
+    traffic = sum(p.get("hbm_bytes", 0) for p in pm["phases"].values()) if pm else None
+    # the dominant kernel against its own s8(d) bytes: k_scatter_s reads every S tuple once (8 B)
+    dom = max(("r_scatter", "build", "s_scatter", "probe", "join"), key=lambda p: mean["ms_" + p])
+    dom_alg = {"r_scatter": 8.0 * nR, "s_scatter": 8.0 * nS}.get(dom)
+    dom_ms = mean["ms_" + dom]
+    word_bytes = 2.75 if st.format == 2 else 4.0  # FMT_C22: 22-bit S words (88-byte chunks)
+    roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": peak, "unit": "GB/s",
+                "frac": round(achieved / peak, 4), "traffic": traffic,
+                "algorithmic_bytes": alg_bytes, "launch": "one full join (every kernel of BPRO)",
+                "launch_ms": round(dev_ms, 4),
+                "modeled_bytes": modeled_bytes(nR, nS, st.filtered, a.bloom_size if args else 0,
+                                               word_bytes),
+                "pmc_source": os.path.relpath(a.pmc_json, ROOT) if pm else None,
+                "dominant_kernel": {
+                    "name": {"s_scatter": "k_scatter_s", "r_scatter": "k_scatter_r",
+                             "probe": "k_probe", "build": "k_build", "join": "k_join"}[dom],
+                    "ms": round(dom_ms, 4), "algorithmic_bytes": dom_alg,
+                    "achieved": round(dom_alg / (dom_ms * 1e-3) / 1e9, 1) if dom_alg else None,
+                    "frac": round(dom_alg / (dom_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if dom_alg else None,
+                    "traffic": pm["phases"].get(dom, {}).get("hbm_bytes") if pm else None}}
 
     cpu = None
     if world == 1 and not a.no_cpu_baseline:
@@ -216,33 +232,71 @@ def main():
         dist.destroy_process_group()
 
 
+def load_pmc(path: str, key: list):
+    """Per-phase HBM bytes of one join (tools/prof_summary.py output) when it was collected on
+    this exact configuration, else None."""
+    try:
+        pm = json.load(open(path))
+    except (OSError, ValueError):
+        return None
+    return pm if pm.get("config_key") == key else None
+
+
+def host_cpu() -> dict:
+    """The host's CPU model, logical CPU count and the CPUs this process may run on."""
+    model = "unknown"
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                model = ln.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    allowed = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    return {"model": model, "nproc": os.cpu_count(), "allowed_cpus": allowed}
+
+
+# Calibration (BASELINE.md "Calibration of the CPU port"): on the same 8-core host the reference
+# binary needs 6.0 s where this port needs 13.5 s (C2, -n 8), i.e. the port runs at 0.45x it.
+PORT_VS_REFERENCE = 6.0 / 13.5
+
+
 def cpu_baseline(a, hw):
-    """The oracle's pthreads restatement of BPRO (oracle/oracle.c), full R and full filter size,
-    on the first --cpu-sample tuples of S; probe-tuples/s over its TOTAL-TIME region."""
+    """The oracle's pthreads restatement of BPRO (oracle/oracle.c, "port") on the GPU host's CPU:
+    full |R| and filter, the first --cpu-sample tuples of S (default: all of it), timed over the
+    reference's TOTAL-TIME region, once on every CPU this process may use (capped by
+    OMP_NUM_THREADS, the box's CPU share) and once at 8 threads (the reference's measured -n 8)."""
+    info = host_cpu()
     try:
         from oracle import pyoracle as orc
         sample = min(a.cpu_sample, a.s_size) if a.cpu_sample > 0 else a.s_size
-        R = hw.generate_host(a.r_size, a.nthreads, a.r_size, a.r_size, 1.0, 12345, a.cpu_threads)
+        cap = int(os.environ.get("OMP_NUM_THREADS") or info["allowed_cpus"])
+        threads = a.cpu_threads if a.cpu_threads > 0 else max(1, min(info["allowed_cpus"], cap))
+        R = hw.generate_host(a.r_size, a.nthreads, a.r_size, a.r_size, 1.0, 12345, threads)
         # a |S|=sample relation of the same generator (same q, same key ranges)
-        S = hw.generate_host(sample, a.nthreads, 2**31 - 1, a.r_size, a.s_sel, 54321,
-                             a.cpu_threads)
+        S = hw.generate_host(sample, a.nthreads, 2**31 - 1, a.r_size, a.s_sel, 54321, threads)
         variant = {"basic": 0, "blocked": 1, "sectorized": 2}.get(a.bloom_filter, 0)
         use = a.bloom_filter != "no"
-        res, filt, tm = orc.bpro(R, S, a.cpu_threads, variant, a.bloom_size, a.bloom_hashes,
-                                 a.bloom_block_size, use)
-        secs = tm["total"] / 1e6
-        return {"value": round(sample / secs, 1), "unit": "probe-tuples/s",
-                "cores": a.cpu_threads, "kind": "port",
+        runs = {}
+        for t in sorted({threads, 8}):
+            res, filt, tm = orc.bpro(R, S, t, variant, a.bloom_size, a.bloom_hashes,
+                                     a.bloom_block_size, use)
+            runs[t] = (sample / (tm["total"] / 1e6), tm["total"] / 1e6, filt, res)
+        v, secs, filt, res = runs[threads]
+        return {"value": round(v, 1), "unit": "probe-tuples/s", "cores": threads, "kind": "port",
+                "host": info, "value_n8": round(runs[8][0], 1),
+                "calibration_port_vs_reference": round(PORT_VS_REFERENCE, 3),
+                "reference_estimate": round(v / PORT_VS_REFERENCE, 1),
                 "sample": (f"|R|={a.r_size}, |S|={sample} tuples of the same generator "
                            f"(q={a.s_sel}), m={a.bloom_size}"
                            + (" (the full workload)" if sample == a.s_size else " (S sample)")
-                           + f"; oracle orc_bpro TOTAL-TIME {secs:.3f} s, filtered={filt} "
-                           f"matches={res}. Calibration: this port needs 13.5 s at 8 threads "
-                           "where the reference binary needs 6.0 s on the same host (BASELINE.md "
-                           "s2), i.e. it understates the reference's CPU rate about 2.2x")}
+                           + f"; oracle orc_bpro TOTAL-TIME {secs:.3f} s on {threads} threads "
+                           f"({runs[8][1]:.3f} s on 8), filtered={filt} matches={res}. The port "
+                           f"runs at {PORT_VS_REFERENCE:.2f}x the reference binary on the same "
+                           "host (BASELINE.md), so reference_estimate = value / that ratio")}
     except Exception as e:  # the baseline is reported, never required for the GPU line
-        return {"value": None, "unit": "probe-tuples/s", "cores": a.cpu_threads, "kind": "port",
-                "sample": f"failed: {e}"}
+        return {"value": None, "unit": "probe-tuples/s", "cores": None, "kind": "port",
+                "host": info, "sample": f"failed: {e}"}
 
 
 if __name__ == "__main__":

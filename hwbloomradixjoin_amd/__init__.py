@@ -17,7 +17,7 @@ import numpy as np
 
 __all__ = [
     "BASIC", "BLOCKED", "SECTORIZED", "BloomFilterArgs", "Relation", "Result", "Stats",
-    "BPRO", "PRO", "join_materialize_device", "set_materialize", "BPRH", "BPRHO", "BRJ", "PRH", "PRHO", "RJ", "assert_args", "join_device", "join_device_async", "join_wait", "generate_device", "generate_device_range",
+    "BPRO", "PRO", "join_materialize_device", "set_materialize", "set_gpus", "BPRH", "BPRHO", "BRJ", "PRH", "PRHO", "RJ", "assert_args", "join_device", "join_device_async", "join_wait", "generate_device", "generate_device_range",
     "generate_host", "nonunique_threshold", "create_relation_nonunique",
     "create_relation_nonunique_from_pk", "create_relation_fk_from_pk", "create_relation_zipf",
     "rand_stream", "reference_relations", "create_relation_zipf_device",
@@ -57,7 +57,7 @@ class _Stats(ctypes.Structure):  # include/hwbrj.h hwbrj_stats_t
                 ("subparts", ctypes.c_uint32), ("slice_segments", ctypes.c_uint32)] + [
                     (n, ctypes.c_double) for n in (
                         "ms_total", "ms_r_scatter", "ms_r_index", "ms_build", "ms_s_scatter",
-                        "ms_s_index", "ms_probe", "ms_surv", "ms_join")]
+                        "ms_s_index", "ms_probe", "ms_surv", "ms_join", "ms_join_probe")]
 
 
 _LIB = None
@@ -108,6 +108,8 @@ def lib() -> ctypes.CDLL:
             ctypes.POINTER(ctypes.c_double)]
         L.hwbrj_set_materialize.restype = None
         L.hwbrj_set_materialize.argtypes = [ctypes.c_int]
+        L.hwbrj_set_gpus.restype = ctypes.c_int
+        L.hwbrj_set_gpus.argtypes = [ctypes.c_int]
         L.hwbrj_generate_device.restype = ctypes.c_int
         L.hwbrj_generate_device.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
                                             ctypes.c_uint64, ctypes.c_uint64, ctypes.c_double,
@@ -245,6 +247,12 @@ def _take_result(r) -> Result:
     return out
 
 
+def set_gpus(gpus: int) -> None:
+    """Shards of S for host BPRO/PRO (hwbrj_set_gpus): shard g on visible device g mod
+    device_count, R replicated, counts summed. 0 restores the default (HWBRJ_GPUS, else 1)."""
+    _err(lib().hwbrj_set_gpus(int(gpus)), "hwbrj_set_gpus")
+
+
 def set_materialize(on: bool) -> None:
     """Materialize {R.payload, S.payload} pairs in BPRO/PRO results (JOIN_RESULT_MATERIALIZE)."""
     lib().hwbrj_set_materialize(1 if on else 0)
@@ -268,6 +276,7 @@ class Stats:
     ms_probe: float
     ms_surv: float
     ms_join: float
+    ms_join_probe: float
 
 
 class Relation:
@@ -346,9 +355,16 @@ def _ptr(t) -> int:
 
 
 def _check_rel(R, S):
+    """Both relations: contiguous (N, 2) torch.int32 tensors ({key, payload}) on one GPU. The
+    library's current HIP device is switched to that GPU (the join runs on its Engine)."""
+    import torch
     for name, t in (("R", R), ("S", S)):
-        if not t.is_cuda or t.dtype.itemsize != 4 or (t.numel() and t.shape[-1] != 2) or not t.is_contiguous():
-            raise ValueError(f"{name} must be a contiguous (N, 2) int32 tensor on the GPU")
+        if (not t.is_cuda or t.dtype != torch.int32 or t.dim() != 2 or t.shape[1] != 2
+                or not t.is_contiguous()):
+            raise ValueError(f"{name} must be a contiguous (N, 2) torch.int32 tensor on the GPU")
+    if R.device != S.device:
+        raise ValueError(f"R is on {R.device} but S is on {S.device}")
+    _err(lib().hwbrj_set_device(R.device.index or 0), "hwbrj_set_device")
 
 
 def join_device_async(R, S, args: Optional[BloomFilterArgs] = None, stream=None) -> None:

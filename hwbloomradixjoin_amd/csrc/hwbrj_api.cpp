@@ -5,6 +5,7 @@
 #include <string.h>
 #include <x86intrin.h>
 
+#include <algorithm>
 #include <chrono>
 #include <string>
 #include <thread>
@@ -97,7 +98,17 @@ int hwbrj_join_materialize_device(const tuple_t* d_R, uint64_t nR, const tuple_t
 }
 
 static int g_materialize = -1;  // -1: from HWBRJ_MATERIALIZE
+static int g_gpus        = 0;   // shards of a host BPRO/PRO (0: from HWBRJ_GPUS, default 1)
 void hwbrj_set_materialize(int on) { g_materialize = on ? 1 : 0; }
+
+int hwbrj_set_gpus(int g) {
+    if (g < 0 || g > 4096) {
+        set_last_error("gpus must be in [0, 4096]");
+        return 2;
+    }
+    g_gpus = g;
+    return 0;
+}
 
 int hwbrj_generate_device(tuple_t* d_out, uint64_t n, uint32_t nthreads, uint64_t maxid,
                           uint64_t threshold, double selectivity, uint64_t seed, void* stream) {
@@ -265,49 +276,165 @@ static threadresult_t* materialize_to_host(const tuple_t* dR, uint64_t nR, const
     return tres;
 }
 
+static int host_shards() {
+    if (g_gpus > 0) return g_gpus;
+    const char* e = getenv("HWBRJ_GPUS");
+    const int   v = e ? atoi(e) : 1;
+    return v > 0 ? v : 1;
+}
+
+// One shard of a host join: R replicated, S rows [s0, s1) (the reference's per-thread chunking of
+// S, src/parallel_radix_join_bloom.c:1646-1670, with a GPU per chunk).
+struct Shard {
+    uint64_t      s0 = 0, s1 = 0;
+    hwbrj_stats_t st{};
+    double        h2d_usec = 0;
+};
+
+// Shards first, first + step, ... on device `dev`, one after the other on its Engine: H2D of R
+// once, then per shard H2D of its S rows and the join. Returns 0 or an error code.
+static int run_device_shards(int dev, int first, int step, const relation_t* relR,
+                             const relation_t* relS, const bloom_filter_args_t* args,
+                             std::vector<Shard>& shards) {
+    if (hipSetDevice(dev) != hipSuccess) {
+        set_last_error("hipSetDevice failed");
+        return 11;
+    }
+    const uint64_t nR = relR->num_tuples;
+    uint64_t       smax = 0;
+    for (size_t g = first; g < shards.size(); g += step) smax = std::max(smax, shards[g].s1 - shards[g].s0);
+    tuple_t *dR = nullptr, *dS = nullptr;
+    if (hipMalloc((void**) &dR, (nR ? nR : 1) * sizeof(tuple_t)) != hipSuccess ||
+        hipMalloc((void**) &dS, (smax ? smax : 1) * sizeof(tuple_t)) != hipSuccess) {
+        set_last_error("hipMalloc of the input relations failed");
+        return 12;
+    }
+    int rc = 0;
+    // H2D outside the timed region (the reference's timer starts after its allocations).
+    const auto h0 = std::chrono::steady_clock::now();
+    if (nR && hipMemcpy(dR, relR->tuples, nR * sizeof(tuple_t), hipMemcpyHostToDevice) != hipSuccess) {
+        set_last_error("H2D copy failed");
+        rc = 13;
+    }
+    double h2d_r = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - h0).count();
+    for (size_t g = first; g < shards.size() && rc == 0; g += step) {
+        Shard&         sh = shards[g];
+        const uint64_t n  = sh.s1 - sh.s0;
+        const auto     h1 = std::chrono::steady_clock::now();
+        if (n && hipMemcpy(dS, relS->tuples + sh.s0, n * sizeof(tuple_t), hipMemcpyHostToDevice) != hipSuccess) {
+            set_last_error("H2D copy failed");
+            rc = 13;
+            break;
+        }
+        sh.h2d_usec = h2d_r + std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - h1).count();
+        h2d_r       = 0;
+        rc          = hwbrj_join_device(dR, nR, dS, n, args, nullptr, &sh.st);
+    }
+    (void) hipFree(dR);
+    (void) hipFree(dS);
+    return rc;
+}
+
 static result_t* run_host_join(relation_t* relR, relation_t* relS, int nthreads,
-                               bloom_filter_args_t* args) {
+                               bloom_filter_args_t* args, bool print_filtered = true) {
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) {
         set_last_error("no MI355X device visible");
         fatal("BPRO");
     }
+    int cur = 0;
+    (void) hipGetDevice(&cur);
     const uint64_t nR = relR->num_tuples, nS = relS->num_tuples;
-    tuple_t *dR = nullptr, *dS = nullptr;
-    if (hipMalloc((void**) &dR, (nR ? nR : 1) * sizeof(tuple_t)) != hipSuccess ||
-        hipMalloc((void**) &dS, (nS ? nS : 1) * sizeof(tuple_t)) != hipSuccess) {
-        set_last_error("hipMalloc of the input relations failed");
-        fatal("BPRO");
+    // G shards of S over the visible devices (shard g on device g mod ndev; G > ndev runs several
+    // shards per device one after the other, e.g. to rehearse G = 8 on one GPU)
+    const int          G    = host_shards();
+    const int          nuse = std::min(G, ndev);
+    std::vector<Shard> shards(G);
+    for (int g = 0; g < G; g++) {
+        shards[g].s0 = nS * (uint64_t) g / (uint64_t) G;
+        shards[g].s1 = nS * (uint64_t) (g + 1) / (uint64_t) G;
     }
-    // H2D outside the timed region (the reference's timer starts after its allocations).
-    const auto h0 = std::chrono::steady_clock::now();
-    if ((nR && hipMemcpy(dR, relR->tuples, nR * sizeof(tuple_t), hipMemcpyHostToDevice) != hipSuccess) ||
-        (nS && hipMemcpy(dS, relS->tuples, nS * sizeof(tuple_t), hipMemcpyHostToDevice) != hipSuccess)) {
-        set_last_error("H2D copy failed");
-        fatal("BPRO");
-    }
-    const double h2d_usec =
-        std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - h0).count();
-    hwbrj_stats_t st;
+    std::vector<int> rcs(nuse, 0);
+    std::vector<std::string> errs(nuse);
     const uint64_t c0 = __rdtsc();
-    if (hwbrj_join_device(dR, nR, dS, nS, args, nullptr, &st) != 0) fatal("BPRO");
+    if (nuse == 1) {
+        rcs[0] = run_device_shards(cur, 0, 1, relR, relS, args, shards);
+        errs[0] = hwbrj_last_error();
+    } else {  // one host thread per device (the reference's nthreads workers, one per GPU)
+        std::vector<std::thread> th;
+        for (int d = 0; d < nuse; d++)
+            th.emplace_back([&, d] {
+                rcs[d]  = run_device_shards(d, d, nuse, relR, relS, args, shards);
+                errs[d] = hwbrj_last_error();
+            });
+        for (auto& t : th) t.join();
+    }
     const uint64_t c1 = __rdtsc();
+    (void) hipSetDevice(cur);
+    for (int d = 0; d < nuse; d++)
+        if (rcs[d]) {
+            set_last_error(errs[d]);
+            fatal("BPRO");
+        }
+    // counts summed over shards; device times: the slowest device (its shards back to back)
+    hwbrj_stats_t st{};
+    std::vector<double> dev_ms(nuse, 0.0), dev_join(nuse, 0.0), dev_probe(nuse, 0.0);
+    double h2d_usec = 0;
+    for (int g = 0; g < G; g++) {
+        const hwbrj_stats_t& s = shards[g].st;
+        st.filtered += s.filtered;
+        st.matches += s.matches;
+        st.mode = s.mode, st.format = s.format, st.partitions = s.partitions;
+        st.subparts = s.subparts, st.slice_segments = s.slice_segments;
+        dev_ms[g % nuse] += s.ms_total;
+        dev_join[g % nuse] += s.ms_join;
+        dev_probe[g % nuse] += s.ms_join_probe;
+        h2d_usec = std::max(h2d_usec, shards[g].h2d_usec);
+        st.ms_r_scatter += s.ms_r_scatter, st.ms_r_index += s.ms_r_index, st.ms_build += s.ms_build;
+        st.ms_s_scatter += s.ms_s_scatter, st.ms_s_index += s.ms_s_index, st.ms_probe += s.ms_probe;
+        st.ms_surv += s.ms_surv;
+    }
+    const int slow = (int) (std::max_element(dev_ms.begin(), dev_ms.end()) - dev_ms.begin());
+    st.ms_total      = dev_ms[slow];
+    st.ms_join       = dev_join[slow];
+    st.ms_join_probe = dev_probe[slow];
+    // materialization (JOIN_RESULT_MATERIALIZE) runs on one device over the whole relations
     const bool mat = g_materialize == 1 || (g_materialize < 0 && getenv("HWBRJ_MATERIALIZE"));
     threadresult_t* tres = nullptr;
-    if (mat) tres = materialize_to_host(dR, nR, dS, nS, args, (uint64_t) st.matches, nthreads);
-    (void) hipFree(dR);
-    (void) hipFree(dS);
-    if (args) fprintf(stdout, "S-tuples after filter: %d\n", (int) st.filtered);  // :1253
-    const double part_ms = st.ms_total - st.ms_join;
-    const uint64_t total_cyc = c1 - c0;
-    const uint64_t part_cyc  = st.ms_total > 0 ? (uint64_t) (total_cyc * (part_ms / st.ms_total)) : 0;
-    print_timing(total_cyc, total_cyc - part_cyc, part_cyc, nS, st.matches, st.ms_total * 1e3,
-                 part_ms * 1e3, st.ms_join * 1e3, st.ms_join * 1e3);
+    if (mat) {
+        tuple_t *dR = nullptr, *dS = nullptr;
+        if (hipMalloc((void**) &dR, (nR ? nR : 1) * sizeof(tuple_t)) != hipSuccess ||
+            hipMalloc((void**) &dS, (nS ? nS : 1) * sizeof(tuple_t)) != hipSuccess ||
+            (nR && hipMemcpy(dR, relR->tuples, nR * sizeof(tuple_t), hipMemcpyHostToDevice) != hipSuccess) ||
+            (nS && hipMemcpy(dS, relS->tuples, nS * sizeof(tuple_t), hipMemcpyHostToDevice) != hipSuccess)) {
+            set_last_error("device copies of the relations for materialization failed");
+            fatal("BPRO");
+        }
+        hwbrj_stats_t one;
+        if (G > 1 && hwbrj_join_device(dR, nR, dS, nS, args, nullptr, &one) != 0) fatal("BPRO");
+        tres = materialize_to_host(dR, nR, dS, nS, args, (uint64_t) st.matches, nthreads);
+        (void) hipFree(dR);
+        (void) hipFree(dS);
+    }
+    // "S-tuples after filter" is printed by BPRO/BPRH/BPRHO's thread 0 (:1253); BRJ has no such line
+    if (args && print_filtered) fprintf(stdout, "S-tuples after filter: %d\n", (int) st.filtered);
+    // print_timing (:1730-1742): PARTITION = start -> partitioned (both partition passes, filter
+    // build and probe), JOIN = partitioned -> end, PROBE = the probe share of the join (the
+    // reference's per-thread probe timers, bucket_chaining_join :289-321), cycles likewise
+    const double total_cyc = (double) (c1 - c0);
+    const double part_ms   = st.ms_total - st.ms_join;
+    const double frac_part = st.ms_total > 0 ? part_ms / st.ms_total : 0.0;
+    const double frac_prob = st.ms_total > 0 ? st.ms_join_probe / st.ms_total : 0.0;
+    const uint64_t part_cyc  = (uint64_t) (total_cyc * frac_part);
+    const uint64_t probe_cyc = (uint64_t) (total_cyc * frac_prob);
+    print_timing((uint64_t) total_cyc, (uint64_t) total_cyc - part_cyc - probe_cyc, part_cyc, nS,
+                 st.matches, st.ms_total * 1e3, part_ms * 1e3, st.ms_join_probe * 1e3, st.ms_join * 1e3);
     if (getenv("HWBRJ_VERBOSE"))
         fprintf(stderr,
-                "[hwbrj] mode=%d format=%d F=%u NSUB=%u nseg=%u h2d_usec=%.1f | ms: r_scatter %.3f "
-                "r_index %.3f build %.3f s_scatter %.3f s_index %.3f probe %.3f surv %.3f join %.3f\n",
-                st.mode, st.format, st.partitions, st.subparts, st.slice_segments, h2d_usec,
+                "[hwbrj] shards=%d devices=%d mode=%d format=%d F=%u NSUB=%u nseg=%u h2d_usec=%.1f | "
+                "ms (summed over shards): r_scatter %.3f r_index %.3f build %.3f s_scatter %.3f "
+                "s_index %.3f probe %.3f surv %.3f | join (slowest device) %.3f\n",
+                G, nuse, st.mode, st.format, st.partitions, st.subparts, st.slice_segments, h2d_usec,
                 st.ms_r_scatter, st.ms_r_index, st.ms_build, st.ms_s_scatter, st.ms_s_index,
                 st.ms_probe, st.ms_surv, st.ms_join);
     result_t* res = (result_t*) malloc(sizeof(result_t));
@@ -345,7 +472,7 @@ result_t* BPRHO(relation_t* relR, relation_t* relS, int nthreads, bloom_filter_a
     return run_host_join(relR, relS, nthreads, a);
 }
 result_t* BRJ(relation_t* relR, relation_t* relS, int nthreads, bloom_filter_args_t* a) {
-    return run_host_join(relR, relS, nthreads, a);
+    return run_host_join(relR, relS, nthreads, a, false);
 }
 result_t* PRH(relation_t* relR, relation_t* relS, int nthreads) {
     return run_host_join(relR, relS, nthreads, nullptr);

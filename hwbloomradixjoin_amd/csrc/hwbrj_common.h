@@ -71,6 +71,18 @@ HWBRJ_HD uint32_t mix32(uint32_t x) {
     return x;
 }
 
+// MODE_SLICE_BASIC partition words: an invertible mix of the key (not the key itself), so the
+// join's sub-partition digit (the word's low bits) is spread even when keys share their low bits
+// (e.g. all multiples of 64), and equal words still mean equal keys.
+constexpr uint32_t kBMixC    = 0x9E3779B1u;  // odd: invertible mod 2^32
+constexpr uint32_t kBMixCinv = 0x0E8B2F51u;  // kBMixC * kBMixCinv == 1 (mod 2^32)
+HWBRJ_HD uint32_t bmix(uint32_t key) {
+    const uint32_t h = key * kBMixC;
+    return h ^ (h >> 16);
+}
+static_assert(kBMixC * kBMixCinv == 1u, "kBMixCinv inverts kBMixC");
+HWBRJ_HD uint32_t bunmix(uint32_t w) { return (w ^ (w >> 16)) * kBMixCinv; }
+
 // ------------------------------------------------------------------------- filter geometry
 // Everything the kernels need about the filter and the partitioning, computed on the host.
 enum Mode : int {

@@ -280,6 +280,9 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
         return 2;
     }
     if (!stream) stream = own_stream_;
+    // Every join on this device shares this Engine's scratch (pools, lists, slices, counters):
+    // a join enqueued on another stream than a still-pending one must run after it.
+    if (pending_) HWBRJ_CHECK(hipStreamWaitEvent(stream, ev_[8], 0));
     const uint32_t F = 1u << g.log2F, NSUB = 1u << g.log2NSUB, NJ = F * NSUB;
     const bool     slice_mode = g.mode == MODE_SLICE_BLOCK || g.mode == MODE_SLICE_BASIC;
     const uint32_t nseg       = slice_mode ? g.nseg : 1;
@@ -316,7 +319,10 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
           survoff.ensure(items_max * NSUB * 4);
     ok &= small.ensure(128 + 64 * 128) && colR.ensure(F * 12) && colS.ensure(F * 12);  // u64 elems | u32 chunks
     // jparts: nparts [NJ] | job_surv [NJ] | nextra; jtask: extra parts {job, part}
-    const bool jnew = jparts.bytes < (size_t) (2 * NJ + 1) * 4;
+    // (job_surv is left zero by k_join_split for the NJ jobs it saw: a join with another NJ
+    // clears the whole buffer, so no stale count of an earlier job layout is read)
+    const bool jnew = jparts.bytes < (size_t) (2 * NJ + 1) * 4 || NJ != last_nj_;
+    last_nj_ = NJ;
     ok &= jtask.ensure((size_t) join_extra_tasks() * 8) && jparts.ensure((size_t) (2 * NJ + 1) * 4);
     if (slice_mode) ok &= slices.ensure((uint64_t) F * nseg * g.seg_words * 4);
     if (g.mode == MODE_GLOBAL) ok &= bitmap.ensure(((g.m + 31) / 32) * 4) && dense.ensure(nS * 4);
@@ -527,9 +533,10 @@ int Engine::wait(hwbrj_stats_t* st) {
     const uint32_t  nseg = (g.mode == MODE_SLICE_BLOCK || g.mode == MODE_SLICE_BASIC) ? g.nseg : 1;
     const uint64_t* d_result   = small.as<uint64_t>();      // (see enqueue)
     const uint64_t* d_filtered = small.as<uint64_t>() + 2;
-    uint64_t matches = 0, filtered = 0;
-    HWBRJ_CHECK(hipMemcpy(&matches, d_result, 8, hipMemcpyDeviceToHost));
-    HWBRJ_CHECK(hipMemcpy(&filtered, d_filtered, 8, hipMemcpyDeviceToHost));
+    uint64_t small_h[5] = {0, 0, 0, 0, 0};  // matches, dcount, filtered, probe ticks, join ticks
+    HWBRJ_CHECK(hipMemcpy(small_h, d_result, sizeof small_h, hipMemcpyDeviceToHost));
+    (void) d_filtered;
+    const uint64_t matches = small_h[0], filtered = small_h[2];
     if (st) {
         memset(st, 0, sizeof(*st));
         st->filtered       = pending_args_ ? filtered : pending_nS_;
@@ -551,6 +558,8 @@ int Engine::wait(hwbrj_stats_t* st) {
         st->ms_probe     = ms[6];
         st->ms_surv      = ms[7];
         st->ms_join      = ms[8];
+        // the probe share of the join's workgroup time (k_join's wall_clock64 sections)
+        st->ms_join_probe = small_h[4] ? ms[8] * (double) small_h[3] / (double) small_h[4] : 0.0;
     }
     return 0;
 }

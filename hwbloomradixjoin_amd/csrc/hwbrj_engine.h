@@ -56,6 +56,7 @@ class Engine {
     bool         pending_      = false;
     bool         pending_args_ = false;
     uint64_t     pending_nS_   = 0;
+    uint32_t     last_nj_      = 0;  // join jobs of the last enqueue (job_surv layout)
     int          enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
                          const bloom_filter_args_t* args, hipStream_t stream, bool dbg);
     CrcTables*   d_tabs_ = nullptr;

@@ -83,7 +83,7 @@ template <int KIND>
 __device__ __forceinline__ Loc locate(uint32_t w, const Geometry& g, const uint32_t* inv, uint32_t q) {
     Loc L;
     if (KIND == KIND_BASIC_K1 || KIND == KIND_BASIC_KK) {
-        const uint32_t key = w;  // MODE_SLICE_BASIC words are the keys themselves
+        const uint32_t key = bunmix(w);  // MODE_SLICE_BASIC words are bmix(key)
         const uint32_t b   = mod_m(crapwow(kSeed, key), (uint32_t) g.m);  // add_basic, first bit
         const uint32_t lb  = b >> g.log2F;
         L.seg  = lb >> g.log2seg;
@@ -404,9 +404,9 @@ __device__ __forceinline__ void sc_word_lds0(uint32_t x, const Geometry& g, cons
 #endif
     if (MODE == MODE_SLICE_BASIC) {
         // the partition is the first filter bit's slice, not a code digit, so the word carries
-        // the key itself: the join compares keys, and nothing downstream needs the CRC
+        // the key (mixed, bmix): the join compares words, and nothing downstream needs the CRC
         q = mod_m(crapwow(kSeed, key), (uint32_t) g.m) & F1;
-        w = key;
+        w = bmix(key);
     } else if (MODE == MODE_SLICE_BLOCK && FMT == FMT_PACKED) {
         q = code & F1;
 #ifdef HWBRJ_ABL_NOCRAP
@@ -1308,7 +1308,7 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
 #pragma unroll
                     for (int k = 0; k < kDense; k++) {
                         const uint32_t j   = lane + 64u * k;
-                        const uint32_t key = scr[j];  // (the word is the key)
+                        const uint32_t key = bunmix(scr[j]);  // (the word is bmix(key))
                         const uint32_t y0  = mod_m(key + kSeed, msz);
                         hh[k]   = mod_m(mod_m(crapwow(kSeed, key), msz) + y0, msz);  // bit 2
                         yy[k]   = mod_m(y0 + 1u, msz);
@@ -1349,7 +1349,7 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
                     for (int i = 0; i < NW; i++) {
                         bool ok = (uint32_t) (i & 3) < Sc.n[i >> 2];
                         if (KIND == KIND_BASIC_KK) {
-                            ok = ok && ((pass1 >> i) & 1u) && basic_rest(sweep_word(Sc, i >> 2, i & 3), g, inv, P.slices);
+                            ok = ok && ((pass1 >> i) & 1u) && basic_rest(bunmix(sweep_word(Sc, i >> 2, i & 3)), g, inv, P.slices);
                         } else if (ok) {
                             const Loc L = locate<KIND>(sweep_word(Sc, i >> 2, i & 3), g, inv, q);
                             ok          = (SEG1 || L.seg == seg) && apply_bits<KIND, false>(L, g, slice);
@@ -1503,7 +1503,8 @@ __global__ __launch_bounds__(256) void k_join_split(const uint32_t* __restrict__
                                                      uint32_t* __restrict__ nparts,
                                                      uint2* __restrict__ extra, uint32_t* nextra,
                                                      uint64_t* __restrict__ jsum) {
-    if (blockIdx.x == 0 && threadIdx.x < kJoinSumSlots) jsum[threadIdx.x * kJoinSumStride] = 0;
+    if (blockIdx.x == 0 && threadIdx.x < kJoinSumSlots)
+        for (int w = 0; w < 3; w++) jsum[threadIdx.x * kJoinSumStride + w] = 0;
     const uint32_t job = blockIdx.x * blockDim.x + threadIdx.x;  // one thread per job
     if (job >= NJ) return;
     const uint32_t q = job >> log2NSUB, items = item_start[q + 1] - item_start[q];
@@ -1551,6 +1552,12 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
     const uint32_t sh  = P.hash_shift;
     const int      tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     uint64_t       cnt = 0;
+    // probe share of the join (the reference's per-thread probe timers, :289-321): thread 0 sums
+    // the 100 MHz ticks of the survivor-probing sections of this workgroup
+    const uint64_t t_start = wall_clock64();
+    uint64_t       t_probe = 0, t_mark = 0;
+    auto probe_begin = [&]() { t_mark = wall_clock64(); };
+    auto probe_end   = [&]() { t_probe += wall_clock64() - t_mark; };
     // The words [from, n) of one run (long runs: high-selectivity survivors, large R runs), with
     // kJoinTailU loads in flight per lane instead of one dependent load per iteration.
     auto tail_run = [&](const uint32_t* data, uint64_t bb, uint32_t from, uint32_t n, auto&& op) {
@@ -1608,6 +1615,7 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
     using SW = std::integral_constant<int, HWBRJ_JSW>;
     // the survivors of (q, s), batch by batch, against the table: bitmap (BM) or hash table
     auto probe_survivors = [&](bool BM) {
+        probe_begin();
         for (uint32_t d0 = i0; d0 < i1; d0 += kJoinDesc) {
             const uint32_t nd = min(kJoinDesc, i1 - d0);
             __syncthreads();  // previous descriptors consumed
@@ -1624,6 +1632,7 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
             if (BM) walk(SR{}, SW{}, P.surv, dcnt, dbase, 0, nd, [&](uint32_t x) { cnt += (tab[x >> 5] >> (x & 31u)) & 1u; });
             else walk(SR{}, SW{}, P.surv, dcnt, dbase, 0, nd, [&](uint32_t x) { cnt += join_count(tab, x); });
         }
+        probe_end();
     };
     // R run descriptors of a batch
     auto load_r = [&](uint32_t d0, uint32_t nd) {
@@ -1720,6 +1729,7 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
         __syncthreads();
         hashed = dupflag != 0;  // uniform
         if (!hashed) {
+            probe_begin();
             auto test = [&](uint32_t x) { cnt += (tab[x >> 5] >> (x & 31u)) & 1u; };
 #pragma unroll
             for (int r = 0; r < FS; r++) {
@@ -1734,6 +1744,7 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
 #ifndef HWBRJ_ABL_JNOS
             walk(SR{}, SW{}, P.surv, dcnt, dbase, (uint32_t) (kJoinWaves * FS), nSd, test);
 #endif
+            probe_end();
             done = true;
         }
     }
@@ -1791,14 +1802,23 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
     if (tid == 0) {
         uint64_t t = 0;
         for (int w = 0; w < kJoinWaves; w++) t += wsum[w];
-        if (t) atomicAdd((unsigned long long*) &P.jsum[(blockIdx.x % kJoinSumSlots) * kJoinSumStride],
-                         (unsigned long long) t);
+        uint64_t* slot = &P.jsum[(blockIdx.x % kJoinSumSlots) * kJoinSumStride];
+        if (t) atomicAdd((unsigned long long*) slot, (unsigned long long) t);
+        atomicAdd((unsigned long long*) (slot + 1), (unsigned long long) t_probe);
+        atomicAdd((unsigned long long*) (slot + 2), (unsigned long long) (wall_clock64() - t_start));
     }
 }
 
+// result[0] += matches; result[3], result[4] += probe / total ticks of the join workgroups
 __global__ __launch_bounds__(64) void k_join_sum(const uint64_t* __restrict__ jsum, uint64_t* result) {
-    const uint64_t v = wave_sum_u64(jsum[threadIdx.x * kJoinSumStride]);
-    if (threadIdx.x == 0 && v) atomicAdd((unsigned long long*) result, (unsigned long long) v);
+    const uint64_t v  = wave_sum_u64(jsum[threadIdx.x * kJoinSumStride]);
+    const uint64_t tp = wave_sum_u64(jsum[threadIdx.x * kJoinSumStride + 1]);
+    const uint64_t tt = wave_sum_u64(jsum[threadIdx.x * kJoinSumStride + 2]);
+    if (threadIdx.x == 0) {
+        if (v) atomicAdd((unsigned long long*) result, (unsigned long long) v);
+        atomicAdd((unsigned long long*) (result + 3), (unsigned long long) tp);
+        atomicAdd((unsigned long long*) (result + 4), (unsigned long long) tt);
+    }
 }
 
 // ============================================== K11: export the filter in reference layout

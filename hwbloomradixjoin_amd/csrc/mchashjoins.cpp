@@ -5,6 +5,7 @@
 //   -b sectorized    selects this build's SECTORIZED filter (the reference silently runs BASIC);
 //   -a               PRO, PRH, PRHO and RJ all run the MI355X partitioned join (their CPU join
 //                    functions differ, their counts do not); NPO / NPO_st print an error;
+//   --gpus=G         S range-sharded into G shards over the visible devices (R replicated);
 //   -z / --non-unique / --full-range relations are the reference's exactly (restated glibc
 //   rand() after srand(-x / -y), hwbrj_gen.cpp); the default PK/FK relations have the reference's
 //   key multiset in a seeded (-x / -y) Feistel order instead of the time-seeded Knuth shuffle
@@ -61,7 +62,7 @@ static void print_help(const char* prog) {
         "       -k --bloom-hashes=<k>     number of bits set per tuple                  \n"
         "       -m --bloom-size=<m>       number of filter entries in bits              \n"
         "       -B --bloom-block-size=<B> number of bits per block (B = 2^x)            \n"
-        "       --gpus=<G>                MI355X devices (S range-sharded) [1]          \n"
+        "       --gpus=<G>                S shards over the MI355X devices [1]          \n"
         "        -h --help         Show this message                                    \n"
         "        --version         Show version                                         \n");
 }
@@ -169,8 +170,9 @@ int main(int argc, char** argv) {
         }
     }
     if (P.bloom) assert_args(&P.bf);  // src/main.c:730
-    if (P.gpus != 1) {
-        printf("[ERROR] --gpus=%d: the CLI drives one device; use bench.py for N>1\n", P.gpus);
+    // --gpus=G: S range-sharded over G shards (shard g on device g mod #devices), R replicated
+    if (hwbrj_set_gpus(P.gpus) != 0) {
+        printf("[ERROR] --gpus=%d: %s\n", P.gpus, hwbrj_last_error());
         exit(EXIT_FAILURE);
     }
     if (P.nthreads == 0) P.nthreads = 1;
@@ -193,7 +195,7 @@ int main(int argc, char** argv) {
         }
     };
     fprintf(stdout, "[INFO ] %s relation R with size = %.3lf MiB, #tuples = %llu : ",
-            P.loadS ? "Loading" : "Creating", 8.0 * P.r_size / 1024.0 / 1024.0,
+            P.loadR ? "Loading" : "Creating", 8.0 * P.r_size / 1024.0 / 1024.0,
             (unsigned long long) P.r_size);
     fflush(stdout);
     uint64_t threshold = 0;

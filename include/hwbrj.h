@@ -110,6 +110,8 @@ typedef struct hwbrj_stats_t {
     double   ms_probe;      /* filter probe + survivor compaction */
     double   ms_surv;       /* survivor sub-partitioning: fused into the probe (k_probe), ~0 */
     double   ms_join;
+    double   ms_join_probe; /* the survivor-probing share of ms_join (k_join's probe sections),
+                               printed as PROBE-TIME-USECS */
 } hwbrj_stats_t;
 
 /* Join device-resident tuple arrays (tuple_t layout). args == NULL runs PRO (no filter).
@@ -135,6 +137,12 @@ int hwbrj_join_materialize_device(const tuple_t * d_R, uint64_t nR, const tuple_
 /* Host BPRO/PRO (and the PRH/PRHO/RJ entries) fill result_t.resultlist with the reference's
  * chained result buffers (src/tuple_buffer.h) when on (default: on iff HWBRJ_MATERIALIZE is set). */
 void hwbrj_set_materialize(int on);
+/* Host BPRO/PRO (and the PRH/PRHO/BRJ/RJ entries) range-shard S into `gpus` shards, shard g on
+ * visible device g mod hwbrj_device_count(), R replicated (the reference's per-thread chunking of S,
+ * src/parallel_radix_join_bloom.c:1646-1670, one host thread per device); counts are summed.
+ * 0 (default) takes HWBRJ_GPUS from the environment, else 1. More shards than devices run one after
+ * the other on each device (a G-GPU rehearsal on fewer GPUs). Returns 0, or 2 for gpus < 0. */
+int  hwbrj_set_gpus(int gpus);
 
 /* Fill d_out / out with the reference generator's key multiset (src/generator.c:304-415 with
  * `nthreads` generator threads) in a seeded permuted order; payload = row index. */
