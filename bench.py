@@ -119,13 +119,16 @@ def main():
     if dist:
         dist.all_reduce(counts)
     filtered, matches = (int(x) for x in counts.tolist())
+    # warmup on the stream the timed joins use (its first launches set up its hardware queue)
+    stream = torch.cuda.Stream()
     for _ in range(a.warmup):
-        hw.join_device(dR, dS, args)
+        hw.join_device_async(dR, dS, args, stream=stream)
+    if a.warmup:
+        hw.join_wait()
 
     # Timed region: K full joins enqueued back to back on one stream (hwbrj_join_device_async: no
     # host round trip between them), bracketed by barrier + synchronize; HIP events on that same
     # stream give the device time of the K joins (the roofline's launch duration).
-    stream = torch.cuda.Stream()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if dist:
         dist.barrier()

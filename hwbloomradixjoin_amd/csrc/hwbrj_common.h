@@ -95,8 +95,11 @@ enum Mode : int {
 };
 
 enum Format : int {
-    FMT_CODE   = 0,  // element word = code = crc32c(42, key) (MODE_SLICE_BASIC: the key)
+    FMT_CODE   = 0,  // element word = code = crc32c(42, key) (MODE_SLICE_BASIC: bmix(key))
     FMT_PACKED = 1,  // blocked, log2B <= log2F: (code >> log2F) | (first bit-in-block << (32 - log2F))
+    FMT_C22    = 2,  // S side, blocked, log2F = 10: the 22-bit code >> 10 alone, 32 elements packed
+                     // into a 22-dword (88-byte) chunk; the probe recomputes the bit-in-block from
+                     // the key (inverse CRC + CrapWow)
 };
 
 struct Geometry {
@@ -122,6 +125,7 @@ struct Geometry {
     uint32_t lbmask;       // (nblocks >> log2F) - 1: slice-local block index mask
     uint32_t log2secw;     // sectorized: log2(min(B, 64))
     uint32_t nsecmask;     // sectorized: B / secw - 1
+    int      s_format;     // element format of the S partitions (format: the R partitions)
 };
 
 // Consumer-kernel specializations (selected on the host from Geometry).
@@ -134,6 +138,8 @@ enum Kind : int {
                            // the word, the key (for the rest) is recovered only for those that pass
     KIND_BASIC_KK    = 5,  // basic, k >= 2: the first bit from the LDS slice, bits 2..k of the
                            // candidates from the global bitmap (slices = its transpose)
+    KIND_BLOCK_Z1    = 6,  // blocked/sectorized, k = 1, FMT_C22 S words (key recovered per word)
+    KIND_BLOCK_ZK    = 7,  // blocked/sectorized, k >= 2, FMT_C22 S words
 };
 
 constexpr uint32_t kMaxLog2F     = 10;

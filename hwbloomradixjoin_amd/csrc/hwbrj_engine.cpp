@@ -182,6 +182,11 @@ bool plan_geometry(const bloom_filter_args_t* a, uint64_t nR, Geometry* g, std::
             g->seg_words  = std::max<uint32_t>(4, g->seg_bits / 32);
         }
         if (g->mode == MODE_SLICE_BLOCK && ilog2u(B) <= g->log2F) g->format = FMT_PACKED;
+        // S partitions: FMT_C22 (22-bit words in 88-byte chunks) is opt-in (HWBRJ_DEV_C22): it cuts
+        // the S traffic by 2.6 GB per join, but the probe's per-word key recovery costs more than
+        // that saves
+        g->s_format = g->format;
+        if (g->mode == MODE_SLICE_BLOCK && g->log2F == 10 && getenv("HWBRJ_DEV_C22")) g->s_format = FMT_C22;
         if (g->mode == MODE_SLICE_BLOCK || g->mode == MODE_SLICE_BASIC) g->log2seg = ilog2u(g->seg_bits);
         if (a->variant != BASIC) {
             g->log2B    = ilog2u(B);
@@ -288,7 +293,10 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     const uint32_t nseg       = slice_mode ? g.nseg : 1;
     const uint32_t CH         = probe_chunks_per_item();  // chunks per probe item
     const size_t   sc_lds     = scatter_lds_bytes(g.log2F);
-    const uint32_t G          = (uint32_t) cus_ * (uint32_t) std::max<size_t>(1, std::min<size_t>(2, 163840 / sc_lds));
+    uint32_t       sc_wpc     = (uint32_t) std::max<size_t>(1, std::min<size_t>(2, 163840 / sc_lds));
+    if (const char* e = getenv("HWBRJ_DEV_SCWPC"))  // dev-only: scatter workgroups per CU
+        sc_wpc = std::max(1u, std::min(sc_wpc, (uint32_t) atoi(e)));
+    const uint32_t G          = (uint32_t) cus_ * sc_wpc;
     // basic k >= 2: the S-side buffers first partition the R keys' k * |R| bit positions
     const bool     basic_kk = g.mode == MODE_SLICE_BASIC && g.k > 1;
     const uint64_t nRk      = basic_kk ? (uint64_t) g.k * nR : 0;
@@ -542,7 +550,7 @@ int Engine::wait(hwbrj_stats_t* st) {
         st->filtered       = pending_args_ ? filtered : pending_nS_;
         st->matches        = (int64_t) matches;
         st->mode           = g.mode;
-        st->format         = g.format;
+        st->format         = g.s_format;
         st->partitions     = F;
         st->subparts       = NSUB;
         st->slice_segments = nseg;

@@ -98,7 +98,7 @@ void   launch_bitpos(const uint2* R, uint64_t n, const Geometry& g, uint32_t* ou
 void   launch_slice_fill(const uint32_t* pool, const uint32_t* list, const uint32_t* list_start,
                          const Geometry& g, uint32_t* slices, hipStream_t st);
 size_t scatter_lds_bytes(uint32_t log2F);
-enum { SIDE_R = 0, SIDE_S = 1 };  // which relation a scatter partitions (kernel name only)
+enum { SIDE_R = 0, SIDE_S = 1 };  // which relation a scatter partitions (kernel name; S uses g.s_format)
 void   launch_scatter(const ScatterParams& p, int src, int side, uint32_t grid, hipStream_t st);
 // k_plan: per-(wg, q) list offsets + per-partition chunk / element totals (colc, cole);
 // k_list_fill: scans the totals into list / element / item starts [F + 1] and fills the lists.
