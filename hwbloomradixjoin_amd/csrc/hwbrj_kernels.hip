@@ -1389,17 +1389,18 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
                     }
                     wv[i] = slice[bb[i] >> 5];
                 }
-                // pass 1: this lane's survivor bits and the wave's survivor count
+                // pass 1: this lane's survivor bits; the wave's survivor count by one DPP sum
 #pragma unroll
                 for (int i = 0; i < NW; i++) {
                     uint32_t ok = (wv[i] >> (bb[i] & 31u)) & ((uint32_t) (i & 3) < Sc.n[i >> 2] ? 1u : 0u);
                     if (!SEG1) ok &= locate<KIND>(sweep_word(Sc, i >> 2, i & 3), g, inv, q).seg == seg ? 1u : 0u;
                     pass |= ok << i;
-                    nsv += (uint32_t) __builtin_popcountll(__builtin_amdgcn_ballot_w64(ok != 0));
                 }
-                // pass 2, only when they fit the wave's scratch (dense ranking below): compact
-                // them there. Otherwise no scratch write at all (high selectivity: the words are
-                // ranked one by one, and 12 LDS writes per thread would buy nothing)
+                nsv = __builtin_amdgcn_readlane(wave_incl_scan_dpp((uint32_t) __builtin_popcount(pass)), 63);
+                // pass 2, only when they fit the wave's scratch (dense ranking below): per slot, the
+                // wave ballot compacts the survivors there (no exec masking: the others write a
+                // shared garbage slot). Otherwise no scratch write at all (high selectivity: the
+                // words are ranked one by one, and 12 LDS writes per thread would buy nothing)
                 if (kScrCap > 0 && nsv <= kScrCap) {  // wave-uniform
                     uint32_t at0 = 0;
 #pragma unroll
