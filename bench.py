@@ -50,6 +50,9 @@ def parse():
     ap.add_argument("-B", "--bloom-block-size", type=int, default=1024)
     ap.add_argument("-n", "--nthreads", type=int, default=2, help="generator threads (multiset)")
     ap.add_argument("--scaling", choices=("strong", "weak"), default="strong")
+    ap.add_argument("--design", choices=("replicated", "partitioned"), default="replicated",
+                    help="N > 1: R replicated on every rank (no exchange), or R and the join "
+                         "partitioned over the ranks (R and survivor all-to-alls, slice all-gather)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=0,
                     help="S tuples in the CPU baseline run (0: the full |S|, the same workload)")
@@ -103,14 +106,23 @@ def main():
         lo, hi = 0, nS_total
         total_units = nS_total * world
     nS = hi - lo
-    dR = torch.empty((nR, 2), dtype=torch.int32, device="cuda")
+    if a.design == "partitioned":
+        if a.scaling != "strong":
+            raise SystemExit("--design partitioned shards R and S: strong scaling only")
+        rlo, rhi = hw.shard_range(nR, rank, world)  # this rank's R rows
+    else:
+        rlo, rhi = 0, nR
+    dR = torch.empty((rhi - rlo, 2), dtype=torch.int32, device="cuda")
     dS = torch.empty((nS, 2), dtype=torch.int32, device="cuda")
-    hw.generate_device(dR, a.nthreads, nR, nR, 1.0, 12345)  # src/main.c:410-431 (-x 12345)
+    hw.generate_device_range(dR, nR, rlo, a.nthreads, nR, nR, 1.0, 12345)  # src/main.c:410-431 (-x 12345)
     hw.generate_device_range(dS, nS_total, lo, a.nthreads, 2**31 - 1, nR, a.s_sel,
                              54321 + (rank if a.scaling == "weak" else 0))  # :443-466 (-y 54321)
     torch.cuda.synchronize()
     args = hw.BloomFilterArgs.from_flag(a.bloom_filter, a.bloom_size, a.bloom_hashes,
                                         a.bloom_block_size)
+
+    if a.design == "partitioned":
+        return run_partitioned(a, hw, torch, dist, rank, world, local, dR, dS, args, shared)
 
     # one untimed parity run (counts reduced over ranks)
     st = hw.join_device(dR, dS, args)
@@ -229,6 +241,76 @@ def main():
         "phase_ms": {k[3:]: round(v, 4) for k, v in mean.items()},
         "published_ref": {"value": 3.98e8, "config": "blocked B=512 k=1 m=2^30, 2x Xeon Gold 6226 "
                           "48 threads (thesis data, BASELINE.md)"},
+    }
+    print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+def run_partitioned(a, hw, torch, dist, rank, world, local, dR, dS, args, shared):
+    """--design partitioned: every step is one hwbrj_join_partitioned on every rank (R and S range
+    shards; R chunks and survivors exchanged, slices all-gathered; the exchanges are synchronous,
+    so a step is timed by wall clock between barriers + synchronize)."""
+    from hwbloomradixjoin_amd import pjoin
+    nR, nS_total = a.r_size, a.s_size
+    x = pjoin.TorchExchange(torch.device("cuda", local))
+    cdev = "cpu" if shared else "cuda"
+    st = pjoin.join_partitioned(dR, dS, nR, args, x)
+    counts = torch.tensor([st.filtered, st.matches], dtype=torch.int64, device=cdev)
+    if dist:
+        dist.all_reduce(counts)
+    filtered, matches = (int(v) for v in counts.tolist())
+    for _ in range(a.warmup):
+        pjoin.join_partitioned(dR, dS, nR, args, x)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    sums = {}
+    for _ in range(a.steps):
+        st = pjoin.join_partitioned(dR, dS, nR, args, x)
+        for f in ("ms_total", "ms_r_scatter", "ms_r_index", "ms_build", "ms_s_scatter", "ms_surv",
+                  "ms_join"):
+            sums[f] = sums.get(f, 0.0) + getattr(st, f)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    if rank != 0:
+        if dist:
+            dist.destroy_process_group()
+        return
+    K = max(a.steps, 1)
+    ms = elapsed / K * 1e3
+    alg_bytes = 8.0 * (nR + nS_total)
+    achieved = alg_bytes / (ms * 1e-3) / 1e9
+    key = (nR, nS_total, a.s_sel, a.bloom_filter, a.bloom_size, a.bloom_hashes, a.bloom_block_size)
+    gold = GOLDEN.get(key)
+    out = {
+        "metric": METRIC, "value": round(nS_total * a.steps / elapsed, 1), "unit": "probe-tuples/s",
+        "n_gpus": world, "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms, 4),
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "int32",
+        "data": "synthetic: reference generator key multiset, seeded permutation, in HBM",
+        "config": {"workload": f"PRO + -b {a.bloom_filter}, |R|={nR} |S|={nS_total} q={a.s_sel}, "
+                               f"m={a.bloom_size} k={a.bloom_hashes} B={a.bloom_block_size}",
+                   "r_size": nR, "s_size": nS_total, "selectivity": a.s_sel,
+                   "bloom": a.bloom_filter, "m": a.bloom_size, "k": a.bloom_hashes,
+                   "B": a.bloom_block_size,
+                   "parallelism": f"R and S range-sharded x{world}, partitions owned by ranks "
+                                  "(R + survivor all-to-all, slice all-gather)"},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS * world,
+                     "unit": "GB/s", "frac": round(achieved / (HBM_PEAK_GBS * world), 4),
+                     "traffic": None, "algorithmic_bytes": alg_bytes,
+                     "launch": "one partitioned join (kernels and exchanges, wall clock)",
+                     "launch_ms": round(ms, 4)},
+        "cpu_baseline": None,
+        "parity": {"filtered": filtered, "matches": matches, "golden": list(gold) if gold else None,
+                   "ok": (gold == (filtered, matches)) if gold else None},
+        "stage_ms_rank0": {k[3:]: round(v / K, 4) for k, v in sums.items()},
     }
     print(json.dumps(out), flush=True)
     if dist:

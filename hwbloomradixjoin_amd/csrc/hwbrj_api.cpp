@@ -64,6 +64,19 @@ int hwbrj_join_device_async(const tuple_t* d_R, uint64_t nR, const tuple_t* d_S,
     return e->run_async((const uint2*) d_R, nR, (const uint2*) d_S, nS, args, (hipStream_t) stream);
 }
 
+int hwbrj_join_partitioned(const hwbrj_exchange_t* x, int rank, int world, const tuple_t* d_R,
+                           uint64_t nR, uint64_t nR_total, const tuple_t* d_S, uint64_t nS,
+                           const bloom_filter_args_t* args, hwbrj_stats_t* stats) {
+    if (!x || !x->buffer || !x->alltoall_u64 || !x->alltoallv || !x->allgather) {
+        set_last_error("incomplete exchange (hwbrj_exchange_t)");
+        return 2;
+    }
+    Engine* e = engine_for_current_device();
+    if (!e) return 10;
+    return e->join_partitioned(x, rank, world, (const uint2*) d_R, nR, nR_total, (const uint2*) d_S, nS,
+                               args, stats);
+}
+
 int hwbrj_join_wait(hwbrj_stats_t* stats) {
     Engine* e = engine_for_current_device();
     if (!e) return 10;

@@ -253,7 +253,9 @@ void Engine::release() {
     for (DevBuf* b : {&poolR, &metaR, &usedR, &wgqcR, &wgqeR, &wgqoR, &lstartR, &estartR, &istartR,
                       &listR, &poolS, &metaS, &usedS, &wgqcS, &wgqeS, &wgqoS, &lstartS, &estartS,
                       &istartS, &listS, &slices, &bitmap, &rjoin, &rrun, &surv, &survcnt, &survoff,
-                      &dense, &small, &bpos, &colR, &colS, &mtab, &mcount, &jtask, &jparts})
+                      &dense, &small, &bpos, &colR, &colS, &mtab, &mcount, &jtask, &jparts, &pjList,
+                      &pjLstart, &pjSweep, &pjTab, &pjRegion, &pjTot, &pjSoff, &pjIbase, &pjCnt, &pjOff,
+                      &pjIstart, &pjJobs})
         b->release();
     have_filter_ = false;
 }

@@ -5,6 +5,7 @@
 #include <stdint.h>
 
 #include <string>
+#include <vector>
 
 #include "../../include/hwbrj.h"
 #include "hwbrj_common.h"
@@ -42,6 +43,10 @@ class Engine {
     int  generate(uint2* d_out, uint64_t n, uint64_t offset, uint64_t count, uint32_t nthreads,
                   uint64_t maxid, uint64_t threshold, double selectivity, uint64_t seed,
                   hipStream_t stream);
+    // The partitioned multi-GPU join of rank `rank` (include/hwbrj.h hwbrj_join_partitioned).
+    int  join_partitioned(const hwbrj_exchange_t* x, int rank, int world, const uint2* dR,
+                          uint64_t nR, uint64_t nR_total, const uint2* dS, uint64_t nS,
+                          const bloom_filter_args_t* args, hwbrj_stats_t* st);
     void release();
     int  device() const { return device_; }
 
@@ -70,6 +75,8 @@ class Engine {
     DevBuf colR, colS;  // per-partition totals from k_plan: u64 elements [F], then u32 chunks [F]
     DevBuf mtab, mcount;  // materialization: R table, pair counter
     DevBuf jtask, jparts;  // join task table; parts per job (+ the task count)
+    // partitioned join: owned partitions' lists, tables and received survivor descriptors
+    DevBuf pjList, pjLstart, pjSweep, pjTab, pjRegion, pjTot, pjSoff, pjIbase, pjCnt, pjOff, pjIstart, pjJobs;
 };
 
 Engine* engine_for_current_device();

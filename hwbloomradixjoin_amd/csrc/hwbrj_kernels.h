@@ -39,6 +39,7 @@ struct BuildParams {
     uint32_t*        out_codes;   // [sweeps][kBSlot]: each sweep's R codes sorted by sub
     uint32_t*        run_cnt;     // [sweeps][NSUB] codes of each (sweep, sub) run
     uint32_t*        run_off;     // [sweeps][NSUB] run offset inside the sweep's slot
+    uint32_t         q_base;      // partition of workgroup 0 (list/sweep tables indexed from it)
 };
 
 struct ProbeParams {
@@ -81,6 +82,8 @@ struct JoinParams {
     uint32_t*       nextra;       // parts requested beyond part 0 (zeroed before the join)
     uint32_t        split_surv;   // survivors per join part (0: the default, kJoinTaskSurv)
     uint64_t*       dbg;          // dev-only: per-workgroup phase cycles (HWBRJ_DBG), or nullptr
+    const uint64_t* item_base;    // [items] survivor region of each item (partitioned multi-GPU
+                                  // join: received runs), or nullptr (k_probe's item regions)
 };
 
 void   launch_gen(uint2* out, uint64_t offset, uint64_t count, const GenPlan* d_plan, const Perm& perm,
@@ -128,6 +131,14 @@ void   launch_mat_probe(const uint2* S, uint64_t n, const uint2* R, const unsign
                         uint64_t mask, uint2* out, uint64_t cap, unsigned long long* count,
                         const Geometry& g, const uint32_t* slices, const uint32_t* bm,
                         const CrcTables* tabs, hipStream_t st);
+// partitioned multi-GPU join (K13): chunks in list order + rebased entries; receiver lists;
+// survivor runs of items packed per destination
+void   launch_pj_gather(const uint32_t* pool, const uint32_t* list, uint32_t n, void* out, uint32_t* ent,
+                        hipStream_t st);
+void   launch_pj_relist(const uint32_t* rent, const int64_t* tab, uint32_t pairs, uint32_t* list,
+                        hipStream_t st);
+void   launch_pj_surv_pack(const uint32_t* surv, const uint64_t* region, const uint32_t* tot,
+                           const uint64_t* soff, uint32_t n, uint32_t* out, hipStream_t st);
 void   launch_export(const uint32_t* slices, const Geometry& g, uint32_t* out, uint64_t nwords,
                      hipStream_t st);
 

@@ -1105,13 +1105,14 @@ __global__ __launch_bounds__(1024) void k_build(BuildParams P) {
     uint32_t*       inv    = slice + segw;
     uint32_t*       stage  = inv + 128;       // kBSlot
     uint32_t*       cnt    = stage + kBSlot;  // 2 x 64: ranks of a sweep by sub (by sweep parity)
-    const uint32_t  q      = blockIdx.x;
+    const uint32_t  ql     = blockIdx.x;       // list / sweep tables are indexed by ql
+    const uint32_t  q      = P.q_base + ql;    // the partition (codes, slices)
     const int       tid    = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     load_tab(inv, &P.tabs->inv[0][0]);
     if (tid < 128) cnt[tid] = 0;
     uint32_t nsw = 0;  // sweeps sorted so far (selects the counter buffer)
-    const uint32_t l0 = P.list_start[q], l1 = P.list_start[q + 1];
-    const uint32_t sw0  = P.sweep_start[q];
+    const uint32_t l0 = P.list_start[ql], l1 = P.list_start[ql + 1];
+    const uint32_t sw0  = P.sweep_start[ql];
     const uint32_t nseg = slices ? g.nseg : 1;
     constexpr uint32_t GRP = kBSweep * kBPQ;
     for (uint32_t seg = 0; seg < nseg; seg++) {
@@ -1683,7 +1684,7 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
     const uint32_t i0  = qi0 + (uint32_t) ((uint64_t) (qi1 - qi0) * part / np);
     const uint32_t i1  = qi0 + (uint32_t) ((uint64_t) (qi1 - qi0) * (part + 1) / np);
     if (w1 == w0 || i1 == i0) return;
-    const uint32_t lq0 = P.list_start[q];
+    const uint32_t lq0 = P.item_base ? 0u : P.list_start[q];
     const uint32_t npc = (qi1 - qi0) / P.nseg;  // probe pieces of q
     const uint32_t sh  = P.hash_shift;
     const int      tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -1761,7 +1762,8 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
                 const uint32_t seg   = local / npc;
                 const uint32_t piece = local - seg * npc;
                 dcnt[tid]  = P.surv_cnt[(uint64_t) it * NSUB + s];
-                dbase[tid] = (uint64_t) seg * P.surv_seg_stride + (uint64_t) (lq0 + piece * P.CH) * 32 +
+                dbase[tid] = (P.item_base ? P.item_base[it]  // (the partitioned multi-GPU join)
+                                          : (uint64_t) seg * P.surv_seg_stride + (uint64_t) (lq0 + piece * P.CH) * 32) +
                              P.surv_off[(uint64_t) it * NSUB + s];
             }
             __syncthreads();
@@ -1812,7 +1814,8 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
             const uint32_t seg   = local / npc;
             const uint32_t piece = local - seg * npc;
             dcnt[tid]  = P.surv_cnt[(uint64_t) it * NSUB + s];
-            dbase[tid] = (uint64_t) seg * P.surv_seg_stride + (uint64_t) (lq0 + piece * P.CH) * 32 +
+            dbase[tid] = (P.item_base ? P.item_base[it]  // (the partitioned multi-GPU join)
+                                      : (uint64_t) seg * P.surv_seg_stride + (uint64_t) (lq0 + piece * P.CH) * 32) +
                          P.surv_off[(uint64_t) it * NSUB + s];
         }
         __syncthreads();
@@ -2185,6 +2188,74 @@ void launch_mat_probe(const uint2* S, uint64_t n, const uint2* R, const unsigned
                       const Geometry& g, const uint32_t* slices, const uint32_t* bm,
                       const CrcTables* tabs, hipStream_t st) {
     k_mat_probe<<<2048, 256, 0, st>>>(S, n, R, tab, mask, out, cap, count, g, slices, bm, tabs);
+}
+
+// ================================= K13: partitioned multi-GPU join (R and survivors exchanged)
+// Rank r of G owns partitions [r F / G, (r + 1) F / G). Its R shard is scattered locally; every
+// partition's chunks go to the owner (k_pj_gather: all chunks in list order, so each destination's
+// chunks are one contiguous block), the owner rebuilds its partitions' lists from what every
+// source sent (k_pj_relist) and builds their slices and join runs; the slices are all-gathered.
+// The S shard is scattered and probed locally against the full filter, and each item's survivors
+// go to the owner of its partition (k_pj_surv_pack), which joins them (k_join with item_base).
+
+// out chunk p (8 lanes of 16 B) = pool chunk of list entry p; ent[p] = p | the entry's count bits
+__global__ __launch_bounds__(256) void k_pj_gather(const uint32_t* __restrict__ pool,
+                                                   const uint32_t* __restrict__ list, uint32_t n,
+                                                   uint4* __restrict__ out, uint32_t* __restrict__ ent) {
+    const uint64_t stride = (uint64_t) gridDim.x * blockDim.x;
+    for (uint64_t t = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x; t < (uint64_t) n * 8; t += stride) {
+        const uint32_t p = (uint32_t) (t >> 3), l8 = (uint32_t) (t & 7);
+        const uint32_t e = list[p];
+        out[t]           = ((const uint4*) pool)[(uint64_t) (e & kListIdMask) * 8 + l8];
+        if (l8 == 0) ent[p] = p | (e & ~kListIdMask);
+    }
+}
+
+// One block per (source, owned partition) pair: tab[4 pair + {0, 1, 2, 3}] = first received
+// entry, count, destination list position, chunk id adjustment (source block base in the received
+// chunks minus the source's id of its block's first chunk).
+__global__ __launch_bounds__(256) void k_pj_relist(const uint32_t* __restrict__ rent,
+                                                   const int64_t* __restrict__ tab,
+                                                   uint32_t* __restrict__ list) {
+    const int64_t* t = tab + 4 * (uint64_t) blockIdx.x;
+    const uint64_t so = (uint64_t) t[0], n = (uint64_t) t[1], dl = (uint64_t) t[2];
+    const int64_t  adj = t[3];
+    for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) {
+        const uint32_t e = rent[so + i];
+        list[dl + i]     = (uint32_t) ((int64_t) (e & kListIdMask) + adj) | (e & ~kListIdMask);
+    }
+}
+
+// One wave per item: its `tot` survivor words (contiguous from the item region's start, grouped
+// by sub) to out + soff[it].
+__global__ __launch_bounds__(256) void k_pj_surv_pack(const uint32_t* __restrict__ surv,
+                                                      const uint64_t* __restrict__ region,
+                                                      const uint32_t* __restrict__ tot,
+                                                      const uint64_t* __restrict__ soff, uint32_t n,
+                                                      uint32_t* __restrict__ out) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wv   = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint32_t nw   = (gridDim.x * blockDim.x) >> 6;
+    for (uint32_t it = wv; it < n; it += nw) {
+        const uint64_t src = region[it], dst = soff[it];
+        const uint32_t c   = tot[it];
+        for (uint32_t i = lane; i < c; i += 64) out[dst + i] = surv[src + i];
+    }
+}
+
+void launch_pj_gather(const uint32_t* pool, const uint32_t* list, uint32_t n, void* out, uint32_t* ent,
+                      hipStream_t st) {
+    if (n) k_pj_gather<<<4096, 256, 0, st>>>(pool, list, n, (uint4*) out, ent);
+}
+
+void launch_pj_relist(const uint32_t* rent, const int64_t* tab, uint32_t pairs, uint32_t* list,
+                      hipStream_t st) {
+    if (pairs) k_pj_relist<<<pairs, 256, 0, st>>>(rent, tab, list);
+}
+
+void launch_pj_surv_pack(const uint32_t* surv, const uint64_t* region, const uint32_t* tot,
+                         const uint64_t* soff, uint32_t n, uint32_t* out, hipStream_t st) {
+    if (n) k_pj_surv_pack<<<2048, 256, 0, st>>>(surv, region, tot, soff, n, out);
 }
 
 // ===================================================================== launch wrappers

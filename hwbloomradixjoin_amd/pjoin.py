@@ -1,0 +1,153 @@
+"""The partitioned multi-GPU join (include/hwbrj.h hwbrj_join_partitioned) driven over
+torch.distributed: one process per GPU, RCCL ("nccl") over xGMI, or gloo (host copies) for
+rehearsals on fewer GPUs than ranks.
+
+SURVEY.md s8f row 3. Rank r of G owns radix partitions [r F / G, (r + 1) F / G): R chunks and
+S survivors travel to the owner (variable all-to-alls), the owners' filter slices are all-gathered
+(the filter broadcast, in 1/G pieces). The library runs every kernel and asks this module for the
+exchanges through the hwbrj_exchange_t callbacks; device buffers are torch tensors (one per slot).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _Stats, Stats, _BloomArgs, _err, _ptr, _check_rel, lib
+
+_U64P = ctypes.POINTER(ctypes.c_uint64)
+_BUFFER = ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_uint64)
+_A2A_U64 = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, _U64P, _U64P, ctypes.c_uint64)
+_A2AV = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int, _U64P, _U64P, ctypes.c_int, _U64P, _U64P)
+_AG = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_uint64)
+
+
+class _Exchange(ctypes.Structure):  # include/hwbrj.h hwbrj_exchange_t
+    _fields_ = [("ctx", ctypes.c_void_p), ("buffer", _BUFFER), ("alltoall_u64", _A2A_U64),
+                ("alltoallv", _A2AV), ("allgather", _AG)]
+
+
+class TorchExchange:
+    """hwbrj_exchange_t over torch.distributed. `group` None: the default group; with world 1 (or
+    no process group) every exchange is a local copy. gloo groups stage through host memory."""
+
+    NSLOTS = 9
+
+    def __init__(self, device, group=None):
+        import torch
+        import torch.distributed as dist
+        self.torch, self.dist, self.group = torch, dist, group
+        self.device = torch.device(device)
+        self.on = dist.is_available() and dist.is_initialized()
+        self.world = dist.get_world_size(group) if self.on else 1
+        self.rank = dist.get_rank(group) if self.on else 0
+        self.gloo = self.on and dist.get_backend(group) == "gloo"
+        self.slots = [None] * self.NSLOTS
+        self.error = None
+        self._c = _Exchange(None, _BUFFER(self._buffer), _A2A_U64(self._a2a_u64),
+                            _A2AV(self._a2av), _AG(self._allgather))
+
+    # every callback returns 0 / a pointer, or records the exception and fails (the library then
+    # returns an error code and join_partitioned raises it)
+    def _guard(self, fn, fail):
+        try:
+            return fn()
+        except Exception as e:  # noqa: BLE001 (re-raised by join_partitioned)
+            self.error = e
+            return fail
+
+    def _buffer(self, _ctx, slot, nbytes):
+        def go():
+            t = self.slots[slot]
+            if t is None or t.numel() < nbytes:
+                t = self.slots[slot] = self.torch.empty(max(int(nbytes), 16), dtype=self.torch.uint8,
+                                                        device=self.device)
+            return t.data_ptr()
+        return self._guard(go, None)
+
+    def _a2a_u64(self, _ctx, send, recv, n):
+        def go():
+            W = self.world
+            s = np.ctypeslib.as_array(send, shape=(W * n,)).astype(np.int64)
+            if W == 1:
+                np.ctypeslib.as_array(recv, shape=(n,))[:] = s
+                return 0
+            st = self.torch.from_numpy(s)
+            if not self.gloo:
+                st = st.to(self.device)
+            rt = self.torch.empty_like(st)
+            self.dist.all_to_all_single(rt, st, group=self.group)
+            np.ctypeslib.as_array(recv, shape=(W * n,))[:] = rt.cpu().numpy().astype(np.uint64)
+            return 0
+        return self._guard(go, 1)
+
+    def _a2av(self, _ctx, sslot, soff, sbytes, rslot, roff, rbytes):
+        def go():
+            W = self.world
+            so, sb = [soff[j] for j in range(W)], [sbytes[j] for j in range(W)]
+            ro, rb = [roff[j] for j in range(W)], [rbytes[j] for j in range(W)]
+            for j in range(W - 1):  # the blocks are consecutive (one all_to_all_single)
+                assert so[j] + sb[j] == so[j + 1] and ro[j] + rb[j] == ro[j + 1]
+            src = self.slots[sslot][so[0]: so[-1] + sb[-1]]
+            dst = self.slots[rslot][ro[0]: ro[-1] + rb[-1]]
+            if W == 1:
+                dst.copy_(src)
+                self.torch.cuda.synchronize(self.device)  # (the library reads it on its own stream)
+                return 0
+            if self.gloo:
+                out = self.torch.empty(dst.numel(), dtype=self.torch.uint8)
+                self.dist.all_to_all_single(out, src.cpu(), rb, sb, group=self.group)
+                dst.copy_(out)
+            else:
+                self.dist.all_to_all_single(dst, src, rb, sb, group=self.group)
+            self.torch.cuda.synchronize(self.device)
+            return 0
+        return self._guard(go, 1)
+
+    def _allgather(self, _ctx, slot, nbytes):
+        def go():
+            W, r = self.world, self.rank
+            full = self.slots[slot][: W * nbytes]
+            if W == 1:
+                return 0
+            mine = full[r * nbytes: (r + 1) * nbytes]
+            if self.gloo:
+                out = self.torch.empty(W * nbytes, dtype=self.torch.uint8)
+                self.dist.all_gather_into_tensor(out, mine.cpu().clone(), group=self.group)
+                full.copy_(out)
+            else:
+                self.dist.all_gather_into_tensor(full, mine.clone(), group=self.group)
+            self.torch.cuda.synchronize(self.device)
+            return 0
+        return self._guard(go, 1)
+
+
+def join_partitioned(R, S, nR_total: int, args=None, exchange: TorchExchange | None = None) -> Stats:
+    """This rank's part of the partitioned join of R and S (device (N, 2) int32 shards; nR_total =
+    |R| over all ranks). Stats.filtered: this rank's S survivors; Stats.matches: the matches of its
+    partitions -- both sum over ranks to the join's counts. ms_* fields are host wall times of the
+    stages (ms_r_index: R exchange, ms_surv: slice all-gather + survivor exchange)."""
+    _check_rel(R, S)
+    x = exchange or TorchExchange(R.device)
+    a = args._c() if args is not None else None
+    st = _Stats()
+    L = lib()
+    rc = L.hwbrj_join_partitioned(ctypes.byref(x._c), x.rank, x.world, _ptr(R), R.shape[0],
+                                  int(nR_total), _ptr(S), S.shape[0],
+                                  ctypes.byref(a) if a is not None else None, ctypes.byref(st))
+    if x.error is not None:
+        e, x.error = x.error, None
+        raise RuntimeError(f"hwbrj_join_partitioned: exchange failed: {e!r}") from e
+    _err(rc, "hwbrj_join_partitioned")
+    return Stats(**{n: getattr(st, n) for n, _ in _Stats._fields_})
+
+
+def _bind(L):
+    L.hwbrj_join_partitioned.restype = ctypes.c_int
+    L.hwbrj_join_partitioned.argtypes = [ctypes.POINTER(_Exchange), ctypes.c_int, ctypes.c_int,
+                                         ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
+                                         ctypes.c_void_p, ctypes.c_uint64,
+                                         ctypes.POINTER(_BloomArgs), ctypes.POINTER(_Stats)]
+
+
+_bind(lib())

@@ -144,6 +144,43 @@ void hwbrj_set_materialize(int on);
  * the other on each device (a G-GPU rehearsal on fewer GPUs). Returns 0, or 2 for gpus < 0. */
 int  hwbrj_set_gpus(int gpus);
 
+/* ---- partitioned multi-GPU join (this build) ----
+ * Rank `rank` of `world` holds an R shard and an S shard (any split, e.g. range shards). Radix
+ * partition q of the F partitions belongs to rank q / (F / world). Every rank scatters its R shard,
+ * sends each partition's chunks to the owner, which builds that partition's filter slice and join
+ * runs; the slices are all-gathered (the filter bitmap broadcast, in 1/world pieces), every rank
+ * scatters and probes its S shard against the whole filter and sends each partition's survivors
+ * to the owner, which joins them. stats->filtered: this rank's S survivors; stats->matches: the
+ * matches of its partitions (the sums over ranks are the join's counts). nR_total = |R| over all
+ * ranks (the filter geometry depends on it). Supported: blocked/sectorized filters, basic k = 1
+ * and no filter (args NULL); returns 9 otherwise. world must divide F (a power of two <= F).
+ *
+ * The transport is the caller's (RCCL through torch.distributed, gloo, peer copies). Every call is
+ * synchronous; device buffers are the caller's, named by slot (hwbrj_pj_slot_t). */
+typedef enum {
+    HWBRJ_PJ_R_SEND = 0, HWBRJ_PJ_R_SEND_ENT, HWBRJ_PJ_R_RECV, HWBRJ_PJ_R_RECV_ENT,
+    HWBRJ_PJ_SLICES, HWBRJ_PJ_S_SEND, HWBRJ_PJ_S_RECV, HWBRJ_PJ_M_SEND, HWBRJ_PJ_M_RECV,
+    HWBRJ_PJ_NSLOTS
+} hwbrj_pj_slot_t;
+
+typedef struct hwbrj_exchange_t {
+    void * ctx;
+    /* device buffer `slot` of at least `bytes` bytes (kept until the next request for the slot) */
+    void * (*buffer)(void * ctx, int slot, uint64_t bytes);
+    /* host all-to-all: send[j n .. (j + 1) n) goes to rank j, recv[j n ..) comes from rank j */
+    int (*alltoall_u64)(void * ctx, const uint64_t * send, uint64_t * recv, uint64_t n);
+    /* device all-to-all of byte blocks between slot buffers: [soff[j], soff[j] + sbytes[j]) of
+     * send_slot goes to rank j; rank j's block lands at roff[j] of recv_slot (rbytes[j] bytes) */
+    int (*alltoallv)(void * ctx, int send_slot, const uint64_t * soff, const uint64_t * sbytes,
+                     int recv_slot, const uint64_t * roff, const uint64_t * rbytes);
+    /* device all-gather in place: block j = [j bytes, (j + 1) bytes) of slot, from rank j */
+    int (*allgather)(void * ctx, int slot, uint64_t bytes);
+} hwbrj_exchange_t;
+
+int hwbrj_join_partitioned(const hwbrj_exchange_t * x, int rank, int world, const tuple_t * d_R,
+                           uint64_t nR, uint64_t nR_total, const tuple_t * d_S, uint64_t nS,
+                           const bloom_filter_args_t * args, hwbrj_stats_t * stats);
+
 /* Fill d_out / out with the reference generator's key multiset (src/generator.c:304-415 with
  * `nthreads` generator threads) in a seeded permuted order; payload = row index. */
 int hwbrj_generate_device(tuple_t * d_out, uint64_t n, uint32_t nthreads, uint64_t maxid,

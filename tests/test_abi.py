@@ -19,7 +19,8 @@ INT_MAX = 2**31 - 1
 def declared_functions():
     src = open(os.path.join(ROOT, "include", "hwbrj.h")).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    names = re.findall(r"\b([A-Za-z_][A-Za-z0-9_]*)\s*\([^;{]*\)\s*;", src)
+    # (function-pointer members, "int (*f)(...);", are not exported functions)
+    names = re.findall(r"\b([A-Za-z_][A-Za-z0-9_]*)\s*\((?!\s*\*)[^;{]*\)\s*;", src)
     return sorted(set(n for n in names if n not in ("if", "while", "for", "sizeof")))
 
 

@@ -218,3 +218,80 @@ def test_basic_kk_materialize_and_skew(hw, cuda, orc, monkeypatch):
     assert np.array_equal(key(p), key(want))
     monkeypatch.setenv("HWBRJ_DEV_JOIN_SPLIT", "700")
     oracle_check(hw, cuda, orc, R, S, a)
+
+
+# ------------------------------------------------------- partitioned multi-GPU join (s8f row 3)
+PJ_ARGS = [None, ("blocked", 1 << 24, 1, 1024), ("blocked", 1 << 22, 3, 512), ("basic", 1 << 20, 1, 0),
+           ("sectorized", 1 << 22, 4, 512), ("blocked", 1 << 31, 2, 512)]
+
+
+@pytest.mark.parametrize("a", PJ_ARGS, ids=str)
+def test_partitioned_world1_vs_oracle(hw, cuda, orc, a):
+    """hwbrj_join_partitioned on one rank (every exchange a local copy): the R chunks go through
+    the gather/relist path, the survivors through the pack/item-table path and k_join's item_base
+    descriptors; counts equal the oracle's."""
+    from hwbloomradixjoin_amd import pjoin
+    args = None if a is None else hw.BloomFilterArgs.from_flag(a[0], a[1], a[2], a[3] or 1024)
+    rng = np.random.default_rng(21)
+    for nR, nS in [(0, 1000), (1000, 0), (7, 33), (100003, 400009), (1000000, 4000000)]:
+        Rk = rng.permutation(nR).astype(np.int64) + 1
+        Sk = rng.integers(0, 2 * max(nR, 1) + 2, size=nS)
+        R, S = rel(Rk), rel(Sk)
+        st = pjoin.join_partitioned(to_dev(cuda, R), to_dev(cuda, S), nR, args)
+        if args is None:
+            res, filt, _ = orc.bpro(R, S, 8, 0, 0, 0, 0, use_bloom=False)
+        else:
+            res, filt, _ = orc.bpro(R, S, 8, args.variant, args.m, args.k, args.B)
+        assert (st.filtered, st.matches) == (filt, res), (a, nR, nS, st)
+
+
+def test_partitioned_world1_skew_and_dups(hw, cuda, orc, gen3, monkeypatch):
+    """Duplicate R keys (hash-path join jobs) and a Zipf S with the skew split forced."""
+    from hwbloomradixjoin_amd import pjoin
+    monkeypatch.setenv("HWBRJ_DEV_JOIN_SPLIT", "700")
+    for mode in ("nonunique", "zipf"):
+        R, S = gen3[1][mode]
+        S = S[:4000000]
+        args = hw.BloomFilterArgs(hw.BLOCKED, 1 << 24, 1, 1024)
+        st = pjoin.join_partitioned(to_dev(cuda, R), to_dev(cuda, S), R.shape[0], args)
+        res, filt, _ = orc.bpro(R, S, 8, 1, 1 << 24, 1, 1024, True)
+        assert (st.filtered, st.matches) == (filt, res)
+
+
+@pytest.fixture(scope="module")
+def gen3(hw):
+    g = GOLD["F3_generators"]
+    kw = dict(r_seed=g["r_seed"], s_seed=g["s_seed"], host_threads=8)
+    return g, {"nonunique": hw.reference_relations(g["r"], g["s"], g["nonunique"]["q"], non_unique=True, **kw),
+               "zipf": hw.reference_relations(g["r"], g["s"], skew=g["zipf"]["z"], **kw)}
+
+
+@pytest.mark.parametrize("world,flags", [(2, []), (4, []), (2, ["-b", "sectorized", "-k", "2"]),
+                                         (4, ["-b", "basic"]), (2, ["-b", "no"])], ids=str)
+def test_bench_partitioned_ranks(hw, orc, world, flags):
+    """bench.py --design partitioned end to end under torch.distributed.run: R and S range shards,
+    R chunk and survivor all-to-alls, slice all-gather, rehearsed with `world` ranks on one GPU
+    (HWBRJ_BENCH_SHARED_GPU=1: gloo through host memory). The reduced counts are the golden."""
+    import socket
+    g = GOLD["F3_grid"]
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    root = os.path.dirname(HERE)
+    env = dict(os.environ, HWBRJ_BENCH_SHARED_GPU="1", HWBRJ_PJ_CHECK="1")
+    out = subprocess.run(["python", "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
+                          "--master-addr", "127.0.0.1", "--master-port", str(port),
+                          os.path.join(root, "bench.py"), "--gpus", str(world), "--steps", "2", "--warmup", "1",
+                          "--design", "partitioned", "-r", str(g["r"]), "-s", str(g["s"]), "-m", str(g["m"])]
+                         + flags, capture_output=True, text=True, timeout=300, env=env, cwd=root)
+    assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-3000:]
+    line = json.loads([x for x in out.stdout.splitlines() if x.startswith("{")][-1])
+    assert line["n_gpus"] == world
+    want = {(): g["rows"]["1024"][0], ("-b", "sectorized", "-k", "2"): None, ("-b", "basic"): g["rows"]["basic"][0],
+            ("-b", "no"): g["s"]}[tuple(flags)]
+    if want is None:  # sectorized (no reference count): the oracle on bench.py's relations
+        R = hw.generate_host(g["r"], 2, g["r"], g["r"], 1.0, 12345)
+        S = hw.generate_host(g["s"], 2, INT_MAX, g["r"], 0.01, 54321)
+        want = orc.bpro(R, S, 8, hw.SECTORIZED, g["m"], 2, 1024)[1]
+    assert (line["parity"]["filtered"], line["parity"]["matches"]) == (want, g["results"])
