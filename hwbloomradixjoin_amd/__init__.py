@@ -95,6 +95,10 @@ def lib() -> ctypes.CDLL:
         L.hwbrj_join_device_async.restype = ctypes.c_int
         L.hwbrj_join_device_async.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
                                               ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]
+        L.hwbrj_join_device_algo.restype = ctypes.c_int
+        L.hwbrj_join_device_algo.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                             ctypes.c_uint64, ctypes.POINTER(_BloomArgs),
+                                             ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(_Stats)]
         L.hwbrj_join_wait.restype = ctypes.c_int
         L.hwbrj_join_wait.argtypes = [ctypes.c_void_p]
         L.hwbrj_join_device.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
@@ -385,16 +389,23 @@ def join_wait() -> Stats:
     return Stats(**{n: getattr(st, n) for n, _ in _Stats._fields_})
 
 
-def join_device(R, S, args: Optional[BloomFilterArgs] = None, stream=None) -> Stats:
+ALGO_PRO, ALGO_PRH, ALGO_PRHO = 0, 1, 2  # include/hwbrj.h HWBRJ_ALGO_* (per-partition join)
+
+
+def join_device(R, S, args: Optional[BloomFilterArgs] = None, stream=None,
+                algorithm: int = ALGO_PRO) -> Stats:
     """Join device-resident torch int32 tensors of shape (N, 2) ({key, payload}) in HBM.
-    args=None runs PRO. `stream` is a torch.cuda.Stream (default: the library's own stream)."""
+    args=None runs PRO. `stream` is a torch.cuda.Stream (default: the library's own stream).
+    algorithm: the per-partition join (ALGO_PRO bucket chaining's role, ALGO_PRH / ALGO_PRHO the
+    histogram joins of src/parallel_radix_join_bloom.c:350-555)."""
     _check_rel(R, S)
     st = _Stats()
     a = args._c() if args is not None else None
     sp = ctypes.c_void_p(stream.cuda_stream) if stream is not None else None
-    rc = lib().hwbrj_join_device(_ptr(R), R.shape[0], _ptr(S), S.shape[0],
-                                 ctypes.byref(a) if a is not None else None, sp, ctypes.byref(st))
-    _err(rc, "hwbrj_join_device")
+    rc = lib().hwbrj_join_device_algo(_ptr(R), R.shape[0], _ptr(S), S.shape[0],
+                                      ctypes.byref(a) if a is not None else None, int(algorithm),
+                                      sp, ctypes.byref(st))
+    _err(rc, "hwbrj_join_device_algo")
     return Stats(**{n: getattr(st, n) for n, _ in _Stats._fields_})
 
 

@@ -57,6 +57,14 @@ int hwbrj_join_device(const tuple_t* d_R, uint64_t nR, const tuple_t* d_S, uint6
     return e->run((const uint2*) d_R, nR, (const uint2*) d_S, nS, args, (hipStream_t) stream, stats);
 }
 
+int hwbrj_join_device_algo(const tuple_t* d_R, uint64_t nR, const tuple_t* d_S, uint64_t nS,
+                           const bloom_filter_args_t* args, int algorithm, void* stream,
+                           hwbrj_stats_t* stats) {
+    Engine* e = engine_for_current_device();
+    if (!e) return 10;
+    return e->run((const uint2*) d_R, nR, (const uint2*) d_S, nS, args, (hipStream_t) stream, stats, algorithm);
+}
+
 int hwbrj_join_device_async(const tuple_t* d_R, uint64_t nR, const tuple_t* d_S, uint64_t nS,
                             const bloom_filter_args_t* args, void* stream) {
     Engine* e = engine_for_current_device();
@@ -308,7 +316,7 @@ struct Shard {
 // once, then per shard H2D of its S rows and the join. Returns 0 or an error code.
 static int run_device_shards(int dev, int first, int step, const relation_t* relR,
                              const relation_t* relS, const bloom_filter_args_t* args,
-                             std::vector<Shard>& shards) {
+                             std::vector<Shard>& shards, int algo) {
     if (hipSetDevice(dev) != hipSuccess) {
         set_last_error("hipSetDevice failed");
         return 11;
@@ -341,15 +349,17 @@ static int run_device_shards(int dev, int first, int step, const relation_t* rel
         }
         sh.h2d_usec = h2d_r + std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - h1).count();
         h2d_r       = 0;
-        rc          = hwbrj_join_device(dR, nR, dS, n, args, nullptr, &sh.st);
+        rc          = hwbrj_join_device_algo(dR, nR, dS, n, args, algo, nullptr, &sh.st);
     }
     (void) hipFree(dR);
     (void) hipFree(dS);
     return rc;
 }
 
+// algo: the per-partition join (HWBRJ_ALGO_PRO / PRH / PRHO, the reference's join_init_run
+// JoinFunction: bucket_chaining_join / histogram_join / histogram_optimized_join)
 static result_t* run_host_join(relation_t* relR, relation_t* relS, int nthreads,
-                               bloom_filter_args_t* args, bool print_filtered = true) {
+                               bloom_filter_args_t* args, bool print_filtered = true, int algo = 0) {
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) {
         set_last_error("no MI355X device visible");
@@ -371,13 +381,13 @@ static result_t* run_host_join(relation_t* relR, relation_t* relS, int nthreads,
     std::vector<std::string> errs(nuse);
     const uint64_t c0 = __rdtsc();
     if (nuse == 1) {
-        rcs[0] = run_device_shards(cur, 0, 1, relR, relS, args, shards);
+        rcs[0] = run_device_shards(cur, 0, 1, relR, relS, args, shards, algo);
         errs[0] = hwbrj_last_error();
     } else {  // one host thread per device (the reference's nthreads workers, one per GPU)
         std::vector<std::thread> th;
         for (int d = 0; d < nuse; d++)
             th.emplace_back([&, d] {
-                rcs[d]  = run_device_shards(d, d, nuse, relR, relS, args, shards);
+                rcs[d]  = run_device_shards(d, d, nuse, relR, relS, args, shards, algo);
                 errs[d] = hwbrj_last_error();
             });
         for (auto& t : th) t.join();
@@ -424,7 +434,7 @@ static result_t* run_host_join(relation_t* relR, relation_t* relS, int nthreads,
             fatal("BPRO");
         }
         hwbrj_stats_t one;
-        if (G > 1 && hwbrj_join_device(dR, nR, dS, nS, args, nullptr, &one) != 0) fatal("BPRO");
+        if (G > 1 && hwbrj_join_device_algo(dR, nR, dS, nS, args, algo, nullptr, &one) != 0) fatal("BPRO");
         tres = materialize_to_host(dR, nR, dS, nS, args, (uint64_t) st.matches, nthreads);
         (void) hipFree(dR);
         (void) hipFree(dS);
@@ -474,24 +484,26 @@ result_t* PRO(relation_t* relR, relation_t* relS, int nthreads) {
     return run_host_join(relR, relS, nthreads, nullptr);
 }
 
-// The other entries of the reference's algorithm table (src/main.c:331-339) that run the same
-// partitioned join: BPRH / BPRHO plug a different per-partition join function into the same
-// join_init_run (src/parallel_radix_join_bloom.c:1789-1804), BRJ is its single-threaded form
-// (:1806-1930). On the MI355X the per-partition join is always k_join, so they are this operator.
+// The other entries of the reference's algorithm table (src/main.c:331-339). BPRH / BPRHO plug a
+// different per-partition join function into the same join_init_run
+// (src/parallel_radix_join_bloom.c:1789-1804): the histogram join of Kim et al. (histogram_join,
+// :350-419) and its SIMD + prefetch form (histogram_optimized_join, :441-555); here k_join runs
+// them (JoinParams::jkind 1 / 2) instead of its bitmap / hash table. BRJ is the single-threaded
+// form of BPRO (:1806-1930) with bucket chaining: the same operator on the MI355X.
 result_t* BPRH(relation_t* relR, relation_t* relS, int nthreads, bloom_filter_args_t* a) {
-    return run_host_join(relR, relS, nthreads, a);
+    return run_host_join(relR, relS, nthreads, a, true, 1);
 }
 result_t* BPRHO(relation_t* relR, relation_t* relS, int nthreads, bloom_filter_args_t* a) {
-    return run_host_join(relR, relS, nthreads, a);
+    return run_host_join(relR, relS, nthreads, a, true, 2);
 }
 result_t* BRJ(relation_t* relR, relation_t* relS, int nthreads, bloom_filter_args_t* a) {
     return run_host_join(relR, relS, nthreads, a, false);
 }
 result_t* PRH(relation_t* relR, relation_t* relS, int nthreads) {
-    return run_host_join(relR, relS, nthreads, nullptr);
+    return run_host_join(relR, relS, nthreads, nullptr, true, 1);
 }
 result_t* PRHO(relation_t* relR, relation_t* relS, int nthreads) {
-    return run_host_join(relR, relS, nthreads, nullptr);
+    return run_host_join(relR, relS, nthreads, nullptr, true, 2);
 }
 result_t* RJ(relation_t* relR, relation_t* relS, int nthreads) {
     return run_host_join(relR, relS, nthreads, nullptr);

@@ -267,18 +267,22 @@ static uint64_t region_cap(uint64_t n, uint32_t G, uint32_t F) {
 }
 
 int Engine::run(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
-                const bloom_filter_args_t* args, hipStream_t stream, hwbrj_stats_t* st) {
-    const int rc = enqueue(dR, nR, dS, nS, args, stream, getenv("HWBRJ_DBG") != nullptr);
+                const bloom_filter_args_t* args, hipStream_t stream, hwbrj_stats_t* st, int jkind) {
+    const int rc = enqueue(dR, nR, dS, nS, args, stream, getenv("HWBRJ_DBG") != nullptr, jkind);
     return rc ? rc : wait(st);
 }
 
 int Engine::run_async(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
-                      const bloom_filter_args_t* args, hipStream_t stream) {
-    return enqueue(dR, nR, dS, nS, args, stream, false);
+                      const bloom_filter_args_t* args, hipStream_t stream, int jkind) {
+    return enqueue(dR, nR, dS, nS, args, stream, false, jkind);
 }
 
 int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
-                    const bloom_filter_args_t* args, hipStream_t stream, bool dbg) {
+                    const bloom_filter_args_t* args, hipStream_t stream, bool dbg, int jkind) {
+    if (jkind < 0 || jkind > 2) {
+        set_last_error("unknown per-partition join algorithm");
+        return 2;
+    }
     HWBRJ_CHECK(hipSetDevice(device_));
     Geometry    g;
     std::string err;
@@ -497,6 +501,7 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     jp.nparts          = jparts.as<uint32_t>();
     jp.extra           = jtask.as<uint2>();
     jp.nextra          = jparts.as<uint32_t>() + 2 * NJ;
+    jp.jkind           = (uint32_t) jkind;
     if (const char* e = getenv("HWBRJ_DEV_JOIN_SPLIT"))  // tests: force the skew split
         jp.split_surv = (uint32_t) strtoul(e, nullptr, 10);
     launch_join(jp, NJ, jparts.as<uint32_t>() + NJ, stream);

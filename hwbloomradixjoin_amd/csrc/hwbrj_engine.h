@@ -30,11 +30,12 @@ class Engine {
     explicit Engine(int device);
     ~Engine();
     // Synchronous join of device-resident tuples. Returns 0 on success.
+    // jkind: the per-partition join (JoinParams::jkind: 0 PRO, 1 PRH, 2 PRHO).
     int  run(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
-             const bloom_filter_args_t* args, hipStream_t stream, hwbrj_stats_t* st);
+             const bloom_filter_args_t* args, hipStream_t stream, hwbrj_stats_t* st, int jkind = 0);
     // Enqueue only (wait = false in run): wait() then waits for the last enqueued join.
     int  run_async(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
-                   const bloom_filter_args_t* args, hipStream_t stream);
+                   const bloom_filter_args_t* args, hipStream_t stream, int jkind = 0);
     int  wait(hwbrj_stats_t* st);
     int  export_filter(uint8_t* host_out, uint64_t nbytes);
     // (R.payload, S.payload) of every match into out[0, cap); *n = number of pairs.
@@ -63,7 +64,7 @@ class Engine {
     uint64_t     pending_nS_   = 0;
     uint32_t     last_nj_      = 0;  // join jobs of the last enqueue (job_surv layout)
     int          enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
-                         const bloom_filter_args_t* args, hipStream_t stream, bool dbg);
+                         const bloom_filter_args_t* args, hipStream_t stream, bool dbg, int jkind);
     CrcTables*   d_tabs_ = nullptr;
     GenPlan*     d_plan_ = nullptr;
     // R side

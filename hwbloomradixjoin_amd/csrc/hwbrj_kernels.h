@@ -82,6 +82,8 @@ struct JoinParams {
     uint32_t*       nextra;       // parts requested beyond part 0 (zeroed before the join)
     uint32_t        split_surv;   // survivors per join part (0: the default, kJoinTaskSurv)
     uint64_t*       dbg;          // dev-only: per-workgroup phase cycles (HWBRJ_DBG), or nullptr
+    uint32_t        jkind;        // per-partition join: 0 bucket chaining's role (bitmap / hash
+                                  // table, PRO), 1 histogram join (PRH), 2 + 16-byte compares (PRHO)
     const uint64_t* item_base;    // [items] survivor region of each item (partitioned multi-GPU
                                   // join: received runs), or nullptr (k_probe's item regions)
 };

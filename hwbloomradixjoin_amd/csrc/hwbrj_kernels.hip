@@ -1751,7 +1751,7 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
     using SR = std::integral_constant<int, HWBRJ_JSR>;  // survivor runs in flight per wave
     using SW = std::integral_constant<int, HWBRJ_JSW>;
     // the survivors of (q, s), batch by batch, against the table: bitmap (BM) or hash table
-    auto probe_survivors = [&](bool BM) {
+    auto probe_survivors = [&](auto&& op) {
         probe_begin();
         for (uint32_t d0 = i0; d0 < i1; d0 += kJoinDesc) {
             const uint32_t nd = min(kJoinDesc, i1 - d0);
@@ -1767,8 +1767,7 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
                              P.surv_off[(uint64_t) it * NSUB + s];
             }
             __syncthreads();
-            if (BM) walk(SR{}, SW{}, P.surv, dcnt, dbase, 0, nd, [&](uint32_t x) { cnt += (tab[x >> 5] >> (x & 31u)) & 1u; });
-            else walk(SR{}, SW{}, P.surv, dcnt, dbase, 0, nd, [&](uint32_t x) { cnt += join_count(tab, x); });
+            walk(SR{}, SW{}, P.surv, dcnt, dbase, 0, nd, op);
         }
         probe_end();
     };
@@ -1785,7 +1784,8 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
         (void) c;
         __syncthreads();
     };
-    bool hashed = !P.bitmap;
+    // PRH / PRHO (P.jkind 1 / 2): the histogram join of every job, below
+    bool hashed = !P.bitmap || P.jkind != 0;
     bool done   = false;
 #ifndef HWBRJ_JFR
 #define HWBRJ_JFR 8  // fused path: R runs per wave
@@ -1902,7 +1902,7 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
         if (dup) dupflag = 1;
         __syncthreads();
         hashed = dupflag != 0;  // uniform
-        if (!hashed) probe_survivors(true);
+        if (!hashed) probe_survivors([&](uint32_t x) { cnt += (tab[x >> 5] >> (x & 31u)) & 1u; });
     }
     if (hashed) {  // duplicate R keys (or keys too wide for the bitmap): counting hash table over
                    // pieces of consecutive R runs holding <= kJoinPiece keys (a run has <= slot)
@@ -1927,11 +1927,61 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
             for (uint32_t pc = 0; pc < np; pc++) {
                 const uint32_t da = pend[pc], db = pend[pc + 1];
                 __syncthreads();
-                for (uint32_t i = tid; i < kJoinT / 4; i += kJoinThreads)
-                    ((uint4*) tab)[i] = make_uint4(kEmpty, kEmpty, kEmpty, kEmpty);
+                if (P.jkind == 0) {  // counting hash table (bucket_chaining_join's role)
+                    for (uint32_t i = tid; i < kJoinT / 4; i += kJoinThreads)
+                        ((uint4*) tab)[i] = make_uint4(kEmpty, kEmpty, kEmpty, kEmpty);
+                    __syncthreads();
+                    walk(RR{}, RW{}, P.r_codes, rcnt, rbase, da, db, [&](uint32_t x) { join_insert(tab, x); });
+                    probe_survivors([&](uint32_t x) { cnt += join_count(tab, x); });  // (starts with a barrier)
+                    continue;
+                }
+                // Histogram join of Kim et al. (histogram_join / histogram_optimized_join,
+                // src/parallel_radix_join_bloom.c:350-419, :441-555): a histogram of the piece's R
+                // keys over NH = max(4, next_pow2(n) / 4) buckets, its prefix sum, the keys
+                // reordered by bucket (keys = tab[0, kJoinPiece), hist = tab[kJoinPiece, +NH + 2));
+                // every survivor compares the keys of its bucket -- one by one (PRH), or 4 per
+                // 16-byte LDS read (PRHO, the reference's SIMD compare).
+                uint32_t n = 0;
+                for (uint32_t d = da; d < db; d++) n += rcnt[d];
+                uint32_t NH = 4;
+                while (NH * 4 < n) NH <<= 1;
+                uint32_t* keys = tab;
+                uint32_t* hist = tab + kJoinPiece;
+                for (uint32_t i = tid; i < NH + 2; i += kJoinThreads) hist[i] = 0;
                 __syncthreads();
-                walk(RR{}, RW{}, P.r_codes, rcnt, rbase, da, db, [&](uint32_t x) { join_insert(tab, x); });
-                probe_survivors(false);  // (starts with a barrier: the table is complete)
+                walk(RR{}, RW{}, P.r_codes, rcnt, rbase, da, db, [&](uint32_t x) { atomicAdd(&hist[(x & (NH - 1u)) + 2], 1u); });
+                __syncthreads();
+                if (wave == 0) {  // inclusive prefix sum of hist[2, NH + 2): 16 buckets per lane
+                    const uint32_t per = (NH + 63) / 64, b0 = 2 + lane * per;
+                    uint32_t       loc = 0;
+                    for (uint32_t i = 0; i < per; i++)
+                        if (b0 + i < NH + 2) loc += hist[b0 + i];
+                    uint32_t run = wave_incl_scan(loc) - loc;
+                    for (uint32_t i = 0; i < per; i++)
+                        if (b0 + i < NH + 2) {
+                            run += hist[b0 + i];
+                            hist[b0 + i] = run;
+                        }
+                }
+                __syncthreads();
+                walk(RR{}, RW{}, P.r_codes, rcnt, rbase, da, db, [&](uint32_t x) {
+                    keys[atomicAdd(&hist[(x & (NH - 1u)) + 1], 1u)] = x;  // bucket b: [hist[b], hist[b + 1])
+                });
+                if (P.jkind == 1) {
+                    probe_survivors([&](uint32_t x) {
+                        const uint32_t b = x & (NH - 1u);
+                        for (uint32_t j = hist[b], e = hist[b + 1]; j < e; j++) cnt += keys[j] == x;
+                    });
+                } else {
+                    probe_survivors([&](uint32_t x) {
+                        const uint32_t b = x & (NH - 1u), j0 = hist[b], e = hist[b + 1];
+                        for (uint32_t j = j0 & ~3u; j < e; j += 4) {
+                            const uint4 k = *(const uint4*) &keys[j];
+                            cnt += (k.x == x && j >= j0) + (k.y == x && j + 1 >= j0 && j + 1 < e) +
+                                   (k.z == x && j + 2 >= j0 && j + 2 < e) + (k.w == x && j + 3 < e);
+                        }
+                    });
+                }
             }
         }
     }

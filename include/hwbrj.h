@@ -69,10 +69,11 @@ result_t * BPRO(relation_t * relR, relation_t * relS, int nthreads,
                 bloom_filter_args_t * bloom_filter_args);
 result_t * PRO(relation_t * relR, relation_t * relS, int nthreads);
 void       assert_args(bloom_filter_args_t * args);
-/* The reference's other partitioned-join entries (src/main.c:331-339). They differ only in the
- * per-partition join function the CPU build plugs into join_init_run (histogram-reorder build for
- * PRH, + SIMD/prefetch probe for PRHO) or in running single-threaded (RJ); the counts are the
- * same. On the MI355X the per-partition join is k_join for all of them, so they run BPRO / PRO.
+/* The reference's other partitioned-join entries (src/main.c:331-339). They differ in the
+ * per-partition join function plugged into join_init_run: the histogram join (Kim et al.) for
+ * BPRH / PRH, with SIMD compares for BPRHO / PRHO (here: k_join's histogram variants, see
+ * hwbrj_join_device_algo), or in running single-threaded (BRJ / RJ: the BPRO / PRO operator on
+ * the MI355X). The counts are the same.
  *   BPRH, BPRHO   src/parallel_radix_join_bloom.h:68-87 (impl. :1789-1804)
  *   BRJ           src/parallel_radix_join_bloom.c:1806-1930
  *   PRH, PRHO, RJ src/parallel_radix_join.h:49-82 */
@@ -118,6 +119,15 @@ typedef struct hwbrj_stats_t {
  * stream: a hipStream_t (NULL = the library's own stream). The call is synchronous. */
 int hwbrj_join_device(const tuple_t * d_R, uint64_t nR, const tuple_t * d_S, uint64_t nS,
                       const bloom_filter_args_t * args, void * stream, hwbrj_stats_t * stats);
+/* The same join with the reference's per-partition join function chosen (join_init_run's
+ * JoinFunction, src/parallel_radix_join_bloom.c:1789-1804): HWBRJ_ALGO_PRO bucket chaining
+ * (:259-329; here an LDS bitmap or counting hash table), HWBRJ_ALGO_PRH the histogram join of
+ * Kim et al. (:350-419), HWBRJ_ALGO_PRHO its SIMD form (:441-555; 16-byte LDS compares). The host
+ * entries BPRH / BPRHO / PRH / PRHO use them. Counts are identical. */
+enum { HWBRJ_ALGO_PRO = 0, HWBRJ_ALGO_PRH = 1, HWBRJ_ALGO_PRHO = 2 };
+int hwbrj_join_device_algo(const tuple_t * d_R, uint64_t nR, const tuple_t * d_S, uint64_t nS,
+                           const bloom_filter_args_t * args, int algorithm, void * stream,
+                           hwbrj_stats_t * stats);
 /* The same join, enqueued on `stream` without waiting (back-to-back joins then run without host
  * gaps); the inputs must stay valid until it completes. hwbrj_join_wait() waits for the last join
  * enqueued on this device and fills stats (counts and phase times of that join). */

@@ -295,3 +295,39 @@ def test_bench_partitioned_ranks(hw, orc, world, flags):
         S = hw.generate_host(g["s"], 2, INT_MAX, g["r"], 0.01, 54321)
         want = orc.bpro(R, S, 8, hw.SECTORIZED, g["m"], 2, 1024)[1]
     assert (line["parity"]["filtered"], line["parity"]["matches"]) == (want, g["results"])
+
+
+# ------------------------------------- BPRH / BPRHO: the histogram per-partition joins (s8f row 2)
+@pytest.mark.parametrize("algo", [1, 2], ids=["PRH", "PRHO"])
+@pytest.mark.parametrize("a", [None, ("blocked", 1 << 20, 1, 1024), ("basic", 1 << 20, 3, 0),
+                               ("blocked", 1 << 16, 2, 4), ("blocked", 1 << 31, 2, 512)], ids=str)
+def test_histogram_joins_vs_oracle(hw, cuda, orc, algo, a):
+    """histogram_join / histogram_optimized_join (src/parallel_radix_join_bloom.c:350-555) as
+    k_join variants: unique and duplicate R keys, negative and extreme keys, hot S keys."""
+    args = None if a is None else hw.BloomFilterArgs.from_flag(a[0], a[1], a[2], a[3] or 1024)
+    rng = np.random.default_rng(31)
+    cases = [(rng.permutation(100003) + 1, rng.integers(0, 200010, size=400009)),
+             (np.concatenate([rng.integers(-3000, 3000, size=60000), [INT_MAX, -INT_MAX - 1, 0, -1] * 3]),
+              np.concatenate([rng.integers(-4000, 4000, size=500000), [INT_MAX, -INT_MAX - 1, 0, -1] * 5])),
+             (np.concatenate([np.full(20000, 5), np.arange(100, 50000)]),
+              np.concatenate([np.full(3000, 5), np.arange(0, 60000)])),
+             (np.arange(1, 8), np.arange(0, 40))]
+    for Rk, Sk in cases:
+        R, S = rel(Rk), rel(Sk)
+        st = hw.join_device(to_dev(cuda, R), to_dev(cuda, S), args, algorithm=algo)
+        if args is None:
+            res, filt, _ = orc.bpro(R, S, 8, 0, 0, 0, 0, use_bloom=False)
+        else:
+            res, filt, _ = orc.bpro(R, S, 8, args.variant, args.m, args.k, args.B)
+        assert (st.filtered, st.matches) == (filt, res), (algo, a, st)
+
+
+@pytest.mark.parametrize("algo", [1, 2], ids=["PRH", "PRHO"])
+def test_histogram_joins_northstar(hw, full_R, cuda, algo):
+    """The north-star golden through the histogram joins."""
+    g = GOLD["F4_northstar"]
+    S = cuda.empty((1024000000, 2), dtype=cuda.int32, device="cuda")
+    hw.generate_device(S, 2, INT_MAX, 128000000, g["q"], 54321)
+    st = hw.join_device(full_R, S, hw.BloomFilterArgs(hw.BLOCKED, g["m"], 1, g["B"]), algorithm=algo)
+    del S
+    assert (st.filtered, st.matches) == (g["k1_filtered"], g["results"])
