@@ -781,3 +781,49 @@ orc_bpro(const orc_tuple_t * R, uint64_t nR, const orc_tuple_t * S, uint64_t nS,
     if (use_bloom) orc_bloom_free(&sh.bloom);
     return result;
 }
+
+/* ------------------------------------------------------------ FPR known answers (F6) */
+
+/* src/unit_tests.c:154-173 random_unique_gen_range: Knuth's selection sampling of n keys out of
+ * [min, max) with libc rand(), in increasing order */
+static void
+fpr_unique_range(int32_t * keys, uint64_t n, int32_t min, int32_t max)
+{
+    uint32_t inserted  = 0;
+    int32_t  m_options = max - min;
+    for (uint32_t i = 0; i < (uint32_t) m_options && inserted < n; ++i) {
+        int rn = (int) (n - inserted);
+        int rm = m_options - (int32_t) i;
+        if (rand() % rm < rn) keys[inserted++] = min + (int32_t) i;
+    }
+}
+
+/* src/unit_tests.c:191-283 (test_bloom_fpr_wrapper, test_bloom_fpr): R and S drawn from disjoint
+ * key ranges, then for the blocked filter (B = 512) and the basic filter, k = 1 .. kmax: a filter
+ * seeded with rand() after srand(seed), R added, S probed. pos[v * kmax + k - 1] = positives of S
+ * (all false: fpr_emp = pos / n_samples), v = 0 blocked, 1 basic. */
+int
+orc_fpr_test(int seed, uint64_t m, uint64_t kmax, uint32_t n_samples, uint32_t n_insertions,
+             uint64_t * pos)
+{
+    srand((unsigned) (seed + 1));
+    int32_t * R = (int32_t *) malloc(sizeof(int32_t) * (n_insertions ? n_insertions : 1));
+    int32_t * S = (int32_t *) malloc(sizeof(int32_t) * (n_samples ? n_samples : 1));
+    if (!R || !S) return 1;
+    int32_t threshold = (int32_t) (INT32_MAX * (n_insertions / (double) (n_insertions + n_samples)));
+    fpr_unique_range(R, n_insertions, 0, threshold);
+    fpr_unique_range(S, n_samples, threshold + 1, INT32_MAX);
+    for (int v = 0; v < 2; v++) {
+        for (uint64_t k = 1; k <= kmax; k++) {
+            srand((unsigned) seed);
+            orc_bloom_t f;
+            if (orc_bloom_init(&f, v == 0 ? 1 : 0, m, k, 512, (uint32_t) rand())) return 1;
+            orc_bloom_add_all(&f, R, n_insertions);
+            pos[v * kmax + k - 1] = orc_count_filtered(&f, S, n_samples);
+            orc_bloom_free(&f);
+        }
+    }
+    free(R);
+    free(S);
+    return 0;
+}

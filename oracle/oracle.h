@@ -96,6 +96,10 @@ int64_t  orc_join_pairs(const orc_tuple_t * R, uint64_t nR, const orc_tuple_t * 
 
 /* Scalar helpers for tests (single-threaded, small inputs). */
 uint64_t orc_count_filtered(const orc_bloom_t * f, const int32_t * keys, uint64_t n);
+/* src/unit_tests.c:191-283: false-positive counts of the FPR unit test (blocked B=512, then
+ * basic, k = 1 .. kmax) */
+int      orc_fpr_test(int seed, uint64_t m, uint64_t kmax, uint32_t n_samples, uint32_t n_insertions,
+                      uint64_t * pos);
 void     orc_bloom_add_all(orc_bloom_t * f, const int32_t * keys, uint64_t n);
 
 #ifdef __cplusplus

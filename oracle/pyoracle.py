@@ -66,8 +66,21 @@ def lib() -> ctypes.CDLL:
         L.orc_join_pairs.restype = ctypes.c_int64
         L.orc_join_pairs.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
                                      ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64]
+        L.orc_fpr_test.restype = ctypes.c_int
+        L.orc_fpr_test.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
+                                   ctypes.c_uint32, ctypes.c_void_p]
         _L = L
     return _L
+
+
+def fpr_test(seed: int, m: int, kmax: int, n_samples: int, n_insertions: int):
+    """The reference's FPR unit test (src/unit_tests.c:191-283): ({k: fpr_emp %} blocked B=512,
+    {k: fpr_emp %} basic), fpr_emp = false positives / n_samples."""
+    pos = np.zeros(2 * kmax, dtype=np.uint64)
+    if lib().orc_fpr_test(seed, m, kmax, n_samples, n_insertions, pos.ctypes.data):
+        raise MemoryError
+    pct = pos.astype(np.float64) / n_samples * 100.0
+    return ({k + 1: pct[k] for k in range(kmax)}, {k + 1: pct[kmax + k] for k in range(kmax)})
 
 
 def join_pairs(R: np.ndarray, S: np.ndarray) -> np.ndarray:
