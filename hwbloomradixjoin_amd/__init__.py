@@ -409,21 +409,29 @@ def join_device(R, S, args: Optional[BloomFilterArgs] = None, stream=None,
     return Stats(**{n: getattr(st, n) for n, _ in _Stats._fields_})
 
 
-def join_materialize_device(R, S, args: Optional[BloomFilterArgs] = None, stream=None):
-    """(Stats, pairs): the join of device tensors R, S with its result materialized as a (n, 2)
-    int32 GPU tensor of {R.payload, S.payload} pairs, unordered (JOIN_RESULT_MATERIALIZE)."""
+def join_materialize_device(R, S, args: Optional[BloomFilterArgs] = None, stream=None,
+                            capacity: Optional[int] = None):
+    """(Stats, pairs, ms): the join of device tensors R, S with its result materialized as a (n, 2)
+    int32 GPU tensor of {R.payload, S.payload} pairs, unordered (JOIN_RESULT_MATERIALIZE); ms is
+    the device time of the materializing pipeline. capacity: output rows to allocate (None: sized
+    by a counting join first; too small: the pipeline runs again at the exact size)."""
     import torch
-    st = join_device(R, S, args, stream)
-    out = torch.empty((max(st.matches, 1), 2), dtype=torch.int32, device=R.device)
+    if capacity is None:
+        capacity = join_device(R, S, args, stream).matches
     a = args._c() if args is not None else None
     sp = ctypes.c_void_p(stream.cuda_stream) if stream is not None else None
-    n = ctypes.c_uint64()
-    st2 = _Stats()
-    ms = ctypes.c_double()
-    rc = lib().hwbrj_join_materialize_device(_ptr(R), R.shape[0], _ptr(S), S.shape[0],
-                                             ctypes.byref(a) if a is not None else None,
-                                             _ptr(out), out.shape[0], ctypes.byref(n), sp,
-                                             ctypes.byref(st2), ctypes.byref(ms))
+    for _ in range(2):
+        out = torch.empty((max(int(capacity), 1), 2), dtype=torch.int32, device=R.device)
+        n = ctypes.c_uint64()
+        st2 = _Stats()
+        ms = ctypes.c_double()
+        rc = lib().hwbrj_join_materialize_device(_ptr(R), R.shape[0], _ptr(S), S.shape[0],
+                                                 ctypes.byref(a) if a is not None else None,
+                                                 _ptr(out), out.shape[0], ctypes.byref(n), sp,
+                                                 ctypes.byref(st2), ctypes.byref(ms))
+        if rc != 7:
+            break
+        capacity = n.value
     _err(rc, "hwbrj_join_materialize_device")
     stats = Stats(**{f: getattr(st2, f) for f, _ in _Stats._fields_})
     return stats, out[: n.value], ms.value

@@ -91,6 +91,34 @@ int hwbrj_join_wait(hwbrj_stats_t* stats) {
     return e->wait(stats);
 }
 
+// The materializing join: the partitioned pipeline carrying payloads (Engine::run_mat); the
+// global-bitmap mode (basic k = 0 or B < 8) falls back to a counting join plus the side pass.
+// *n = all pairs (also beyond cap); *ms = the device time of the pairs' production.
+static int materialize_pairs(Engine* e, const tuple_t* d_R, uint64_t nR, const tuple_t* d_S, uint64_t nS,
+                             const bloom_filter_args_t* args, tuple_t* d_out, uint64_t cap, uint64_t* n,
+                             hipStream_t stream, hwbrj_stats_t* st, double* ms) {
+    int rc = e->run_mat((const uint2*) d_R, nR, (const uint2*) d_S, nS, args, stream,
+                        MatReq{(uint2*) d_out, cap}, st);
+    if (rc == 0) {
+        *n = (uint64_t) st->matches;
+        if (ms) *ms = st->ms_total;
+        return 0;
+    }
+    if (rc != kRcMatGlobal) return rc;
+    rc = e->run((const uint2*) d_R, nR, (const uint2*) d_S, nS, args, stream, st);
+    if (rc) return rc;
+    *n = (uint64_t) st->matches;
+    if (*n > cap) return 0;  // (the caller reports the capacity)
+    uint64_t m = 0;
+    rc = e->materialize((const uint2*) d_R, nR, (const uint2*) d_S, nS, (uint2*) d_out, cap, &m, stream, ms);
+    if (rc) return rc;
+    if (m != *n) {
+        set_last_error("materialized pairs differ from the counted matches");
+        return 8;
+    }
+    return 0;
+}
+
 int hwbrj_join_materialize_device(const tuple_t* d_R, uint64_t nR, const tuple_t* d_S, uint64_t nS,
                                   const bloom_filter_args_t* args, tuple_t* d_out,
                                   uint64_t capacity, uint64_t* n_out, void* stream,
@@ -98,22 +126,15 @@ int hwbrj_join_materialize_device(const tuple_t* d_R, uint64_t nR, const tuple_t
     Engine* e = engine_for_current_device();
     if (!e) return 10;  // (last error set by engine_for_current_device)
     hwbrj_stats_t st;
-    int rc = e->run((const uint2*) d_R, nR, (const uint2*) d_S, nS, args, (hipStream_t) stream, &st);
+    uint64_t      n  = 0;
+    const int     rc = materialize_pairs(e, d_R, nR, d_S, nS, args, d_out, capacity, &n, (hipStream_t) stream,
+                                         &st, ms_materialize);
     if (rc) return rc;
     if (stats) *stats = st;
-    uint64_t n = 0;
-    if ((uint64_t) st.matches > capacity) {
-        if (n_out) *n_out = (uint64_t) st.matches;
+    if (n_out) *n_out = n;
+    if (n > capacity) {
         set_last_error("output capacity below the match count (*n_out holds the count)");
         return 7;
-    }
-    rc = e->materialize((const uint2*) d_R, nR, (const uint2*) d_S, nS, (uint2*) d_out, capacity, &n,
-                        (hipStream_t) stream, ms_materialize);
-    if (rc) return rc;
-    if (n_out) *n_out = n;
-    if (n != (uint64_t) st.matches) {
-        set_last_error("materialized pairs differ from the counted matches");
-        return 8;
     }
     return 0;
 }
@@ -269,16 +290,16 @@ ChainedTupleBuffer* chained_from(const tuple_t* pairs, uint64_t n) {
 static threadresult_t* materialize_to_host(const tuple_t* dR, uint64_t nR, const tuple_t* dS,
                                            uint64_t nS, const bloom_filter_args_t* args,
                                            uint64_t matches, int nthreads) {
-    (void) args;
     tuple_t* dout = nullptr;
     if (hipMalloc((void**) &dout, (matches ? matches : 1) * sizeof(tuple_t)) != hipSuccess) {
         set_last_error("hipMalloc of the result pairs failed");
         fatal("BPRO");
     }
-    Engine*  e = engine_for_current_device();
-    uint64_t n = 0;
-    if (!e || e->materialize((const uint2*) dR, nR, (const uint2*) dS, nS, (uint2*) dout, matches, &n,
-                             nullptr, nullptr) != 0 || n != matches)
+    Engine*       e = engine_for_current_device();
+    uint64_t      n = 0;
+    hwbrj_stats_t st;
+    if (!e || materialize_pairs(e, dR, nR, dS, nS, args, dout, matches, &n, nullptr, &st, nullptr) != 0 ||
+        n != matches)
         fatal("BPRO (materialize)");
     std::vector<tuple_t> host(matches ? matches : 1);
     if (matches && hipMemcpy(host.data(), dout, matches * sizeof(tuple_t), hipMemcpyDeviceToHost) != hipSuccess) {

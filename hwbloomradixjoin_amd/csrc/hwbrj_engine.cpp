@@ -110,7 +110,7 @@ int make_gen_plan(GenPlan* plan, uint64_t num_tuples, uint32_t nthreads, uint64_
 }
 
 // ------------------------------------------------------------------------------ geometry
-bool plan_geometry(const bloom_filter_args_t* a, uint64_t nR, Geometry* g, std::string* err) {
+bool plan_geometry(const bloom_filter_args_t* a, uint64_t nR, Geometry* g, std::string* err, bool mat) {
     memset(g, 0, sizeof(*g));
     g->variant = -1;
     if (!a) {
@@ -186,7 +186,7 @@ bool plan_geometry(const bloom_filter_args_t* a, uint64_t nR, Geometry* g, std::
         // the S traffic by 2.6 GB per join, but the probe's per-word key recovery costs more than
         // that saves
         g->s_format = g->format;
-        if (g->mode == MODE_SLICE_BLOCK && g->log2F == 10 && getenv("HWBRJ_DEV_C22")) g->s_format = FMT_C22;
+        if (!mat && g->mode == MODE_SLICE_BLOCK && g->log2F == 10 && getenv("HWBRJ_DEV_C22")) g->s_format = FMT_C22;
         if (g->mode == MODE_SLICE_BLOCK || g->mode == MODE_SLICE_BASIC) g->log2seg = ilog2u(g->seg_bits);
         if (a->variant != BASIC) {
             g->log2B    = ilog2u(B);
@@ -203,7 +203,9 @@ bool plan_geometry(const bloom_filter_args_t* a, uint64_t nR, Geometry* g, std::
     const uint64_t rper = (nR + F - 1) / F;
     uint32_t       l2s  = 0;
     g->sub_shift  = (g->mode == MODE_SLICE_BASIC) ? 0 : g->log2F;
-    if (g->sub_shift > 0 && g->log2F + 6 >= 14) {
+    if (mat) {  // k_join_mat: a table of <= 2048 R tuples per piece, so ~1536 per job on average
+        while (l2s < 6 && (rper >> l2s) > 1536) l2s++;
+    } else if (g->sub_shift > 0 && g->log2F + 6 >= 14) {
         l2s = g->log2F >= 14 ? 0 : 14 - g->log2F;
     } else {
         while (l2s < 6 && (rper >> l2s) > 4096) l2s++;
@@ -255,7 +257,7 @@ void Engine::release() {
                       &istartS, &listS, &slices, &bitmap, &rjoin, &rrun, &surv, &survcnt, &survoff,
                       &dense, &small, &bpos, &colR, &colS, &mtab, &mcount, &jtask, &jparts, &pjList,
                       &pjLstart, &pjSweep, &pjTab, &pjRegion, &pjTot, &pjSoff, &pjIbase, &pjCnt, &pjOff,
-                      &pjIstart, &pjJobs})
+                      &pjIstart, &pjJobs, &ppoolR, &ppoolS, &rpay, &survpos})
         b->release();
     have_filter_ = false;
 }
@@ -277,8 +279,16 @@ int Engine::run_async(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS
     return enqueue(dR, nR, dS, nS, args, stream, false, jkind);
 }
 
+int Engine::run_mat(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
+                    const bloom_filter_args_t* args, hipStream_t stream, const MatReq& mat,
+                    hwbrj_stats_t* st) {
+    const int rc = enqueue(dR, nR, dS, nS, args, stream, false, 0, &mat);
+    return rc ? rc : wait(st);
+}
+
 int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
-                    const bloom_filter_args_t* args, hipStream_t stream, bool dbg, int jkind) {
+                    const bloom_filter_args_t* args, hipStream_t stream, bool dbg, int jkind,
+                    const MatReq* mat) {
     if (jkind < 0 || jkind > 2) {
         set_last_error("unknown per-partition join algorithm");
         return 2;
@@ -286,9 +296,13 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     HWBRJ_CHECK(hipSetDevice(device_));
     Geometry    g;
     std::string err;
-    if (!plan_geometry(args, nR, &g, &err)) {
+    if (!plan_geometry(args, nR, &g, &err, mat != nullptr)) {
         set_last_error(err);
         return 2;
+    }
+    if (mat && g.mode == MODE_GLOBAL) {
+        set_last_error("global-bitmap mode: materialized by the side pass");
+        return kRcMatGlobal;
     }
     if (!stream) stream = own_stream_;
     // Every join on this device shares this Engine's scratch (pools, lists, slices, counters):
@@ -298,7 +312,7 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     const bool     slice_mode = g.mode == MODE_SLICE_BLOCK || g.mode == MODE_SLICE_BASIC;
     const uint32_t nseg       = slice_mode ? g.nseg : 1;
     const uint32_t CH         = probe_chunks_per_item();  // chunks per probe item
-    const size_t   sc_lds     = scatter_lds_bytes(g.log2F);
+    const size_t   sc_lds     = mat ? scatter_pay_lds_bytes(g.log2F) : scatter_lds_bytes(g.log2F);
     uint32_t       sc_wpc     = (uint32_t) std::max<size_t>(1, std::min<size_t>(2, 163840 / sc_lds));
     if (const char* e = getenv("HWBRJ_DEV_SCWPC"))  // dev-only: scatter workgroups per CU
         sc_wpc = std::max(1u, std::min(sc_wpc, (uint32_t) atoi(e)));
@@ -316,6 +330,10 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     }
     if (LS > (1ull << 27) || LR > (1ull << 27) || capS >= (1u << 22) || capR >= (1u << 22)) {
         set_last_error("relation too large for 27-bit chunk ids (|S| or |R| > ~4.2e9 tuples per GPU)");
+        return 3;
+    }
+    if (mat && (capS >= (1u << 21) || capR >= (1u << 21))) {  // half indices (scatter_body_pay) < 2^22
+        set_last_error("relation too large for the materializing scatter's 22-bit half indices");
         return 3;
     }
     const uint64_t GF = (uint64_t) G * F;
@@ -341,6 +359,10 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     if (slice_mode) ok &= slices.ensure((uint64_t) F * nseg * g.seg_words * 4);
     if (g.mode == MODE_GLOBAL) ok &= bitmap.ensure(((g.m + 31) / 32) * 4) && dense.ensure(nS * 4);
     if (basic_kk) ok &= bpos.ensure(nRk * 4);
+    if (mat) {
+        ok &= ppoolR.ensure(LR * 128) && ppoolS.ensure(LS * 128) && rpay.ensure(sweeps_max * SLOT * 4) &&
+              survpos.ensure(nseg * LS * 128);
+    }
     if (!ok) {
         set_last_error("hipMalloc failed (device memory)");
         return 4;
@@ -368,12 +390,14 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     sp.n          = nR;
     sp.n_dev      = nullptr;
     sp.pool       = poolR.as<uint32_t>();
+    sp.ppool      = mat ? ppoolR.as<uint32_t>() : nullptr;
     sp.meta       = metaR.as<uint32_t>();
     sp.wg_used    = usedR.as<uint32_t>();
     sp.wgq_chunks = wgqcR.as<uint32_t>();
     sp.wgq_elems  = wgqeR.as<uint32_t>();
     sp.cap        = capR;
     launch_scatter(sp, SRC_TUPLES, SIDE_R, G, stream);
+    sp.ppool      = nullptr;
     HWBRJ_CHECK(hipEventRecord(ev_[1], stream));
     launch_plan(wgqcR.as<uint32_t>(), wgqeR.as<uint32_t>(), G, g.log2F, wgqoR.as<uint32_t>(),
                 colR.as<uint32_t>() + 2 * F, colR.as<uint64_t>(), stream);
@@ -393,6 +417,8 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     bp.out_codes   = rjoin.as<uint32_t>();
     bp.run_cnt     = rrun.as<uint32_t>();
     bp.run_off     = rrun.as<uint32_t>() + sweeps_max * NSUB;
+    bp.ppool       = mat ? ppoolR.as<uint32_t>() : nullptr;
+    bp.out_pay     = mat ? rpay.as<uint32_t>() : nullptr;
     launch_build(bp, F, stream);
     if (basic_kk) {
         // basic k >= 2: the k bit positions of every R key, partitioned by slice with the S-side
@@ -442,6 +468,7 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
         HWBRJ_CHECK(hipMemsetAsync(dbgS.p, 0, dbgS.bytes, stream));
         sp.dbg = dbgS.as<uint64_t>();
     }
+    sp.ppool = mat ? ppoolS.as<uint32_t>() : nullptr;
     launch_scatter(sp, g.mode == MODE_GLOBAL ? SRC_CODES : SRC_TUPLES, SIDE_S, G, stream);
     sp.dbg = nullptr;
     HWBRJ_CHECK(hipEventRecord(ev_[4], stream));
@@ -465,6 +492,7 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     pp.surv_off        = survoff.as<uint32_t>();
     pp.filtered        = d_filtered;
     pp.job_surv        = jparts.as<uint32_t>() + NJ;
+    pp.surv_pos        = mat ? survpos.as<uint32_t>() : nullptr;
     const size_t   pl_lds = probe_lds_bytes(g, nullptr);
     const uint32_t PG = (uint32_t) cus_ * (uint32_t) std::max<size_t>(1, std::min<size_t>(2, 163840 / pl_lds));
     const bool dbg_on = dbg;  // dev-only phase stamps (HWBRJ_DBG)
@@ -504,7 +532,35 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     jp.jkind           = (uint32_t) jkind;
     if (const char* e = getenv("HWBRJ_DEV_JOIN_SPLIT"))  // tests: force the skew split
         jp.split_surv = (uint32_t) strtoul(e, nullptr, 10);
-    launch_join(jp, NJ, jparts.as<uint32_t>() + NJ, stream);
+    if (mat) {
+        // (k_join_split, which leaves job_surv zero for the next join, does not run here)
+        HWBRJ_CHECK(hipMemsetAsync(jparts.as<uint32_t>() + NJ, 0, (size_t) NJ * 4, stream));
+        MatJoinParams mp{};
+        mp.r_codes         = jp.r_codes;
+        mp.r_pay           = rpay.as<uint32_t>();
+        mp.r_sweep_start   = jp.r_sweep_start;
+        mp.r_cnt           = jp.r_cnt;
+        mp.r_off           = jp.r_off;
+        mp.slot            = jp.slot;
+        mp.surv            = jp.surv;
+        mp.surv_pos        = survpos.as<uint32_t>();
+        mp.surv_cnt        = jp.surv_cnt;
+        mp.surv_off        = jp.surv_off;
+        mp.item_start      = jp.item_start;
+        mp.list_start      = jp.list_start;
+        mp.surv_seg_stride = jp.surv_seg_stride;
+        mp.nseg            = nseg;
+        mp.CH              = CH;
+        mp.log2NSUB        = g.log2NSUB;
+        mp.hash_shift      = g.hash_shift;
+        mp.s_pay           = ppoolS.as<uint32_t>();
+        mp.out             = mat->out;
+        mp.cap             = mat->cap;
+        mp.count           = (unsigned long long*) d_result;
+        launch_join_mat(mp, NJ, stream);
+    } else {
+        launch_join(jp, NJ, jparts.as<uint32_t>() + NJ, stream);
+    }
     HWBRJ_CHECK(hipEventRecord(ev_[8], stream));
     HWBRJ_CHECK(hipGetLastError());
     pending_      = true;

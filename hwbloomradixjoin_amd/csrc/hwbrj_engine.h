@@ -15,7 +15,17 @@ namespace hwbrj {
 
 // Picks mode / partitioning / slice geometry for a filter configuration (DESIGN.md "Modes").
 // Returns false (and sets *err) for configurations outside the reference's contract.
-bool plan_geometry(const bloom_filter_args_t* args, uint64_t nR, Geometry* g, std::string* err);
+// mat: the materializing pipeline's geometry (no FMT_C22 S words; join jobs sized for its hash
+// table, k_join_mat).
+bool plan_geometry(const bloom_filter_args_t* args, uint64_t nR, Geometry* g, std::string* err,
+                   bool mat = false);
+
+// A materializing join's output: {R.payload, S.payload} pairs into out[0, cap).
+struct MatReq {
+    uint2*   out;
+    uint64_t cap;
+};
+constexpr int kRcMatGlobal = 11;  // run_mat: global-bitmap mode, use the side pass (materialize)
 
 struct DevBuf {
     void*  p     = nullptr;
@@ -38,7 +48,13 @@ class Engine {
                    const bloom_filter_args_t* args, hipStream_t stream, int jkind = 0);
     int  wait(hwbrj_stats_t* st);
     int  export_filter(uint8_t* host_out, uint64_t nbytes);
-    // (R.payload, S.payload) of every match into out[0, cap); *n = number of pairs.
+    // The materializing join (the partitioned pipeline carrying payloads): st->matches = pairs
+    // (all of them, also beyond cap). kRcMatGlobal: not for the global-bitmap mode.
+    int  run_mat(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
+                 const bloom_filter_args_t* args, hipStream_t stream, const MatReq& mat,
+                 hwbrj_stats_t* st);
+    // Side pass after a counting join (global-bitmap mode): (R.payload, S.payload) of every match
+    // into out[0, cap); *n = number of pairs.
     int  materialize(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS, uint2* out,
                      uint64_t cap, uint64_t* n, hipStream_t stream, double* ms);
     int  generate(uint2* d_out, uint64_t n, uint64_t offset, uint64_t count, uint32_t nthreads,
@@ -64,7 +80,8 @@ class Engine {
     uint64_t     pending_nS_   = 0;
     uint32_t     last_nj_      = 0;  // join jobs of the last enqueue (job_surv layout)
     int          enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
-                         const bloom_filter_args_t* args, hipStream_t stream, bool dbg, int jkind);
+                         const bloom_filter_args_t* args, hipStream_t stream, bool dbg, int jkind,
+                         const MatReq* mat = nullptr);
     CrcTables*   d_tabs_ = nullptr;
     GenPlan*     d_plan_ = nullptr;
     // R side
@@ -74,7 +91,10 @@ class Engine {
     DevBuf slices, bitmap, rjoin, rrun, surv, survcnt, survoff, dense, small, dbgP, dbgJ, dbgS;
     DevBuf bpos;        // basic k >= 2: R bit positions (k_bitpos)
     DevBuf colR, colS;  // per-partition totals from k_plan: u64 elements [F], then u32 chunks [F]
-    DevBuf mtab, mcount;  // materialization: R table, pair counter
+    DevBuf mtab, mcount;  // materialization (side pass): R table, pair counter
+    // materializing pipeline: payload pools (chunk layout of poolR / poolS), R payloads of the
+    // build sweeps, survivors' chunk positions
+    DevBuf ppoolR, ppoolS, rpay, survpos;
     DevBuf jtask, jparts;  // join task table; parts per job (+ the task count)
     // partitioned join: owned partitions' lists, tables and received survivor descriptors
     DevBuf pjList, pjLstart, pjSweep, pjTab, pjRegion, pjTot, pjSoff, pjIbase, pjCnt, pjOff, pjIstart, pjJobs;

@@ -17,6 +17,7 @@ struct ScatterParams {
     uint64_t         n;            // element count (ignored when n_dev != nullptr)
     const uint64_t*  n_dev;        // optional device-resident element count
     uint32_t*        pool;         // [G * cap][32] chunk words
+    uint32_t*        ppool;        // [G * cap][32] the words' payloads (materialization), or nullptr
     uint32_t*        meta;         // [G * cap]: partition | count << 16
     uint32_t*        wg_used;      // [G] chunks used by each workgroup
     uint32_t*        wgq_chunks;   // [G][F] chunks of partition q in workgroup wg's region
@@ -40,6 +41,8 @@ struct BuildParams {
     uint32_t*        run_cnt;     // [sweeps][NSUB] codes of each (sweep, sub) run
     uint32_t*        run_off;     // [sweeps][NSUB] run offset inside the sweep's slot
     uint32_t         q_base;      // partition of workgroup 0 (list/sweep tables indexed from it)
+    const uint32_t*  ppool;       // payloads of pool's words (materialization), or nullptr
+    uint32_t*        out_pay;     // [sweeps][kBSlot]: the payloads of out_codes (ppool set)
 };
 
 struct ProbeParams {
@@ -57,6 +60,8 @@ struct ProbeParams {
     uint64_t*        filtered;    // += survivors ("S-tuples after filter")
     uint32_t*        job_surv;    // [F * NSUB] += survivors of each join job (zero on entry)
     uint32_t         stage_cap;   // survivor stage words (set by launch_probe)
+    uint32_t*        surv_pos;    // materialization: each survivor's chunk position (its payload's
+                                  // index in the S payload pool), parallel to surv; or nullptr
     uint64_t*        dbg;         // dev-only: per-workgroup phase cycles (HWBRJ_DBG), or nullptr
 };
 
@@ -88,6 +93,29 @@ struct JoinParams {
                                   // join: received runs), or nullptr (k_probe's item regions)
 };
 
+// The materializing join (k_join_mat): R codes + payloads of the build sweeps, survivors + their
+// chunk positions, {R.payload, S.payload} pairs appended to out (up to cap; count = all pairs).
+struct MatJoinParams {
+    const uint32_t* r_codes;
+    const uint32_t* r_pay;          // BuildParams::out_pay
+    const uint32_t* r_sweep_start;  // [F + 1]
+    const uint32_t* r_cnt;
+    const uint32_t* r_off;
+    uint32_t        slot;
+    const uint32_t* surv;
+    const uint32_t* surv_pos;       // ProbeParams::surv_pos
+    const uint32_t* surv_cnt;
+    const uint32_t* surv_off;
+    const uint32_t* item_start;
+    const uint32_t* list_start;
+    uint64_t        surv_seg_stride;
+    uint32_t        nseg, CH, log2NSUB, hash_shift;
+    const uint32_t* s_pay;          // S payload pool (ScatterParams::ppool of the S pass)
+    uint2*          out;
+    uint64_t        cap;
+    unsigned long long* count;      // += pairs (zero on entry)
+};
+
 void   launch_gen(uint2* out, uint64_t offset, uint64_t count, const GenPlan* d_plan, const Perm& perm,
                   hipStream_t st);
 void   launch_zipf(const int32_t* rnd, uint64_t cnt, uint64_t row0, const double* lut,
@@ -103,6 +131,7 @@ void   launch_bitpos(const uint2* R, uint64_t n, const Geometry& g, uint32_t* ou
 void   launch_slice_fill(const uint32_t* pool, const uint32_t* list, const uint32_t* list_start,
                          const Geometry& g, uint32_t* slices, hipStream_t st);
 size_t scatter_lds_bytes(uint32_t log2F);
+size_t scatter_pay_lds_bytes(uint32_t log2F);  // (ScatterParams::ppool set)
 enum { SIDE_R = 0, SIDE_S = 1 };  // which relation a scatter partitions (kernel name; S uses g.s_format)
 void   launch_scatter(const ScatterParams& p, int src, int side, uint32_t grid, hipStream_t st);
 // k_plan: per-(wg, q) list offsets + per-partition chunk / element totals (colc, cole);
@@ -125,6 +154,7 @@ void   launch_probe(const ProbeParams& p, uint32_t grid, hipStream_t st);
 // splits skewed jobs (job_surv: survivors per job from k_probe, cleared here) and runs the join
 void   launch_join(const JoinParams& p, uint32_t jobs, uint32_t* job_surv, hipStream_t st);
 uint32_t join_extra_tasks();
+void   launch_join_mat(const MatJoinParams& p, uint32_t jobs, hipStream_t st);
 // result materialization (K12): R table build, S probe writing (R.payload, S.payload) pairs
 void   launch_mat_build(const uint2* R, uint64_t n, unsigned long long* tab, uint64_t mask,
                         hipStream_t st);

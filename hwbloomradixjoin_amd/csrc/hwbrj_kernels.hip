@@ -823,6 +823,259 @@ __device__ __forceinline__ void scatter_body(const ScatterParams& P) {
     }
 }
 
+// ------------------------------------------------- K3p: SWWC partitioning with payloads
+// Result materialization (JOIN_RESULT_MATERIALIZE, src/parallel_radix_join_bloom.c:307-312) needs
+// every tuple's payload where its word lands: `ppool` shares the chunk layout of `pool`, so a
+// survivor names its payload by chunk position. The LDS stage holds words and payloads of
+// kPayDepth = 16 slots per partition (2 x 64 KiB at F = 1024): a stage line is half a chunk, and
+// a partition's chunk is written as two 64-byte halves, rounds apart. Chunk ids are taken when a
+// chunk's first half is flushed; per partition cst = current chunk << 1 | 1 while only its first
+// half is written (0: none). Halves are numbered chunk * 2 + half: a plan sends the stage line to
+// half H0 and, in a skewed round (a partition overfilled by >= 16), its further halves k = 1 ..
+// nh - 1 to Bk + k, written directly by the threads holding those words. Pending words (slots past
+// the stage line) go to the line after its flush, at slot - 16 * nh; in a skewed round they are
+// resolved against the plan before the next round's first barrier. All chunks but a partition's
+// last are full, so the per-partition chunk count is ceil(elements / 32).
+constexpr uint32_t kPayDepth = 16;
+constexpr int      kScKP     = 2;  // flush tasks per thread per round (4 per half: 16 B of words + of payloads)
+typedef unsigned int v2u __attribute__((ext_vector_type(2)));
+
+template <int MODE, int FMT>
+__device__ __forceinline__ void scatter_body_pay(const ScatterParams& P) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    __shared__ uint32_t crc_tab[128];
+    const uint32_t F     = 1u << P.g.log2F;
+    const uint32_t SL    = F * kPayDepth + 64;  // stage words (+ 64 per-lane dummy slots)
+    uint32_t*      stw   = lds;                 // words
+    uint32_t*      stp   = stw + SL;            // payloads
+    uint32_t*      fill  = stp + SL;            // F + 4 (entry F: invalid elements)
+    uint32_t*      pl0   = fill + F + 4;        // F: half index of the stage line's flush
+    uint32_t*      pl1   = pl0 + F;             // F: Bk | nh << 22
+    uint32_t*      cst   = pl1 + F;             // F: current chunk << 1 | 1, or 0
+    uint32_t*      tel   = cst + F;             // F: elements of q (this workgroup)
+    uint32_t*      flq   = tel + F;             // F: partitions flushed by the last plan
+    uint32_t*      misc  = flq + F;             // [0] chunks used, [1 + parity] flushes, [3 + parity] skew
+    const int      tid   = threadIdx.x, lane = tid & 63;
+    const uint32_t dummy = F * kPayDepth + lane;
+    for (uint32_t i = tid; i < F + 1; i += kScThreads) fill[i] = 0;
+    for (uint32_t i = tid; i < F; i += kScThreads) {
+        cst[i] = 0;
+        tel[i] = 0;
+    }
+    if (tid < 128) {  // nibble table; f(kSeed) folded into row 0 (as in scatter_body)
+        const uint32_t* src = &P.tabs->fwd[0][0];
+        uint32_t        v   = src[tid];
+        if (tid < 16) {
+#pragma unroll
+            for (int j = 0; j < 8; j++) v ^= src[j * 16 + ((kSeed >> (4 * j)) & 15u)];
+        }
+        crc_tab[tid] = v;
+    }
+    if (tid < 8) misc[tid] = 0;
+
+    const uint64_t n     = P.n;
+    const uint64_t units = (n + 3) >> 2;
+    const uint64_t G = gridDim.x, wg = blockIdx.x;
+    const uint64_t e0  = 4 * (wg * units / G);
+    const uint64_t e1r = 4 * ((wg + 1) * units / G);
+    const uint64_t e1  = e1r < n ? e1r : n;
+    const uint32_t len = __builtin_amdgcn_readfirstlane(e1 > e0 ? (uint32_t) (e1 - e0) : 0u);
+    uint32_t* __restrict__ meta = P.meta + wg * P.cap;
+    const auto rsrc   = buf_rsrc((const uint8_t*) P.src + e0 * 8, len * 8);  // OOB loads return 0
+    const auto rpool  = buf_rsrc(P.pool + wg * P.cap * 32, (uint32_t) (P.cap * 128));
+    const auto rppool = buf_rsrc(P.ppool + wg * P.cap * 32, (uint32_t) (P.cap * 128));
+    const auto rmeta  = buf_rsrc(meta, (uint32_t) (P.cap * 4));
+    __syncthreads();
+
+    auto load_round = [&](uint32_t base, v2u (&R)[kScE]) {  // {key, payload} as one 8-byte load
+        if (base + kScRound <= len) {
+#pragma unroll
+            for (int j = 0; j < kScE; j++)
+                R[j] = __builtin_amdgcn_raw_buffer_load_b64(rsrc, tid * 8, (base + j * kScThreads) * 8, 0);
+        } else {
+#pragma unroll
+            for (int j = 0; j < kScE; j++) {
+                const uint32_t i = base + j * kScThreads + tid;
+                R[j] = __builtin_amdgcn_raw_buffer_load_b64(rsrc, i < len ? i * 8 : kOob, 0, 0);
+            }
+        }
+    };
+    uint32_t par = 0;
+    // copy-out of the last plan's stage lines: task k = (flush entry k >> 2, 16-byte column k & 3)
+    auto flush_copy = [&]() {
+        const uint32_t nf = misc[1 + (par ^ 1u)];
+        auto task = [&](uint32_t k) {
+            const bool     ok = k < nf * 4;
+            const uint32_t qq = flq[ok ? k >> 2 : 0];
+            const uint32_t l4 = k & 3;
+            const uint32_t H  = pl0[qq];
+            const v4u      vw = *(const v4u*) &stw[qq * kPayDepth + l4 * 4];
+            const v4u      vp = *(const v4u*) &stp[qq * kPayDepth + l4 * 4];
+            const uint32_t o  = ok ? (H * 16 + l4 * 4) * 4 : kOob;
+            __builtin_amdgcn_raw_buffer_store_b128(vw, rpool, o, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b128(vp, rppool, o, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(qq | (32u << 16), rmeta, ok && l4 == 0 && (H & 1u) ? (H >> 1) * 4 : kOob, 0, 0);
+        };
+#pragma unroll
+        for (int i = 0; i < kScKP; i++) task(tid + i * kScThreads);
+        for (uint32_t k = kScKP * kScThreads + tid; k < nf * 4; k += kScThreads) task(k);  // rare
+    };
+    // previous round's pending words: q | slot << 11 (kNoPend: none); resolved into a stage index
+    // (ps) or, in a skewed round, written directly into the plan's further halves
+    constexpr uint32_t kNoPend = 0xFFFFFFFFu;
+    uint32_t pq[kScE], pw[kScE], pp[kScE], ps[kScE];
+    bool     pskew = false;
+#pragma unroll
+    for (int j = 0; j < kScE; j++) pq[j] = kNoPend;
+    auto resolve_pending = [&]() {
+#pragma unroll
+        for (int j = 0; j < kScE; j++) {
+            const bool     ok = pq[j] != kNoPend;
+            const uint32_t qq = ok ? pq[j] & 2047u : 0u, sl = pq[j] >> 11;
+            uint32_t       nh = 1, Bk = 0;
+            if (pskew) {
+                const uint32_t b = pl1[qq];
+                nh = b >> 22;
+                Bk = b & ((1u << 22) - 1u);
+            }
+            const uint32_t k      = sl >> 4;
+            const bool     direct = ok && pskew && k < nh;
+            const uint32_t o      = direct ? ((Bk + k) * 16 + (sl & 15u)) * 4 : kOob;
+            __builtin_amdgcn_raw_buffer_store_b32(pw[j], rpool, o, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(pp[j], rppool, o, 0, 0);
+            ps[j] = ok && !direct ? qq * kPayDepth + sl - nh * kPayDepth : dummy;
+        }
+    };
+    auto write_pending = [&]() {
+#pragma unroll
+        for (int j = 0; j < kScE; j++) {
+            stw[ps[j]] = pw[j];
+            stp[ps[j]] = pp[j];
+        }
+    };
+
+    v2u RA[kScE];
+    load_round(0, RA);
+    auto round = [&](uint32_t base) {
+        const bool full = base + kScRound <= len;  // uniform
+        uint32_t   q[kScE], w[kScE], p[kScE];
+#pragma unroll
+        for (int j = 0; j < kScE; j++) {
+            sc_word_lds0<SRC_TUPLES, MODE, FMT>(RA[j].x, P.g, crc_tab, w[j], q[j]);
+            p[j] = RA[j].y;
+            if ((j % HWBRJ_SC_SB) == HWBRJ_SC_SB - 1) __builtin_amdgcn_sched_barrier(0);
+        }
+        if (!full) {
+#pragma unroll
+            for (int j = 0; j < kScE; j++)
+                if (base + j * kScThreads + tid >= len) q[j] = F;  // invalid: ranked on the dummy counter
+        }
+        load_round(base + kScRound, RA);
+        flush_copy();
+        resolve_pending();
+        if (tid == 0) {
+            misc[1 + par]        = 0;
+            misc[3 + (par ^ 1u)] = 0;
+        }
+        bool sk = false;  // a slot >= 31: some partition reaches 32 words this round
+#pragma unroll
+        for (int j = 0; j < kScE; j++) {
+            q[j] |= atomicAdd(&fill[q[j]], 1u) << 11;
+            sk |= q[j] >= (31u << 11) && (q[j] & 2047u) < F;
+        }
+        if (__builtin_amdgcn_ballot_w64(sk) != 0 && lane == 0) misc[3 + par] = 1u;
+        __syncthreads();  // B1: last plan copied out, pending resolved; every rank taken
+        write_pending();
+        const bool skew = __builtin_amdgcn_readfirstlane(misc[3 + par]) != 0;
+#pragma unroll
+        for (int j = 0; j < kScE; j++) {
+            const uint32_t qq = q[j] & 2047u, sl = q[j] >> 11;
+            const bool     ok = full || qq < F;
+            const uint32_t a  = ok && sl < kPayDepth ? qq * kPayDepth + sl : dummy;
+            stw[a] = w[j];
+            stp[a] = p[j];
+            pq[j]  = ok && sl >= kPayDepth ? q[j] : kNoPend;
+            pw[j]  = w[j];
+            pp[j]  = p[j];
+        }
+        pskew = skew;
+        {  // one thread per partition (F <= 1024): flush plan
+            const uint32_t qq   = tid;
+            const uint32_t f    = qq < F ? fill[qq] : 0u;
+            const uint32_t nh   = f >> 4;
+            const uint32_t cs   = qq < F ? cst[qq] : 0u;
+            const uint32_t hcur = cs & 1u;
+            const uint32_t newc = nh ? ((hcur + nh + 1u) >> 1) - hcur : 0u;  // chunks to allocate
+            const uint32_t v    = newc | (nh ? (1u << 16) : 0u);
+            const uint32_t incl = wave_incl_scan_dpp(v);
+            const uint32_t tot  = __builtin_amdgcn_readlane(incl, 63);
+            uint32_t       wbc = 0, wbf = 0;
+            if (lane == 0 && tot) {
+                wbc = atomicAdd(&misc[0], tot & 0xFFFFu);
+                wbf = atomicAdd(&misc[1 + par], tot >> 16);
+            }
+            wbc = __builtin_amdgcn_readfirstlane(wbc);
+            wbf = __builtin_amdgcn_readfirstlane(wbf);
+            if (nh) {
+                const uint32_t cb = wbc + (incl & 0xFFFFu) - newc;
+                const uint32_t H0 = hcur ? cs | 1u : cb * 2u;  // (cs = chunk << 1 | 1)
+                const uint32_t Bk = cb * 2u - hcur;            // half of further half k: Bk + k
+                pl0[qq] = H0;
+                pl1[qq] = Bk | (nh << 22);
+                flq[wbf + (incl >> 16) - 1] = qq;
+                fill[qq] = f & (kPayDepth - 1u);
+                tel[qq] += nh * kPayDepth;
+                for (uint32_t k = 1; k < nh; k++)  // chunks completed by a direct half
+                    if ((Bk + k) & 1u) meta[(Bk + k) >> 1] = qq | (32u << 16);
+                const uint32_t Hl = nh == 1 ? H0 : Bk + nh - 1u;  // last half written
+                cst[qq] = (Hl & 1u) ? 0u : (Hl | 1u);
+            }
+        }
+        __syncthreads();  // B2: plan visible
+        par ^= 1u;
+    };
+    for (uint32_t base = 0; base < len; base += kScRound) round(base);
+    // ---- tail: last plan, the last pending words, then every partial stage as a partial half
+    {
+        flush_copy();
+        resolve_pending();
+        __syncthreads();
+        write_pending();
+        __syncthreads();
+        {
+            const uint32_t qq   = tid;
+            const uint32_t f    = qq < F ? fill[qq] : 0u;
+            const uint32_t cs   = qq < F ? cst[qq] : 0u;
+            const uint32_t hcur = cs & 1u;
+            const uint32_t need = f > 0 && !hcur ? 1u : 0u;
+            const uint32_t incl = wave_incl_scan_dpp(need);
+            const uint32_t tot  = __builtin_amdgcn_readlane(incl, 63);
+            uint32_t       wb   = 0;
+            if (lane == 0 && tot) wb = atomicAdd(&misc[0], tot);
+            wb = __builtin_amdgcn_readfirstlane(wb);
+            if (f > 0 || hcur) {
+                const uint32_t ch = hcur ? cs >> 1 : wb + incl - 1u;
+                meta[ch] = qq | ((hcur * kPayDepth + f) << 16);
+                pl0[qq]  = ch * 2u + hcur;
+                tel[qq] += f;
+            }
+        }
+        __syncthreads();
+        for (uint32_t k = tid; k < F * 4; k += kScThreads) {
+            const uint32_t qq = k >> 2, l4 = k & 3;
+            const uint32_t o  = fill[qq] > 0 ? (pl0[qq] * 16 + l4 * 4) * 4 : kOob;
+            __builtin_amdgcn_raw_buffer_store_b128(*(const v4u*) &stw[qq * kPayDepth + l4 * 4], rpool, o, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b128(*(const v4u*) &stp[qq * kPayDepth + l4 * 4], rppool, o, 0, 0);
+        }
+        __syncthreads();
+        if (tid == 0) P.wg_used[wg] = misc[0];
+        for (uint32_t qq = tid; qq < F; qq += kScThreads) {
+            P.wgq_chunks[wg * F + qq] = (tel[qq] + 31u) >> 5;
+            P.wgq_elems[wg * F + qq]  = tel[qq];
+        }
+    }
+}
+
 // ====================================================== K4: planning scan and chunk lists
 // List entries carry the chunk's element count, so consumers never read `meta`:
 //   entry = chunk_id | (count & 31) << kListIdBits   (count 32 is stored as 0)
@@ -1011,7 +1264,8 @@ __global__ __launch_bounds__(kLfThreads) void k_list_fill(const uint32_t* __rest
 template <int NPQ>
 struct Sweep {
     uint4    v[NPQ];
-    uint32_t n[NPQ];  // valid words of this thread's quad (0..4)
+    uint32_t n[NPQ];   // valid words of this thread's quad (0..4)
+    uint32_t id[NPQ];  // list entries' chunk ids (load_chunks_u; read by the materializing probe)
 };
 
 template <int NPQ>
@@ -1067,7 +1321,8 @@ __device__ __forceinline__ void load_chunks_u(const uint32_t* __restrict__ pool,
             S.v[j] = *(const uint4*) &pool[(uint64_t) (ent[j] & kListIdMask) * 32 + l8 * 4];
         const uint32_t cnt   = lb + cslot + (uint32_t) j * 128u < le ? list_count(ent[j]) : 0u;
         const uint32_t first = l8 * 4;
-        S.n[j] = cnt > first ? min(cnt - first, 4u) : 0u;
+        S.n[j]  = cnt > first ? min(cnt - first, 4u) : 0u;
+        S.id[j] = ent[j] & kListIdMask;
     }
 }
 
@@ -1094,7 +1349,9 @@ constexpr int      kBPQ    = HWBRJ_BPQ;       // sweeps per group (chunk quads p
 constexpr uint32_t kBSweep = 128u;            // chunks per sweep (8 threads per chunk)
 constexpr uint32_t kBSlot  = kBSweep * 32u;   // out_codes words per sweep (4096)
 
-template <int KIND>
+// PAY (materialization): the payload of every R word (ppool, same chunk positions) is written to
+// out_pay at the word's sorted position.
+template <int KIND, bool PAY = false>
 __global__ __launch_bounds__(1024) void k_build(BuildParams P) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const Geometry& g      = P.g;
@@ -1120,16 +1377,18 @@ __global__ __launch_bounds__(1024) void k_build(BuildParams P) {
         __syncthreads();
         const bool  last = seg + 1 == nseg;
         uint32_t    eA[kBPQ], eB[kBPQ];
-        Sweep<kBPQ> SA, SB;
+        Sweep<kBPQ> SA, SB, PA, PB;  // words; payloads (PAY)
         if (l0 < l1) {
             load_list_u<kBPQ>(P.list, l0, l1, eA);
             load_chunks_u<kBPQ>(P.pool, eA, l0, l1, SA);
+            if (PAY) load_chunks_u<kBPQ>(P.ppool, eA, l0, l1, PA);
         }
         for (uint32_t lb = l0; lb < l1; lb += GRP) {
             const uint32_t nb = min(lb + GRP, l1 - 1u);  // next group (re-reads the last entry past the end)
             const uint32_t ne = min(nb + GRP, l1);
             load_list_u<kBPQ>(P.list, nb, ne, eB);
             load_chunks_u<kBPQ>(P.pool, eB, nb, ne, SB);
+            if (PAY) load_chunks_u<kBPQ>(P.ppool, eB, nb, ne, PB);
 #pragma unroll
             for (int jj = 0; jj < kBPQ; jj++) {
                 const uint32_t sb = lb + (uint32_t) jj * kBSweep;  // first list position of the sweep
@@ -1183,7 +1442,10 @@ __global__ __launch_bounds__(1024) void k_build(BuildParams P) {
                 for (int t = 0; t < 4; t++) {
                     const uint32_t sub = (c[t] >> g.sub_shift) & (NSUB - 1u);
                     const uint32_t o   = (uint32_t) __shfl((int) (incl - cs), (int) sub, 64) + rk[t];
-                    if (rk[t] != 0xFFFFFFFFu) stage[o] = c[t];
+                    if (rk[t] != 0xFFFFFFFFu) {
+                        stage[o] = c[t];
+                        if (PAY) P.out_pay[(uint64_t) sw * kBSlot + o] = sweep_word(PA, jj, t);
+                    }
                 }
                 nsw++;
                 __syncthreads();  // B3: the sweep is sorted
@@ -1194,6 +1456,7 @@ __global__ __launch_bounds__(1024) void k_build(BuildParams P) {
             for (int jj = 0; jj < kBPQ; jj++) {
                 SA.v[jj] = SB.v[jj];
                 SA.n[jj] = SB.n[jj];
+                if (PAY) PA.v[jj] = PB.v[jj];
                 eA[jj]   = eB[jj];
             }
         }
@@ -1240,7 +1503,9 @@ __device__ __forceinline__ uint32_t find_q(const uint32_t* item_start, uint32_t 
 // covers list positions [lq0 + p * CH, min(lq1, lq0 + (p + 1) * CH)). Survivors of an item are
 // written at seg * surv_seg_stride + lb * 32 (lb = first list position of the piece).
 
-template <int KIND, bool SEG1>
+// PAY (materialization): every survivor's chunk position goes to surv_pos beside its code (the
+// words are ranked one by one and stored directly, no LDS stage).
+template <int KIND, bool SEG1, bool PAY = false>
 __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     constexpr uint32_t NT  = 1024;
@@ -1402,7 +1667,7 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
                 // wave ballot compacts the survivors there (no exec masking: the others write a
                 // shared garbage slot). Otherwise no scratch write at all (high selectivity: the
                 // words are ranked one by one, and 12 LDS writes per thread would buy nothing)
-                if (kScrCap > 0 && nsv <= kScrCap) {  // wave-uniform
+                if (!PAY && kScrCap > 0 && nsv <= kScrCap) {  // wave-uniform
                     uint32_t at0 = 0;
 #pragma unroll
                     for (int i = 0; i < NW; i++) {
@@ -1427,7 +1692,7 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
                 nsv = kScrCap + 1;  // (word-by-word ranking)
             }
             // ---- ranks inside the piece's sub runs
-            const bool dense = kScrCap > 0 && nsv <= kScrCap;  // wave-uniform
+            const bool dense = !PAY && kScrCap > 0 && nsv <= kScrCap;  // wave-uniform
             // dense: rank << 16 | sub of scratch entry lane + 64 k (kNoRank: not a survivor); the
             // code itself is re-read from the wave's scratch after the barrier (fewer live VGPRs)
             constexpr uint32_t kNoRank = 0xFFFFFFFFu;
@@ -1525,7 +1790,7 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
             stamp(3);
             uint32_t* __restrict__ out = P.surv + (uint64_t) seg * P.surv_seg_stride + (uint64_t) lb_of(p) * 32;
             const uint32_t buf    = nstep & 1u;
-            const bool     staged = total <= scap;
+            const bool     staged = !PAY && total <= scap;
             uint32_t*      stg    = stage + buf * sstr;
             const auto     ro     = buf_rsrc(out, total * 4);
             if (dense) {
@@ -1545,11 +1810,16 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
                     stg[(pass >> i) & 1u ? o : scap + lane] = c;
                 }
             } else {  // more survivors than a stage buffer holds: scattered global (buffer) stores
+                const auto rpo = buf_rsrc(PAY ? P.surv_pos + (out - P.surv) : nullptr, PAY ? total * 4 : 0u);
 #pragma unroll
                 for (int i = 0; i < NW; i++) {
-                    const uint32_t c = decode_k<KIND>(sweep_word(Sc, i >> 2, i & 3), q, g.log2F);
-                    const uint32_t o = subo[(c >> g.sub_shift) & (NSUB - 1u)] + ((rank2[i / 2] >> (16 * (i & 1))) & 0xFFFFu);
-                    __builtin_amdgcn_raw_buffer_store_b32(c, ro, ((pass >> i) & 1u) ? o * 4 : 0x7FFFFFF0u, 0, 0);
+                    const uint32_t c  = decode_k<KIND>(sweep_word(Sc, i >> 2, i & 3), q, g.log2F);
+                    const uint32_t o  = subo[(c >> g.sub_shift) & (NSUB - 1u)] + ((rank2[i / 2] >> (16 * (i & 1))) & 0xFFFFu);
+                    const uint32_t oo = ((pass >> i) & 1u) ? o * 4 : 0x7FFFFFF0u;
+                    __builtin_amdgcn_raw_buffer_store_b32(c, ro, oo, 0, 0);
+                    if (PAY)
+                        __builtin_amdgcn_raw_buffer_store_b32(Sc.id[i >> 2] * 32u + ((uint32_t) tid & 7u) * 4u + (uint32_t) (i & 3),
+                                                              rpo, oo, 0, 0);
                 }
             }
             stamp(4);
@@ -2010,6 +2280,165 @@ __global__ __launch_bounds__(64) void k_join_sum(const uint64_t* __restrict__ js
     }
 }
 
+// ============================================================ K10m: the materializing join
+// One workgroup per (q, sub) job. The job's R codes and payloads (the sub's runs in q's build
+// sweeps) go into an LDS open-addressing table, one slot per R tuple (linear probing; duplicate
+// keys keep every payload), in pieces of <= kMatPiece tuples. Every survivor of the job walks its
+// probe sequence and appends {R.payload, S.payload} per equal key (bucket_chaining_join under
+// JOIN_RESULT_MATERIALIZE, src/parallel_radix_join_bloom.c:259-329, :307-312); its S payload is
+// read from the S payload pool at the survivor's chunk position. Pairs are staged in LDS and
+// appended with one global atomic per flush.
+constexpr int      kMatThreads = 512;
+constexpr uint32_t kMatLog2T   = 12;
+constexpr uint32_t kMatT       = 1u << kMatLog2T;  // table slots
+constexpr uint32_t kMatPiece   = kMatT / 2;        // R tuples per piece
+constexpr uint32_t kMatStage   = 1024;             // staged pairs
+constexpr uint32_t kMatDesc    = kMatThreads;      // run descriptors per batch
+
+__device__ __forceinline__ uint32_t mat_jslot(uint32_t v) { return (v * 0x9E3779B1u) >> (32 - kMatLog2T); }
+
+// Exclusive prefix of one value per thread over the workgroup (contains barriers).
+__device__ __forceinline__ uint32_t mat_block_scan(uint32_t v, uint32_t* wsum, uint32_t& total) {
+    const int      lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t incl = wave_incl_scan_dpp(v);
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    uint32_t before = 0;
+    total           = 0;
+#pragma unroll
+    for (int w = 0; w < kMatThreads / 64; w++) {
+        const uint32_t x = wsum[w];
+        before += w < wave ? x : 0u;
+        total += x;
+    }
+    __syncthreads();  // (wsum reusable)
+    return before + incl - v;
+}
+
+// the descriptor d of element e: pre[d] <= e < pre[d + 1] (n descriptors)
+__device__ __forceinline__ uint32_t mat_find(const uint32_t* pre, uint32_t n, uint32_t e) {
+    uint32_t lo = 0, hi = n - 1;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        if (pre[mid] <= e) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+}
+
+__global__ __launch_bounds__(kMatThreads) void k_join_mat(MatJoinParams P) {
+    __shared__ uint32_t tk[kMatT], tp[kMatT];  // table: keys (kEmpty: free), R payloads
+    __shared__ uint32_t rpre[kMatDesc + 1], spre[kMatDesc + 1];
+    __shared__ uint64_t rbase[kMatDesc], sbase[kMatDesc];
+    __shared__ uint2    est[kMatStage];
+    __shared__ uint32_t wsum[kMatThreads / 64];
+    __shared__ uint32_t ecnt;
+    __shared__ unsigned long long eoff;
+    const int      tid  = threadIdx.x;
+    const uint32_t NSUB = 1u << P.log2NSUB;
+    const uint32_t job = blockIdx.x, q = job >> P.log2NSUB, s = job & (NSUB - 1u);
+    const uint32_t r0 = P.r_sweep_start[q], r1 = P.r_sweep_start[q + 1];
+    const uint32_t qi0 = P.item_start[q], qi1 = P.item_start[q + 1];
+    if (r0 == r1 || qi0 == qi1) return;  // (uniform) no R or no survivors in q
+    const uint32_t lq0 = P.list_start[q];
+    const uint32_t npc = (qi1 - qi0) / P.nseg;  // probe pieces of q per segment
+    if (tid == 0) ecnt = 0;
+    auto emit = [&](uint32_t rp, uint32_t sp) {
+        const uint32_t i = atomicAdd(&ecnt, 1u);
+        if (i < kMatStage) {
+            est[i] = make_uint2(rp, sp);
+        } else {  // stage full (many duplicate keys): one global append
+            const unsigned long long gi = atomicAdd(P.count, 1ull);
+            if (gi < P.cap) P.out[gi] = make_uint2(rp, sp);
+        }
+    };
+    auto flush = [&]() {  // every thread (uniform)
+        __syncthreads();
+        const uint32_t n = min(ecnt, kMatStage);
+        if (tid == 0) eoff = n ? atomicAdd(P.count, (unsigned long long) n) : 0ull;
+        __syncthreads();
+        const uint64_t b = eoff;
+        for (uint32_t i = tid; i < n; i += kMatThreads)
+            if (b + i < P.cap) P.out[b + i] = est[i];
+        __syncthreads();
+        if (tid == 0) ecnt = 0;
+        __syncthreads();
+    };
+    for (uint32_t rd0 = r0; rd0 < r1; rd0 += kMatDesc) {  // R run descriptors, batch by batch
+        const uint32_t nrd = min(kMatDesc, r1 - rd0);
+        __syncthreads();  // previous descriptors consumed
+        uint32_t c = 0;
+        if ((uint32_t) tid < nrd) {
+            const uint64_t r = (uint64_t) (rd0 + tid) * NSUB + s;
+            c          = P.r_cnt[r];
+            rbase[tid] = (uint64_t) (rd0 + tid) * P.slot + P.r_off[r];
+        }
+        uint32_t       rtot;
+        const uint32_t rx = mat_block_scan(c, wsum, rtot);
+        if ((uint32_t) tid < nrd) rpre[tid] = rx;
+        if (tid == 0) rpre[nrd] = rtot;
+        __syncthreads();
+        for (uint32_t pb = 0; pb < rtot; pb += kMatPiece) {
+            const uint32_t pe = min(rtot, pb + kMatPiece);
+            for (uint32_t i = tid; i < kMatT; i += kMatThreads) tk[i] = kEmpty;
+            __syncthreads();
+            for (uint32_t e = pb + tid; e < pe; e += kMatThreads) {
+                const uint32_t d = mat_find(rpre, nrd, e);
+                const uint64_t a = rbase[d] + (e - rpre[d]);
+                const uint32_t v = P.r_codes[a] >> P.hash_shift;
+                uint32_t       h = mat_jslot(v);
+                while (atomicCAS(&tk[h], kEmpty, v) != kEmpty) h = (h + 1) & (kMatT - 1);
+                tp[h] = P.r_pay[a];
+            }
+            __syncthreads();
+            for (uint32_t sd0 = qi0; sd0 < qi1; sd0 += kMatDesc) {  // survivor runs of the job
+                const uint32_t nsd = min(kMatDesc, qi1 - sd0);
+                uint32_t       sc  = 0;
+                if ((uint32_t) tid < nsd) {
+                    const uint32_t it = sd0 + tid, local = it - qi0;
+                    const uint32_t seg = local / npc, piece = local - seg * npc;
+                    sc         = P.surv_cnt[(uint64_t) it * NSUB + s];
+                    sbase[tid] = (uint64_t) seg * P.surv_seg_stride + (uint64_t) (lq0 + piece * P.CH) * 32 +
+                                 P.surv_off[(uint64_t) it * NSUB + s];
+                }
+                uint32_t       stot;
+                const uint32_t sx = mat_block_scan(sc, wsum, stot);
+                if ((uint32_t) tid < nsd) spre[tid] = sx;
+                if (tid == 0) spre[nsd] = stot;
+                __syncthreads();
+                for (uint32_t e0 = 0; e0 < stot; e0 += kMatThreads) {
+                    const uint32_t e = e0 + tid;
+                    if (e < stot) {
+                        const uint32_t d = mat_find(spre, nsd, e);
+                        const uint64_t a = sbase[d] + (e - spre[d]);
+                        const uint32_t v = P.surv[a] >> P.hash_shift;
+                        uint32_t       spay = 0;
+                        bool           got  = false;
+                        for (uint32_t h = mat_jslot(v);; h = (h + 1) & (kMatT - 1)) {
+                            const uint32_t k = tk[h];
+                            if (k == kEmpty) break;
+                            if (k == v) {
+                                if (!got) {
+                                    spay = P.s_pay[P.surv_pos[a]];
+                                    got  = true;
+                                }
+                                emit(tp[h], spay);
+                            }
+                        }
+                    }
+                    __syncthreads();
+                    if (ecnt >= kMatStage - kMatThreads) flush();  // (uniform: read after the barrier)
+                }
+                __syncthreads();  // before the next descriptors
+            }
+        }
+    }
+    flush();
+}
+
+void launch_join_mat(const MatJoinParams& p, uint32_t jobs, hipStream_t st) {
+    k_join_mat<<<jobs, kMatThreads, 0, st>>>(p);
+}
+
 // ============================================== K11: export the filter in reference layout
 // Output word o holds reference bits 32*o .. 32*o+31 (src/bloom_filter.c byte addressing).
 __global__ void k_export(const uint32_t* slices, Geometry g, uint32_t* out, uint64_t nwords) {
@@ -2345,8 +2774,36 @@ static void scatter_inst(const ScatterParams& p, int side, uint32_t grid, hipStr
     else k_scatter_s<SRC, MODE, FMT><<<grid, kScThreads, lds, st>>>(p);
 }
 
+size_t scatter_pay_lds_bytes(uint32_t log2F) {
+    const size_t F = (size_t) 1 << log2F;
+    return (2 * (F * kPayDepth + 64) + F + 4 + 5 * F + 8) * sizeof(uint32_t);  // (+512 B static)
+}
+
+template <int MODE, int FMT>
+__global__ __launch_bounds__(kScThreads) void k_scatter_rp(ScatterParams P) { scatter_body_pay<MODE, FMT>(P); }
+template <int MODE, int FMT>
+__global__ __launch_bounds__(kScThreads) void k_scatter_sp(ScatterParams P) { scatter_body_pay<MODE, FMT>(P); }
+
+template <int MODE, int FMT>
+static void scatter_pay_inst(const ScatterParams& p, int side, uint32_t grid, hipStream_t st) {
+    const size_t lds = scatter_pay_lds_bytes(p.g.log2F);
+    const void*  fn  = side == SIDE_R ? (const void*) &k_scatter_rp<MODE, FMT> : (const void*) &k_scatter_sp<MODE, FMT>;
+    (void) hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds);
+    if (side == SIDE_R) k_scatter_rp<MODE, FMT><<<grid, kScThreads, lds, st>>>(p);
+    else k_scatter_sp<MODE, FMT><<<grid, kScThreads, lds, st>>>(p);
+}
+
 void launch_scatter(const ScatterParams& p, int src, int side, uint32_t grid, hipStream_t st) {
     const Geometry& g = p.g;
+    if (p.ppool) {  // tuples with payloads (materialization): no FMT_C22, no global-mode codes
+        switch (g.mode) {
+            case MODE_SLICE_BLOCK:
+                if (g.format == FMT_PACKED) return scatter_pay_inst<MODE_SLICE_BLOCK, FMT_PACKED>(p, side, grid, st);
+                return scatter_pay_inst<MODE_SLICE_BLOCK, FMT_CODE>(p, side, grid, st);
+            case MODE_SLICE_BASIC: return scatter_pay_inst<MODE_SLICE_BASIC, FMT_CODE>(p, side, grid, st);
+            default: return scatter_pay_inst<MODE_NOBLOOM, FMT_CODE>(p, side, grid, st);
+        }
+    }
     if (src == SRC_CODES) return scatter_inst<SRC_CODES, MODE_GLOBAL, FMT_CODE>(p, side, grid, st);
     switch (g.mode) {
         case MODE_SLICE_BLOCK:
@@ -2403,12 +2860,27 @@ static int probe_kind(const Geometry& g) {
 
 template <int KIND>
 static void build_inst(const BuildParams& p, uint32_t F, size_t lds, hipStream_t st) {
+    if (p.ppool) {
+        (void) hipFuncSetAttribute((const void*) &k_build<KIND, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds);
+        k_build<KIND, true><<<F, 1024, lds, st>>>(p);
+        return;
+    }
     (void) hipFuncSetAttribute((const void*) &k_build<KIND>, hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds);
     k_build<KIND><<<F, 1024, lds, st>>>(p);
 }
 
 template <int KIND>
 static void probe_inst(const ProbeParams& p, uint32_t grid, size_t lds, hipStream_t st) {
+    if (p.surv_pos) {
+        if (KIND == KIND_PASS || p.g.nseg == 1) {
+            (void) hipFuncSetAttribute((const void*) &k_probe<KIND, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds);
+            k_probe<KIND, true, true><<<grid, 1024, lds, st>>>(p);
+        } else {
+            (void) hipFuncSetAttribute((const void*) &k_probe<KIND, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds);
+            k_probe<KIND, false, true><<<grid, 1024, lds, st>>>(p);
+        }
+        return;
+    }
     if (KIND == KIND_PASS || p.g.nseg == 1) {  // one slice segment per partition: no per-word segment check
         (void) hipFuncSetAttribute((const void*) &k_probe<KIND, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds);
         k_probe<KIND, true><<<grid, 1024, lds, st>>>(p);

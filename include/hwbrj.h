@@ -137,9 +137,11 @@ int hwbrj_join_wait(hwbrj_stats_t * stats);
 
 /* The join with result materialization (the reference's JOIN_RESULT_MATERIALIZE output,
  * src/parallel_radix_join_bloom.c:307-312): d_out[i] = {R.payload, S.payload} of every match, in
- * no particular order. Runs the counting join (stats) and then the pairs pass; capacity is in
- * pairs. Returns 7 with *n_out = the match count when capacity is too small.
- * ms_materialize (optional) receives the pairs pass's device time. */
+ * no particular order. One pass of the partitioned pipeline with every tuple's payload carried
+ * beside its word (stats: its counts and phase times); the global-bitmap configurations (basic
+ * k = 0, B < 8) run the counting join and a pairs pass instead. capacity is in pairs; with too
+ * small a capacity the first `capacity` pairs are written and 7 is returned with *n_out = the
+ * match count. ms_materialize (optional) receives the device time of the pairs' production. */
 int hwbrj_join_materialize_device(const tuple_t * d_R, uint64_t nR, const tuple_t * d_S,
                                   uint64_t nS, const bloom_filter_args_t * args, tuple_t * d_out,
                                   uint64_t capacity, uint64_t * n_out, void * stream,
