@@ -203,7 +203,10 @@ bool plan_geometry(const bloom_filter_args_t* a, uint64_t nR, Geometry* g, std::
     const uint64_t rper = (nR + F - 1) / F;
     uint32_t       l2s  = 0;
     g->sub_shift  = (g->mode == MODE_SLICE_BASIC) ? 0 : g->log2F;
-    if (mat) {  // k_join_mat: a table of <= 2048 R tuples per piece, so ~1536 per job on average
+    if (mat && g->sub_shift > 0) {  // k_join_mat's bitmap path: keys v < 2^17, <= 4096 R tuples per job
+        l2s = g->log2F >= 15 ? 0 : std::min<uint32_t>(6, 15 - g->log2F);
+        while (l2s < 6 && (rper >> l2s) > 4000) l2s++;
+    } else if (mat) {  // its hash table: <= 2048 R tuples per piece, so ~1536 per job on average
         while (l2s < 6 && (rper >> l2s) > 1536) l2s++;
     } else if (g->sub_shift > 0 && g->log2F + 6 >= 14) {
         l2s = g->log2F >= 14 ? 0 : 14 - g->log2F;
@@ -493,7 +496,7 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     pp.filtered        = d_filtered;
     pp.job_surv        = jparts.as<uint32_t>() + NJ;
     pp.surv_pos        = mat ? survpos.as<uint32_t>() : nullptr;
-    const size_t   pl_lds = probe_lds_bytes(g, nullptr);
+    const size_t   pl_lds = probe_lds_bytes(g, nullptr, mat != nullptr);
     const uint32_t PG = (uint32_t) cus_ * (uint32_t) std::max<size_t>(1, std::min<size_t>(2, 163840 / pl_lds));
     const bool dbg_on = dbg;  // dev-only phase stamps (HWBRJ_DBG)
     if (dbg_on) {
@@ -553,6 +556,7 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
         mp.CH              = CH;
         mp.log2NSUB        = g.log2NSUB;
         mp.hash_shift      = g.hash_shift;
+        mp.bm              = (g.sub_shift > 0 && 32 - g.hash_shift <= 17) ? 1u : 0u;
         mp.s_pay           = ppoolS.as<uint32_t>();
         mp.out             = mat->out;
         mp.cap             = mat->cap;

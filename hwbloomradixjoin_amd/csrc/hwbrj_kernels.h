@@ -110,6 +110,8 @@ struct MatJoinParams {
     const uint32_t* list_start;
     uint64_t        surv_seg_stride;
     uint32_t        nseg, CH, log2NSUB, hash_shift;
+    uint32_t        bm;             // 1: job keys v = code >> hash_shift < 2^17 (the bitmap path)
+    uint32_t        xcd8;           // 1: XCD-aware job order (F a multiple of 8; set by launch_join_mat)
     const uint32_t* s_pay;          // S payload pool (ScatterParams::ppool of the S pass)
     uint2*          out;
     uint64_t        cap;
@@ -145,7 +147,7 @@ bool   launch_plan(const uint32_t* wgq_chunks, const uint32_t* wgq_elems, uint32
                    uint32_t log2F, uint32_t* wgq_off, uint32_t* colc, uint64_t* cole,
                    hipStream_t st);
 uint32_t probe_chunks_per_item();
-size_t   probe_lds_bytes(const Geometry& g, uint32_t* stage_cap);
+size_t   probe_lds_bytes(const Geometry& g, uint32_t* stage_cap, bool pay = false);
 size_t slice_lds_bytes(const Geometry& g);
 uint32_t build_chunks_per_sweep();  // R chunks per k_build sweep
 uint32_t build_sweep_slot();        // out_codes words per k_build sweep

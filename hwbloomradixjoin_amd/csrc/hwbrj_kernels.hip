@@ -827,7 +827,7 @@ __device__ __forceinline__ void scatter_body(const ScatterParams& P) {
 // Result materialization (JOIN_RESULT_MATERIALIZE, src/parallel_radix_join_bloom.c:307-312) needs
 // every tuple's payload where its word lands: `ppool` shares the chunk layout of `pool`, so a
 // survivor names its payload by chunk position. The LDS stage holds words and payloads of
-// kPayDepth = 16 slots per partition (2 x 64 KiB at F = 1024): a stage line is half a chunk, and
+// kPayDepth = 16 {word, payload} slots per partition (128 KiB at F = 1024): a stage line is half a chunk, and
 // a partition's chunk is written as two 64-byte halves, rounds apart. Chunk ids are taken when a
 // chunk's first half is flushed; per partition cst = current chunk << 1 | 1 while only its first
 // half is written (0: none). Halves are numbered chunk * 2 + half: a plan sends the stage line to
@@ -837,7 +837,11 @@ __device__ __forceinline__ void scatter_body(const ScatterParams& P) {
 // resolved against the plan before the next round's first barrier. All chunks but a partition's
 // last are full, so the per-partition chunk count is ceil(elements / 32).
 constexpr uint32_t kPayDepth = 16;
-constexpr int      kScKP     = 2;  // flush tasks per thread per round (4 per half: 16 B of words + of payloads)
+#ifndef HWBRJ_SC_KP
+#define HWBRJ_SC_KP 3
+#endif
+constexpr int      kScKP     = HWBRJ_SC_KP;  // flush tasks per thread per round (4 per half: 16 B of
+                                             // words + of payloads); ~512 halves per round on average
 typedef unsigned int v2u __attribute__((ext_vector_type(2)));
 
 template <int MODE, int FMT>
@@ -845,10 +849,9 @@ __device__ __forceinline__ void scatter_body_pay(const ScatterParams& P) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     __shared__ uint32_t crc_tab[128];
     const uint32_t F     = 1u << P.g.log2F;
-    const uint32_t SL    = F * kPayDepth + 64;  // stage words (+ 64 per-lane dummy slots)
-    uint32_t*      stw   = lds;                 // words
-    uint32_t*      stp   = stw + SL;            // payloads
-    uint32_t*      fill  = stp + SL;            // F + 4 (entry F: invalid elements)
+    const uint32_t SL    = F * kPayDepth + 64;  // stage slots (+ 64 per-lane dummy slots)
+    uint2*         stg   = (uint2*) lds;        // {word, payload} per slot
+    uint32_t*      fill  = lds + 2 * SL;        // F + 4 (entry F: invalid elements)
     uint32_t*      pl0   = fill + F + 4;        // F: half index of the stage line's flush
     uint32_t*      pl1   = pl0 + F;             // F: Bk | nh << 22
     uint32_t*      cst   = pl1 + F;             // F: current chunk << 1 | 1, or 0
@@ -887,6 +890,11 @@ __device__ __forceinline__ void scatter_body_pay(const ScatterParams& P) {
     const auto rmeta  = buf_rsrc(meta, (uint32_t) (P.cap * 4));
     __syncthreads();
 
+#ifdef HWBRJ_ABL_SPLITH  // dev ablation (results invalid): second halves in a separate array
+    auto hword = [&](uint32_t H) { return (H & 1u) * (uint32_t) (P.cap * 16) + (H >> 1) * 16u; };
+#else
+    auto hword = [&](uint32_t H) { return H * 16u; };  // word offset of half H in the region
+#endif
     auto load_round = [&](uint32_t base, v2u (&R)[kScE]) {  // {key, payload} as one 8-byte load
         if (base + kScRound <= len) {
 #pragma unroll
@@ -909,10 +917,16 @@ __device__ __forceinline__ void scatter_body_pay(const ScatterParams& P) {
             const uint32_t qq = flq[ok ? k >> 2 : 0];
             const uint32_t l4 = k & 3;
             const uint32_t H  = pl0[qq];
-            const v4u      vw = *(const v4u*) &stw[qq * kPayDepth + l4 * 4];
-            const v4u      vp = *(const v4u*) &stp[qq * kPayDepth + l4 * 4];
-            const uint32_t o  = ok ? (H * 16 + l4 * 4) * 4 : kOob;
+            const v4u      x0 = *(const v4u*) &stg[qq * kPayDepth + l4 * 4];
+            const v4u      x1 = *(const v4u*) &stg[qq * kPayDepth + l4 * 4 + 2];
+            v4u            vw, vp;  // (de-interleave)
+            vw.x = x0.x; vw.y = x0.z; vw.z = x1.x; vw.w = x1.z;
+            vp.x = x0.y; vp.y = x0.w; vp.z = x1.y; vp.w = x1.w;
+            const uint32_t o  = ok ? (hword(H) + l4 * 4) * 4 : kOob;
             __builtin_amdgcn_raw_buffer_store_b128(vw, rpool, o, 0, 0);
+#ifdef HWBRJ_ABL_PNOPST  // dev ablation (results invalid): no payload stores
+            if (vp.x == 0x12345678u && vp.y == 0x9abcdef0u)
+#endif
             __builtin_amdgcn_raw_buffer_store_b128(vp, rppool, o, 0, 0);
             __builtin_amdgcn_raw_buffer_store_b32(qq | (32u << 16), rmeta, ok && l4 == 0 && (H & 1u) ? (H >> 1) * 4 : kOob, 0, 0);
         };
@@ -940,18 +954,17 @@ __device__ __forceinline__ void scatter_body_pay(const ScatterParams& P) {
             }
             const uint32_t k      = sl >> 4;
             const bool     direct = ok && pskew && k < nh;
-            const uint32_t o      = direct ? ((Bk + k) * 16 + (sl & 15u)) * 4 : kOob;
-            __builtin_amdgcn_raw_buffer_store_b32(pw[j], rpool, o, 0, 0);
-            __builtin_amdgcn_raw_buffer_store_b32(pp[j], rppool, o, 0, 0);
+            if (pskew) {  // (uniform; a skewed round is rare, so the waits it costs are too)
+                const uint32_t o = direct ? (hword(Bk + k) + (sl & 15u)) * 4 : kOob;
+                __builtin_amdgcn_raw_buffer_store_b32(pw[j], rpool, o, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b32(pp[j], rppool, o, 0, 0);
+            }
             ps[j] = ok && !direct ? qq * kPayDepth + sl - nh * kPayDepth : dummy;
         }
     };
     auto write_pending = [&]() {
 #pragma unroll
-        for (int j = 0; j < kScE; j++) {
-            stw[ps[j]] = pw[j];
-            stp[ps[j]] = pp[j];
-        }
+        for (int j = 0; j < kScE; j++) stg[ps[j]] = make_uint2(pw[j], pp[j]);
     };
 
     v2u RA[kScE];
@@ -991,9 +1004,7 @@ __device__ __forceinline__ void scatter_body_pay(const ScatterParams& P) {
         for (int j = 0; j < kScE; j++) {
             const uint32_t qq = q[j] & 2047u, sl = q[j] >> 11;
             const bool     ok = full || qq < F;
-            const uint32_t a  = ok && sl < kPayDepth ? qq * kPayDepth + sl : dummy;
-            stw[a] = w[j];
-            stp[a] = p[j];
+            stg[ok && sl < kPayDepth ? qq * kPayDepth + sl : dummy] = make_uint2(w[j], p[j]);
             pq[j]  = ok && sl >= kPayDepth ? q[j] : kNoPend;
             pw[j]  = w[j];
             pp[j]  = p[j];
@@ -1063,9 +1074,14 @@ __device__ __forceinline__ void scatter_body_pay(const ScatterParams& P) {
         __syncthreads();
         for (uint32_t k = tid; k < F * 4; k += kScThreads) {
             const uint32_t qq = k >> 2, l4 = k & 3;
-            const uint32_t o  = fill[qq] > 0 ? (pl0[qq] * 16 + l4 * 4) * 4 : kOob;
-            __builtin_amdgcn_raw_buffer_store_b128(*(const v4u*) &stw[qq * kPayDepth + l4 * 4], rpool, o, 0, 0);
-            __builtin_amdgcn_raw_buffer_store_b128(*(const v4u*) &stp[qq * kPayDepth + l4 * 4], rppool, o, 0, 0);
+            const uint32_t o  = fill[qq] > 0 ? (hword(pl0[qq]) + l4 * 4) * 4 : kOob;
+            const v4u      x0 = *(const v4u*) &stg[qq * kPayDepth + l4 * 4];
+            const v4u      x1 = *(const v4u*) &stg[qq * kPayDepth + l4 * 4 + 2];
+            v4u            vw, vp;
+            vw.x = x0.x; vw.y = x0.z; vw.z = x1.x; vw.w = x1.z;
+            vp.x = x0.y; vp.y = x0.w; vp.z = x1.y; vp.w = x1.w;
+            __builtin_amdgcn_raw_buffer_store_b128(vw, rpool, o, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b128(vp, rppool, o, 0, 0);
         }
         __syncthreads();
         if (tid == 0) P.wg_used[wg] = misc[0];
@@ -1529,9 +1545,10 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
     uint32_t*       subow  = subc + 3 * 128;  // 16 waves x NSUB: each wave's copy of the offsets
     constexpr uint32_t kScrCap = scr_cap<KIND>();
     constexpr int      kDense  = kScrCap / 64 > 0 ? kScrCap / 64 : 1;
-    uint32_t*       scratch = subow + 16 * NSUB;  // 16 waves x kScrCap: compacted survivors
-    uint32_t*       scrdum = scratch + 16 * kScrCap;  // 64 dummy slots shared by all waves
+    uint32_t*       scratch = subow + 16 * NSUB;  // 16 waves x kScrCap: compacted survivors (not PAY)
+    uint32_t*       scrdum = scratch + (PAY ? 0u : 16 * kScrCap);  // 64 dummy slots shared by all waves
     uint32_t*       stage  = scrdum + 64;             // 2 x sstr, double-buffered by item
+    const uint32_t  hp     = scap / 2;                // PAY: codes at [0, hp), positions at [hp, scap)
     const int       tid    = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     load_tab(inv, &P.tabs->inv[0][0]);
     for (uint32_t i = tid; i < 3 * 128; i += NT) subc[i] = 0;
@@ -1563,11 +1580,22 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
         const uint32_t nbytes = ((prev_total + 3u) & ~3u) * 4u;  // item region holds round_up(total, 4)
         const auto     ro     = buf_rsrc(prev_out, nbytes);
         const v4u*     src    = (const v4u*) (stage + prev_buf * sstr);
+        if (PAY) {  // codes and their chunk positions (half a stage buffer each)
+            const auto rp = buf_rsrc(P.surv_pos + (prev_out - P.surv), nbytes);
+#pragma unroll
+            for (int k = 0; k < (kPC + 1) / 2; k++) {
+                const uint32_t i = tid + k * NT;
+                const uint32_t j = min(i, hp / 4 - 1);  // reads past the half are never stored
+                __builtin_amdgcn_raw_buffer_store_b128(src[j], ro, i * 16, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b128(src[hp / 4 + j], rp, i * 16, 0, 0);
+            }
+        } else {
 #pragma unroll
         for (int k = 0; k < kPC; k++) {
             const uint32_t i = tid + k * NT;
             const v4u      v = src[min(i, scap / 4 - 1)];  // reads past the stage are never stored
             __builtin_amdgcn_raw_buffer_store_b128(v, ro, i * 16, 0, 0);
+        }
         }
         const uint32_t tb = prev_it == kNoItem ? 0u : NSUB * 4;  // run table (wave 0 holds it)
         const auto rc = buf_rsrc(P.surv_cnt + (uint64_t) (prev_it & ~kNoItem) * NSUB, tb);
@@ -1790,7 +1818,7 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
             stamp(3);
             uint32_t* __restrict__ out = P.surv + (uint64_t) seg * P.surv_seg_stride + (uint64_t) lb_of(p) * 32;
             const uint32_t buf    = nstep & 1u;
-            const bool     staged = !PAY && total <= scap;
+            const bool     staged = PAY ? total <= hp : total <= scap;
             uint32_t*      stg    = stage + buf * sstr;
             const auto     ro     = buf_rsrc(out, total * 4);
             if (dense) {
@@ -1808,6 +1836,9 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
                     const uint32_t c = decode_k<KIND>(sweep_word(Sc, i >> 2, i & 3), q, g.log2F);
                     const uint32_t o = subo[(c >> g.sub_shift) & (NSUB - 1u)] + ((rank2[i / 2] >> (16 * (i & 1))) & 0xFFFFu);
                     stg[(pass >> i) & 1u ? o : scap + lane] = c;
+                    if (PAY)  // the survivor's chunk position beside it
+                        stg[(pass >> i) & 1u ? hp + o : scap + lane] =
+                            Sc.id[i >> 2] * 32u + ((uint32_t) tid & 7u) * 4u + (uint32_t) (i & 3);
                 }
             } else {  // more survivors than a stage buffer holds: scattered global (buffer) stores
                 const auto rpo = buf_rsrc(PAY ? P.surv_pos + (out - P.surv) : nullptr, PAY ? total * 4 : 0u);
@@ -2283,17 +2314,22 @@ __global__ __launch_bounds__(64) void k_join_sum(const uint64_t* __restrict__ js
 // ============================================================ K10m: the materializing join
 // One workgroup per (q, sub) job. The job's R codes and payloads (the sub's runs in q's build
 // sweeps) go into an LDS open-addressing table, one slot per R tuple (linear probing; duplicate
-// keys keep every payload), in pieces of <= kMatPiece tuples. Every survivor of the job walks its
-// probe sequence and appends {R.payload, S.payload} per equal key (bucket_chaining_join under
-// JOIN_RESULT_MATERIALIZE, src/parallel_radix_join_bloom.c:259-329, :307-312); its S payload is
-// read from the S payload pool at the survivor's chunk position. Pairs are staged in LDS and
-// appended with one global atomic per flush.
+// keys keep every payload), in pieces of <= kMatPiece tuples. The job's survivors are taken
+// kMatPiece at a time: every thread loads its kMatU codes at once and counts their matches in the
+// table; a workgroup scan gives every match its output row (one global atomic per batch); then the
+// matching survivors' chunk positions and S payloads are gathered, kMatU loads in flight, and the
+// {R.payload, S.payload} pairs written (bucket_chaining_join under JOIN_RESULT_MATERIALIZE,
+// src/parallel_radix_join_bloom.c:259-329, :307-312).
 constexpr int      kMatThreads = 512;
+constexpr int      kMatU       = 4;                    // elements per thread per batch
 constexpr uint32_t kMatLog2T   = 12;
-constexpr uint32_t kMatT       = 1u << kMatLog2T;  // table slots
-constexpr uint32_t kMatPiece   = kMatT / 2;        // R tuples per piece
-constexpr uint32_t kMatStage   = 1024;             // staged pairs
-constexpr uint32_t kMatDesc    = kMatThreads;      // run descriptors per batch
+constexpr uint32_t kMatT       = 1u << kMatLog2T;      // table slots
+constexpr uint32_t kMatPiece   = kMatThreads * kMatU;  // R tuples per piece, survivors per batch
+constexpr uint32_t kMatDesc    = 128;                  // run descriptors per batch
+constexpr int      kMatUB      = 8;                    // bitmap path: elements per thread per batch
+constexpr uint32_t kMatRCap    = kMatThreads * kMatUB; // bitmap path: R tuples of a job (at most)
+constexpr uint32_t kMatBmWords = 1u << (17 - 5);       // bitmap path: keys v < 2^17
+static_assert(2 * kMatPiece == kMatT, "the table is at most half full");
 
 __device__ __forceinline__ uint32_t mat_jslot(uint32_t v) { return (v * 0x9E3779B1u) >> (32 - kMatLog2T); }
 
@@ -2325,44 +2361,252 @@ __device__ __forceinline__ uint32_t mat_find(const uint32_t* pre, uint32_t n, ui
     return lo;
 }
 
-__global__ __launch_bounds__(kMatThreads) void k_join_mat(MatJoinParams P) {
-    __shared__ uint32_t tk[kMatT], tp[kMatT];  // table: keys (kEmpty: free), R payloads
+// insert an R tuple (linear probing, one slot per tuple)
+__device__ __forceinline__ void mat_insert1(uint32_t* tk, uint32_t* tp, uint32_t v, uint32_t pay) {
+    uint32_t h = mat_jslot(v);
+    while (atomicCAS(&tk[h], kEmpty, v) != kEmpty) h = (h + 1) & (kMatT - 1);
+    tp[h] = pay;
+}
+
+// matches of kMatU survivor keys (v = kEmpty: none)
+__device__ __forceinline__ void mat_count(const uint32_t* tk, const uint32_t (&v)[kMatU], uint32_t (&m)[kMatU]) {
+#pragma unroll
+    for (int k = 0; k < kMatU; k++) {
+        m[k] = 0;
+        if (v[k] != kEmpty)
+            for (uint32_t h = mat_jslot(v[k]);; h = (h + 1) & (kMatT - 1)) {
+                const uint32_t x = tk[h];
+                if (x == kEmpty) break;
+                m[k] += x == v[k] ? 1u : 0u;
+            }
+    }
+}
+
+// Bitmap path (unique R keys v < 2^17, the blocked / sectorized join's jobs): every R key sets its
+// bit (ds_or_rtn; a bit already set means duplicate keys, and the job takes the hash table);
+// a prefix popcount per 64-bit word ranks the keys, and the R payloads are stored by rank. A
+// survivor costs a bit test, and a match two more LDS reads: no probe sequences, no CAS.
+__global__ __launch_bounds__(kMatThreads) __attribute__((amdgpu_waves_per_eu(8))) void k_join_mat(MatJoinParams P) {
+    // LDS union: hash table {keys (kEmpty: free) [kMatT], R payloads [kMatT]}, or the bitmap path's
+    // {bitmap [kMatBmWords], rank prefix per 64-bit word (u16) [kMatBmWords / 2], payloads [kMatRCap]}
+    __shared__ __attribute__((aligned(16))) uint32_t smem[kMatBmWords + kMatBmWords / 4 + kMatRCap];
+    static_assert(kMatBmWords + kMatBmWords / 4 + kMatRCap >= 2 * kMatT, "LDS union");
+    uint32_t* tk = smem;
+    uint32_t* tp = smem + kMatT;
+    __shared__ uint32_t dupf;
     __shared__ uint32_t rpre[kMatDesc + 1], spre[kMatDesc + 1];
     __shared__ uint64_t rbase[kMatDesc], sbase[kMatDesc];
-    __shared__ uint2    est[kMatStage];
     __shared__ uint32_t wsum[kMatThreads / 64];
-    __shared__ uint32_t ecnt;
-    __shared__ unsigned long long eoff;
+    __shared__ unsigned long long obase;
     const int      tid  = threadIdx.x;
-    const uint32_t NSUB = 1u << P.log2NSUB;
-    const uint32_t job = blockIdx.x, q = job >> P.log2NSUB, s = job & (NSUB - 1u);
+    const uint32_t NSUB = 1u << P.log2NSUB, hs = P.hash_shift;
+    // XCD-aware order: workgroups are dealt round-robin to the 8 XCDs, so the jobs of partition q
+    // (which read the same R sweeps and S payload lines) all go to XCD q mod 8 and share its L2
+    uint32_t job = blockIdx.x;
+    if (P.xcd8) {
+        const uint32_t x = blockIdx.x & 7u, l = blockIdx.x >> 3;
+        job = ((((l >> P.log2NSUB) << 3) | x) << P.log2NSUB) | (l & (NSUB - 1u));
+    }
+    const uint32_t q = job >> P.log2NSUB, s = job & (NSUB - 1u);
     const uint32_t r0 = P.r_sweep_start[q], r1 = P.r_sweep_start[q + 1];
     const uint32_t qi0 = P.item_start[q], qi1 = P.item_start[q + 1];
     if (r0 == r1 || qi0 == qi1) return;  // (uniform) no R or no survivors in q
     const uint32_t lq0 = P.list_start[q];
     const uint32_t npc = (qi1 - qi0) / P.nseg;  // probe pieces of q per segment
-    if (tid == 0) ecnt = 0;
-    auto emit = [&](uint32_t rp, uint32_t sp) {
-        const uint32_t i = atomicAdd(&ecnt, 1u);
-        if (i < kMatStage) {
-            est[i] = make_uint2(rp, sp);
-        } else {  // stage full (many duplicate keys): one global append
-            const unsigned long long gi = atomicAdd(P.count, 1ull);
-            if (gi < P.cap) P.out[gi] = make_uint2(rp, sp);
+    auto s_desc = [&](uint32_t it, uint32_t& cnt, uint64_t& base) {  // survivor run of item it
+        const uint32_t local = it - qi0, seg = local / npc, piece = local - seg * npc;
+        cnt  = P.surv_cnt[(uint64_t) it * NSUB + s];
+        base = (uint64_t) seg * P.surv_seg_stride + (uint64_t) (lq0 + piece * P.CH) * 32 +
+               P.surv_off[(uint64_t) it * NSUB + s];
+    };
+    // ---- single-shot form (the usual job): every descriptor in one batch, R in one piece, the
+    // survivors in one batch; R and S descriptors, then R tuples and survivor codes, are loaded
+    // together, so the job costs four dependent global round trips
+    if (r1 - r0 <= kMatDesc && qi1 - qi0 <= kMatDesc) {  // (uniform)
+        const uint32_t nrd = r1 - r0, nsd = qi1 - qi0;
+#ifdef HWBRJ_ABL_MJ_EMPTY  // dev ablation (results invalid): descriptors only
+        if (nrd != 0x12345) {
+            uint32_t c0 = (uint32_t) tid < nrd ? P.r_cnt[(uint64_t) (r0 + tid) * NSUB + s] : 0u, t0;
+            c0 = mat_block_scan(c0, wsum, t0);
+            if (t0 == 0x12345678u) P.out[0] = make_uint2(c0, 0);
+            return;
         }
-    };
-    auto flush = [&]() {  // every thread (uniform)
-        __syncthreads();
-        const uint32_t n = min(ecnt, kMatStage);
-        if (tid == 0) eoff = n ? atomicAdd(P.count, (unsigned long long) n) : 0ull;
-        __syncthreads();
-        const uint64_t b = eoff;
-        for (uint32_t i = tid; i < n; i += kMatThreads)
-            if (b + i < P.cap) P.out[b + i] = est[i];
-        __syncthreads();
-        if (tid == 0) ecnt = 0;
-        __syncthreads();
-    };
+#endif
+        uint32_t       rcn = 0, scn = 0;
+        if ((uint32_t) tid < nrd) {
+            const uint64_t r = (uint64_t) (r0 + tid) * NSUB + s;
+            rcn        = P.r_cnt[r];
+            rbase[tid] = (uint64_t) (r0 + tid) * P.slot + P.r_off[r];
+        }
+        if ((uint32_t) tid < nsd) s_desc(qi0 + tid, scn, sbase[tid]);
+        uint32_t       rtot, stot;
+        const uint32_t rx = mat_block_scan(rcn, wsum, rtot);
+        const uint32_t sx = mat_block_scan(scn, wsum, stot);
+        if ((uint32_t) tid < nrd) rpre[tid] = rx;
+        if ((uint32_t) tid < nsd) spre[tid] = sx;
+        if (tid == 0) {
+            rpre[nrd] = rtot;
+            spre[nsd] = stot;
+            dupf      = 0;
+        }
+        if (P.bm && rtot <= kMatRCap) {  // (uniform) ---- bitmap path
+            uint32_t*       bmw = smem;
+            uint16_t*       pfx = (uint16_t*) (smem + kMatBmWords);
+            uint32_t*       rpy = smem + kMatBmWords + kMatBmWords / 4;
+            const uint64_t* bm64 = (const uint64_t*) smem;
+            for (uint32_t i = tid; i < kMatBmWords; i += kMatThreads) bmw[i] = 0;
+            __syncthreads();  // descriptors visible, bitmap cleared
+            uint32_t rv[kMatUB], rp[kMatUB];
+#pragma unroll
+            for (int k = 0; k < kMatUB; k++) {
+                const uint32_t e = tid + k * kMatThreads;
+                rv[k] = kEmpty;
+                if (e < rtot) {
+                    const uint32_t d  = mat_find(rpre, nrd, e);
+                    const uint64_t ra = rbase[d] + (e - rpre[d]);
+                    rv[k] = P.r_codes[ra] >> hs;
+                    rp[k] = P.r_pay[ra];
+                }
+            }
+            uint32_t dup = 0;
+#pragma unroll
+            for (int k = 0; k < kMatUB; k++)
+                if (rv[k] != kEmpty) dup |= (atomicOr(&bmw[rv[k] >> 5], 1u << (rv[k] & 31u)) >> (rv[k] & 31u)) & 1u;
+            if (dup) dupf = 1;
+            __syncthreads();
+            if (!dupf) {  // (uniform)
+                // rank prefix: thread t owns 64-bit words 4t .. 4t + 3
+                uint32_t c4[4], c = 0;
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    c4[j] = (uint32_t) __builtin_popcountll(bm64[tid * 4 + j]);
+                    c += c4[j];
+                }
+                uint32_t       ntot;
+                uint32_t       run = mat_block_scan(c, wsum, ntot);
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    pfx[tid * 4 + j] = (uint16_t) run;
+                    run += c4[j];
+                }
+                __syncthreads();
+                auto rank = [&](uint32_t v) {
+                    const uint64_t w = bm64[v >> 6];
+                    return (uint32_t) pfx[v >> 6] + (uint32_t) __builtin_popcountll(w & ((1ull << (v & 63u)) - 1ull));
+                };
+#pragma unroll
+                for (int k = 0; k < kMatUB; k++)
+                    if (rv[k] != kEmpty) rpy[rank(rv[k])] = rp[k];
+                __syncthreads();  // payloads by rank complete
+                for (uint32_t e0 = 0; e0 < stot; e0 += kMatRCap) {  // survivors, batch by batch
+                    uint64_t a[kMatUB];
+                    uint32_t v[kMatUB], hit = 0;
+#pragma unroll
+                    for (int k = 0; k < kMatUB; k++) {
+                        const uint32_t e = e0 + tid + k * kMatThreads;
+                        v[k] = kEmpty;
+                        a[k] = 0;
+                        if (e < stot) {
+                            const uint32_t d = mat_find(spre, nsd, e);
+                            a[k] = sbase[d] + (e - spre[d]);
+                            v[k] = P.surv[a[k]] >> hs;
+                        }
+                    }
+#pragma unroll
+                    for (int k = 0; k < kMatUB; k++)
+                        if (v[k] != kEmpty) hit |= ((bmw[v[k] >> 5] >> (v[k] & 31u)) & 1u) << k;
+                    uint32_t pos[kMatUB], sp[kMatUB];
+#pragma unroll
+                    for (int k = 0; k < kMatUB; k++) pos[k] = (hit >> k) & 1u ? P.surv_pos[a[k]] : 0u;
+                    uint32_t       tot;
+                    const uint32_t off = mat_block_scan((uint32_t) __builtin_popcount(hit), wsum, tot);
+                    if (tot == 0) continue;  // (uniform)
+                    if (tid == 0) obase = atomicAdd(P.count, (unsigned long long) tot);
+#pragma unroll
+                    for (int k = 0; k < kMatUB; k++) sp[k] = (hit >> k) & 1u ? P.s_pay[pos[k]] : 0u;
+                    __syncthreads();
+                    uint64_t o = obase + off;
+#pragma unroll
+                    for (int k = 0; k < kMatUB; k++) {
+                        if (!((hit >> k) & 1u)) continue;
+                        if (o < P.cap) P.out[o] = make_uint2(rpy[rank(v[k])], sp[k]);
+                        o++;
+                    }
+                }
+                return;
+            }
+            // duplicate R keys: the hash table (over the same LDS)
+        }
+        if (rtot <= kMatPiece && stot <= kMatPiece) {  // (uniform)
+            __syncthreads();  // descriptors visible; the bitmap path is done with the LDS
+            for (uint32_t i = tid; i < kMatT; i += kMatThreads) tk[i] = kEmpty;
+            __syncthreads();
+            uint32_t rc[kMatU], rp[kMatU], v[kMatU], m[kMatU];
+            uint64_t a[kMatU];
+#pragma unroll
+            for (int k = 0; k < kMatU; k++) {
+                const uint32_t e = tid + k * kMatThreads;
+                if (e < rtot) {
+#ifdef HWBRJ_ABL_MJ_NOLOAD  // dev ablation (results invalid): no R loads
+                    rc[k] = e * 2654435761u;
+                    rp[k] = e;
+#else
+                    const uint32_t d  = mat_find(rpre, nrd, e);
+                    const uint64_t ra = rbase[d] + (e - rpre[d]);
+                    rc[k] = P.r_codes[ra];
+                    rp[k] = P.r_pay[ra];
+#endif
+                }
+                v[k] = kEmpty;
+                a[k] = 0;
+                if (e < stot) {
+                    const uint32_t d = mat_find(spre, nsd, e);
+                    a[k] = sbase[d] + (e - spre[d]);
+                    v[k] = P.surv[a[k]] >> hs;
+                }
+            }
+#ifdef HWBRJ_ABL_MJ_NOINS  // dev ablation (results invalid): R loaded, not inserted
+            if (rc[0] + rc[1] + rc[2] + rc[3] + rp[0] + rp[1] + rp[2] + rp[3] == 0x12345678u) P.out[0] = make_uint2(0, 0);
+            return;
+#endif
+#pragma unroll
+            for (int k = 0; k < kMatU; k++)
+                if (tid + k * kMatThreads < rtot) mat_insert1(tk, tp, rc[k] >> hs, rp[k]);
+            __syncthreads();  // table complete
+#ifdef HWBRJ_ABL_MJ_R  // dev ablation (results invalid): R table only
+            if (v[0] != 0x12345678u) return;
+#endif
+            mat_count(tk, v, m);
+            uint32_t cnt = 0;
+#pragma unroll
+            for (int k = 0; k < kMatU; k++) cnt += m[k];
+            uint32_t pos[kMatU], sp[kMatU];
+#pragma unroll
+            for (int k = 0; k < kMatU; k++) pos[k] = m[k] ? P.surv_pos[a[k]] : 0u;  // (in flight over the scan)
+            uint32_t       tot;
+            const uint32_t off = mat_block_scan(cnt, wsum, tot);
+            if (tot == 0) return;  // (uniform)
+            if (tid == 0) obase = atomicAdd(P.count, (unsigned long long) tot);
+#pragma unroll
+            for (int k = 0; k < kMatU; k++) sp[k] = m[k] ? P.s_pay[pos[k]] : 0u;
+            __syncthreads();
+            uint64_t o = obase + off;
+#pragma unroll
+            for (int k = 0; k < kMatU; k++) {
+                if (!m[k]) continue;
+                for (uint32_t h = mat_jslot(v[k]);; h = (h + 1) & (kMatT - 1)) {
+                    const uint32_t x = tk[h];
+                    if (x == kEmpty) break;
+                    if (x == v[k]) {
+                        if (o < P.cap) P.out[o] = make_uint2(tp[h], sp[k]);
+                        o++;
+                    }
+                }
+            }
+            return;
+        }
+    }
+    // ---- general form: R descriptor batches x R pieces x survivor batches
     for (uint32_t rd0 = r0; rd0 < r1; rd0 += kMatDesc) {  // R run descriptors, batch by batch
         const uint32_t nrd = min(kMatDesc, r1 - rd0);
         __syncthreads();  // previous descriptors consumed
@@ -2379,63 +2623,84 @@ __global__ __launch_bounds__(kMatThreads) void k_join_mat(MatJoinParams P) {
         __syncthreads();
         for (uint32_t pb = 0; pb < rtot; pb += kMatPiece) {
             const uint32_t pe = min(rtot, pb + kMatPiece);
+            __syncthreads();  // the previous piece's survivors are done with the table
             for (uint32_t i = tid; i < kMatT; i += kMatThreads) tk[i] = kEmpty;
-            __syncthreads();
-            for (uint32_t e = pb + tid; e < pe; e += kMatThreads) {
-                const uint32_t d = mat_find(rpre, nrd, e);
-                const uint64_t a = rbase[d] + (e - rpre[d]);
-                const uint32_t v = P.r_codes[a] >> P.hash_shift;
-                uint32_t       h = mat_jslot(v);
-                while (atomicCAS(&tk[h], kEmpty, v) != kEmpty) h = (h + 1) & (kMatT - 1);
-                tp[h] = P.r_pay[a];
+            uint32_t rc[kMatU], rp[kMatU];  // this thread's R tuples of the piece (loads in flight)
+#pragma unroll
+            for (int k = 0; k < kMatU; k++) {
+                const uint32_t e = pb + tid + k * kMatThreads;
+                rc[k] = kEmpty;
+                if (e < pe) {
+                    const uint32_t d = mat_find(rpre, nrd, e);
+                    const uint64_t a = rbase[d] + (e - rpre[d]);
+                    rc[k] = P.r_codes[a];
+                    rp[k] = P.r_pay[a];
+                }
             }
-            __syncthreads();
+            __syncthreads();  // table cleared
+#pragma unroll
+            for (int k = 0; k < kMatU; k++)
+                if (pb + tid + k * kMatThreads < pe) mat_insert1(tk, tp, rc[k] >> hs, rp[k]);
             for (uint32_t sd0 = qi0; sd0 < qi1; sd0 += kMatDesc) {  // survivor runs of the job
                 const uint32_t nsd = min(kMatDesc, qi1 - sd0);
-                uint32_t       sc  = 0;
-                if ((uint32_t) tid < nsd) {
-                    const uint32_t it = sd0 + tid, local = it - qi0;
-                    const uint32_t seg = local / npc, piece = local - seg * npc;
-                    sc         = P.surv_cnt[(uint64_t) it * NSUB + s];
-                    sbase[tid] = (uint64_t) seg * P.surv_seg_stride + (uint64_t) (lq0 + piece * P.CH) * 32 +
-                                 P.surv_off[(uint64_t) it * NSUB + s];
-                }
+                __syncthreads();  // table complete; previous descriptors consumed
+                uint32_t sc = 0;
+                if ((uint32_t) tid < nsd) s_desc(sd0 + tid, sc, sbase[tid]);
                 uint32_t       stot;
                 const uint32_t sx = mat_block_scan(sc, wsum, stot);
                 if ((uint32_t) tid < nsd) spre[tid] = sx;
                 if (tid == 0) spre[nsd] = stot;
                 __syncthreads();
-                for (uint32_t e0 = 0; e0 < stot; e0 += kMatThreads) {
-                    const uint32_t e = e0 + tid;
-                    if (e < stot) {
-                        const uint32_t d = mat_find(spre, nsd, e);
-                        const uint64_t a = sbase[d] + (e - spre[d]);
-                        const uint32_t v = P.surv[a] >> P.hash_shift;
-                        uint32_t       spay = 0;
-                        bool           got  = false;
-                        for (uint32_t h = mat_jslot(v);; h = (h + 1) & (kMatT - 1)) {
-                            const uint32_t k = tk[h];
-                            if (k == kEmpty) break;
-                            if (k == v) {
-                                if (!got) {
-                                    spay = P.s_pay[P.surv_pos[a]];
-                                    got  = true;
-                                }
-                                emit(tp[h], spay);
+                for (uint32_t e0 = 0; e0 < stot; e0 += kMatPiece) {
+                    uint64_t a[kMatU];
+                    uint32_t v[kMatU], m[kMatU];
+#pragma unroll
+                    for (int k = 0; k < kMatU; k++) {
+                        const uint32_t e = e0 + tid + k * kMatThreads;
+                        a[k] = ~0ull;
+                        v[k] = kEmpty;
+                        if (e < stot) {
+                            const uint32_t d = mat_find(spre, nsd, e);
+                            a[k] = sbase[d] + (e - spre[d]);
+                            v[k] = P.surv[a[k]] >> hs;
+                        }
+                    }
+                    mat_count(tk, v, m);
+                    uint32_t cnt = 0;
+#pragma unroll
+                    for (int k = 0; k < kMatU; k++) cnt += m[k];
+                    uint32_t       tot;
+                    const uint32_t off = mat_block_scan(cnt, wsum, tot);
+                    if (tot == 0) continue;  // (uniform)
+                    if (tid == 0) obase = atomicAdd(P.count, (unsigned long long) tot);
+                    __syncthreads();
+                    uint64_t o = obase + off;
+                    uint32_t pos[kMatU], sp[kMatU];
+#pragma unroll
+                    for (int k = 0; k < kMatU; k++) pos[k] = m[k] ? P.surv_pos[a[k]] : 0u;
+#pragma unroll
+                    for (int k = 0; k < kMatU; k++) sp[k] = m[k] ? P.s_pay[pos[k]] : 0u;
+#pragma unroll
+                    for (int k = 0; k < kMatU; k++) {
+                        if (!m[k]) continue;
+                        for (uint32_t h = mat_jslot(v[k]);; h = (h + 1) & (kMatT - 1)) {
+                            const uint32_t x = tk[h];
+                            if (x == kEmpty) break;
+                            if (x == v[k]) {
+                                if (o < P.cap) P.out[o] = make_uint2(tp[h], sp[k]);
+                                o++;
                             }
                         }
                     }
-                    __syncthreads();
-                    if (ecnt >= kMatStage - kMatThreads) flush();  // (uniform: read after the barrier)
                 }
-                __syncthreads();  // before the next descriptors
             }
         }
     }
-    flush();
 }
 
-void launch_join_mat(const MatJoinParams& p, uint32_t jobs, hipStream_t st) {
+void launch_join_mat(const MatJoinParams& p0, uint32_t jobs, hipStream_t st) {
+    MatJoinParams p = p0;
+    p.xcd8          = ((jobs >> p.log2NSUB) % 8 == 0 && !getenv("HWBRJ_DEV_NOXCD")) ? 1u : 0u;
     k_join_mat<<<jobs, kMatThreads, 0, st>>>(p);
 }
 
@@ -2903,22 +3168,23 @@ void launch_build(const BuildParams& p, uint32_t F, hipStream_t st) {
 }
 
 // Probe LDS: slice segment + tables + a survivor stage using what is left of the CU's 160 KiB.
-size_t probe_lds_bytes(const Geometry& g, uint32_t* stage_cap) {
+size_t probe_lds_bytes(const Geometry& g, uint32_t* stage_cap, bool pay) {
     const bool   slices = g.mode == MODE_SLICE_BLOCK || g.mode == MODE_SLICE_BASIC;
     const size_t NSUB   = (size_t) 1 << g.log2NSUB;
     const int    kind   = probe_kind(g);
-    const size_t scap   = kind == KIND_BLOCK_PKK || kind == KIND_BASIC_KK || kind == KIND_BLOCK_ZK
+    const size_t scap   = pay ? 0 : kind == KIND_BLOCK_PKK || kind == KIND_BASIC_KK || kind == KIND_BLOCK_ZK
                               ? scr_cap<KIND_BLOCK_PKK>() : scr_cap<KIND_PASS>();
     const size_t base   = ((slices ? g.seg_words : 0) + 3 * 128 + 16 * NSUB + 16 * scap + 64) * sizeof(uint32_t);
     // 2 buffers of cap words + 64 dummy slots each, in what the 512-byte static table leaves
-    size_t cap = std::min<size_t>(kProbeCH * 32, (163840 - 512 - base) / 8 - 64) & ~(size_t) 3;
+    // (pay: codes and positions, half a buffer each)
+    size_t cap = std::min<size_t>(kProbeCH * 32, (163840 - 512 - base) / 8 - 64) & ~(size_t) 7;
     if (stage_cap) *stage_cap = (uint32_t) cap;
     return base + 2 * (cap + 64) * 4;
 }
 
 void launch_probe(const ProbeParams& p0, uint32_t grid, hipStream_t st) {
     ProbeParams p = p0;
-    const size_t lds = probe_lds_bytes(p.g, &p.stage_cap);
+    const size_t lds = probe_lds_bytes(p.g, &p.stage_cap, p.surv_pos != nullptr);
     switch (probe_kind(p.g)) {
         case KIND_BLOCK_Z1: return probe_inst<KIND_BLOCK_Z1>(p, grid, lds, st);
         case KIND_BLOCK_ZK: return probe_inst<KIND_BLOCK_ZK>(p, grid, lds, st);
