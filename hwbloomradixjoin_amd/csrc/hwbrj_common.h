@@ -92,6 +92,9 @@ enum Mode : int {
                             // LDS slices (k >= 2:
                             // bits 2..k of the first-bit candidates from the global bitmap)
     MODE_GLOBAL       = 3,  // basic k = 0 or B < 8: global atomics build + direct probe (fallback)
+    // scatter modes of basic k >= 2's repartitioning passes (words = bmix(key) in, SRC_CODES):
+    MODE_BASIC_BITJ   = 4,  // partition = the slice of bit j (Geometry::bitj) of add_basic; word kept
+    MODE_CODE_OF_KEY  = 5,  // partition = code & (F-1), word = code = crc32c(42, key) (join layout)
 };
 
 enum Format : int {
@@ -126,6 +129,7 @@ struct Geometry {
     uint32_t log2secw;     // sectorized: log2(min(B, 64))
     uint32_t nsecmask;     // sectorized: B / secw - 1
     int      s_format;     // element format of the S partitions (format: the R partitions)
+    uint32_t bitj;         // MODE_BASIC_BITJ / k_probe_bitj: which bit of add_basic's sequence (0-based)
 };
 
 // Consumer-kernel specializations (selected on the host from Geometry).
@@ -158,6 +162,17 @@ HWBRJ_HD uint32_t ilog2u(uint64_t v) {
 // h_{i+1} = (h_i + y_i) & (size-1), y_{i+1} = (y_i + i + 1) & (size-1). `size` arrives as uint32
 // and is widened (mod_m), so size = 0 means "no masking".
 HWBRJ_HD uint32_t mod_m(uint32_t v, uint32_t size) { return (uint32_t) (v & ((uint64_t) size - 1ull)); }
+
+// Bit j (0-based) of add_basic's sequence for key (src/bloom_filter.c:73-111): the position in
+// the whole m-bit filter.
+HWBRJ_HD uint32_t basic_bit(uint32_t key, uint32_t j, uint32_t msz) {
+    uint32_t h = mod_m(crapwow(kSeed, key), msz), y = mod_m(key + kSeed, msz);
+    for (uint32_t i = 0; i < j; i++) {
+        h = mod_m(h + y, msz);
+        y = mod_m(y + i + 1u, msz);
+    }
+    return h;
+}
 
 // SECTORIZED (the build's extension): bit i of the sequence is moved into 64-bit sector
 // (s0 + i) mod nsec, s0 = sector of the first bit. k = 1 is bit-identical to BLOCKED.

@@ -260,7 +260,7 @@ void Engine::release() {
                       &istartS, &listS, &slices, &bitmap, &rjoin, &rrun, &surv, &survcnt, &survoff,
                       &dense, &small, &bpos, &colR, &colS, &mtab, &mcount, &jtask, &jparts, &pjList,
                       &pjLstart, &pjSweep, &pjTab, &pjRegion, &pjTot, &pjSoff, &pjIbase, &pjCnt, &pjOff,
-                      &pjIstart, &pjJobs, &ppoolR, &ppoolS, &rpay, &survpos})
+                      &pjIstart, &pjJobs, &ppoolR, &ppoolS, &rpay, &survpos, &dense2, &kkcnt})
         b->release();
     have_filter_ = false;
 }
@@ -306,6 +306,12 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     if (mat && g.mode == MODE_GLOBAL) {
         set_last_error("global-bitmap mode: materialized by the side pass");
         return kRcMatGlobal;
+    }
+    if (!mat && g.mode == MODE_SLICE_BASIC && g.k > 1 && (uint64_t) g.k * nR <= (1ull << 31) &&
+        !getenv("HWBRJ_DEV_KK_GATHER")) {
+        if (!stream) stream = own_stream_;
+        if (pending_) HWBRJ_CHECK(hipStreamWaitEvent(stream, ev_[8], 0));
+        return enqueue_basic_kk(dR, nR, dS, nS, g, stream, jkind);
     }
     if (!stream) stream = own_stream_;
     // Every join on this device shares this Engine's scratch (pools, lists, slices, counters):
@@ -593,6 +599,227 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
         fprintf(stderr, "[dbg] probe cyc/WG: top %.0f test %.0f b1 %.0f scan+b2 %.0f write %.0f b3+copy %.0f\n",
                 sp_[0], sp_[1], sp_[2], sp_[3], sp_[4], sp_[5]);
     }
+    return 0;
+}
+
+// Basic k >= 2. A key's k bits lie in k unrelated slices, so the S words are
+// tested one bit per pass: pass j partitions the candidates by the slice of their bit j and tests
+// it in LDS (k_probe_bitj), the passing words (dense) feed pass j + 1's scatter. The survivors of
+// the last pass are re-partitioned by code (MODE_CODE_OF_KEY), the join's layout, so the join
+// takes its bitmap path like the blocked filter's: R is partitioned by code for the join, and the
+// slices are built from R's partitioned bit positions (k_bitpos, k_slice_fill).
+int Engine::enqueue_basic_kk(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
+                             const Geometry& g, hipStream_t stream, int jkind) {
+    Geometry    gj;  // the join layout: R and the survivors partitioned by code
+    std::string err;
+    if (!plan_geometry(nullptr, nR, &gj, &err)) {
+        set_last_error(err);
+        return 2;
+    }
+    const uint32_t F = 1u << g.log2F, Fj = 1u << gj.log2F, Fm = std::max(F, Fj);
+    const uint32_t NSUB = 1u << gj.log2NSUB, NJ = Fj * NSUB;
+    const uint32_t nseg = g.nseg, CH = probe_chunks_per_item();
+    // one workgroup per CU for every scatter and bit pass: pass j's workgroup w writes region w
+    // (rw words) and pass j + 1's scatter workgroup w partitions it
+    const uint32_t G    = (uint32_t) cus_;
+    const uint64_t nRk  = (uint64_t) g.k * nR;
+    const uint64_t Ib   = ((nS / 32 + (uint64_t) G * (Fm + 1)) / CH + Fm + 1) * nseg;  // items of a pass
+    const uint64_t rw   = ((Ib + G - 1) / G) * CH * 32;  // words a pass workgroup may append
+    const uint64_t capR = region_cap(nR, G, Fm);
+    const uint64_t capS = std::max(region_cap(std::max(nS, nRk), G, Fm), rw / 32 + Fm + 1);
+    const uint64_t LR = (uint64_t) G * capR, LS = (uint64_t) G * capS;
+    const uint64_t items_max = (LS / CH + Fm + 1) * nseg;
+    if (G > 512 || LS > (1ull << 27) || LR > (1ull << 27) || capS >= (1u << 22) || capR >= (1u << 22)) {
+        set_last_error("relation too large for 27-bit chunk ids (|S| or |R| > ~4.2e9 tuples per GPU)");
+        return 3;
+    }
+    const uint64_t GF = (uint64_t) G * Fm;
+    bool ok = true;
+    ok &= poolR.ensure(LR * 128) && metaR.ensure(LR * 4) && listR.ensure(LR * 4);
+    ok &= usedR.ensure(G * 4) && wgqcR.ensure(GF * 4) && wgqeR.ensure(GF * 4) && wgqoR.ensure(GF * 4);
+    ok &= lstartR.ensure((Fm + 1) * 4) && estartR.ensure((Fm + 1) * 8) && istartR.ensure((Fm + 1) * 4);
+    ok &= poolS.ensure(LS * 128) && metaS.ensure(LS * 4) && listS.ensure(LS * 4);
+    ok &= usedS.ensure(G * 4) && wgqcS.ensure(GF * 4) && wgqeS.ensure(GF * 4) && wgqoS.ensure(GF * 4);
+    ok &= lstartS.ensure((Fm + 1) * 4) && estartS.ensure((Fm + 1) * 8) && istartS.ensure((Fm + 1) * 4);
+    const uint64_t BSW = build_chunks_per_sweep(), SLOT = build_sweep_slot();
+    const uint64_t sweeps_max = LR / BSW + Fm + 1;
+    ok &= rjoin.ensure(sweeps_max * SLOT * 4) && rrun.ensure(2 * sweeps_max * NSUB * 4);
+    ok &= surv.ensure(LS * 128) && survcnt.ensure(items_max * NSUB * 4) && survoff.ensure(items_max * NSUB * 4);
+    ok &= small.ensure(128 + 64 * 128) && colR.ensure(Fm * 12) && colS.ensure(Fm * 12);
+    const bool jnew = jparts.bytes < (size_t) (2 * NJ + 1) * 4 || NJ != last_nj_;
+    last_nj_ = NJ;
+    ok &= jtask.ensure((size_t) join_extra_tasks() * 8) && jparts.ensure((size_t) (2 * NJ + 1) * 4);
+    ok &= slices.ensure((uint64_t) F * nseg * g.seg_words * 4) && bpos.ensure(nRk * 4);
+    ok &= dense.ensure(G * rw * 4) && dense2.ensure(G * rw * 4) && kkcnt.ensure(64 * 8 + 2 * G * 4);
+    if (!ok) {
+        set_last_error("hipMalloc failed (device memory)");
+        return 4;
+    }
+    uint64_t* d_result   = small.as<uint64_t>();
+    uint64_t* d_filtered = small.as<uint64_t>() + 2;
+    uint64_t* cnt        = kkcnt.as<uint64_t>();  // [j]: candidates after pass j (j < k - 1); [63]: dummy
+    uint32_t* wgc[2]     = {(uint32_t*) (cnt + 64), (uint32_t*) (cnt + 64) + G};  // per-workgroup counts
+    HWBRJ_CHECK(hipMemsetAsync(small.p, 0, 64, stream));
+    HWBRJ_CHECK(hipMemsetAsync(kkcnt.p, 0, kkcnt.bytes, stream));
+    if (jnew) HWBRJ_CHECK(hipMemsetAsync(jparts.p, 0, jparts.bytes, stream));
+    HWBRJ_CHECK(hipMemsetAsync(jparts.as<uint32_t>() + 2 * NJ, 0, 4, stream));
+
+    auto side = [&](bool r) {
+        ScatterParams sp{};
+        sp.tabs       = d_tabs_;
+        sp.pool       = (r ? poolR : poolS).as<uint32_t>();
+        sp.meta       = (r ? metaR : metaS).as<uint32_t>();
+        sp.wg_used    = (r ? usedR : usedS).as<uint32_t>();
+        sp.wgq_chunks = (r ? wgqcR : wgqcS).as<uint32_t>();
+        sp.wgq_elems  = (r ? wgqeR : wgqeS).as<uint32_t>();
+        sp.cap        = r ? capR : capS;
+        return sp;
+    };
+    auto index = [&](bool r, uint32_t log2F, uint32_t ch, uint32_t ns) {
+        const uint32_t Fx = 1u << log2F;
+        DevBuf& col = r ? colR : colS;
+        launch_plan((r ? wgqcR : wgqcS).as<uint32_t>(), (r ? wgqeR : wgqeS).as<uint32_t>(), G, log2F,
+                    (r ? wgqoR : wgqoS).as<uint32_t>(), col.as<uint32_t>() + 2 * Fx, col.as<uint64_t>(), stream);
+        launch_list_fill((r ? metaR : metaS).as<uint32_t>(), (r ? usedR : usedS).as<uint32_t>(), r ? capR : capS,
+                         log2F, (r ? wgqoR : wgqoS).as<uint32_t>(), col.as<uint32_t>() + 2 * Fx, col.as<uint64_t>(),
+                         ch, ns, (r ? lstartR : lstartS).as<uint32_t>(), (r ? estartR : estartS).as<uint64_t>(),
+                         (r ? istartR : istartS).as<uint32_t>(), (r ? listR : listS).as<uint32_t>(), G, stream);
+    };
+
+    HWBRJ_CHECK(hipEventRecord(ev_[0], stream));
+    // ---------------------------------------------------------------- R: the join layout
+    ScatterParams sp = side(true);
+    sp.g   = gj;
+    sp.src = dR;
+    sp.n   = nR;
+    launch_scatter(sp, SRC_TUPLES, SIDE_R, G, stream);
+    HWBRJ_CHECK(hipEventRecord(ev_[1], stream));
+    index(true, gj.log2F, (uint32_t) BSW, 1);
+    HWBRJ_CHECK(hipEventRecord(ev_[2], stream));
+    BuildParams bp{};
+    bp.g           = gj;
+    bp.tabs        = d_tabs_;
+    bp.pool        = poolR.as<uint32_t>();
+    bp.list        = listR.as<uint32_t>();
+    bp.list_start  = lstartR.as<uint32_t>();
+    bp.elem_start  = estartR.as<uint64_t>();
+    bp.sweep_start = istartR.as<uint32_t>();
+    bp.out_codes   = rjoin.as<uint32_t>();
+    bp.run_cnt     = rrun.as<uint32_t>();
+    bp.run_off     = rrun.as<uint32_t>() + sweeps_max * NSUB;
+    launch_build(bp, Fj, stream);
+    // ---------------------------------------------------------------- the filter slices
+    launch_bitpos(dR, nR, g, bpos.as<uint32_t>(), stream);
+    sp     = side(false);
+    sp.g   = g;
+    sp.src = bpos.p;
+    sp.n   = nRk;
+    launch_scatter(sp, SRC_CODES, SIDE_R, G, stream);
+    index(false, g.log2F, (uint32_t) BSW, 1);
+    launch_slice_fill(poolS.as<uint32_t>(), listS.as<uint32_t>(), lstartS.as<uint32_t>(), g,
+                      slices.as<uint32_t>(), stream);
+    HWBRJ_CHECK(hipEventRecord(ev_[3], stream));
+    // ---------------------------------------------------------------- S: by the slice of bit 0
+    sp     = side(false);
+    sp.g   = g;
+    sp.src = dS;
+    sp.n   = nS;
+    launch_scatter(sp, SRC_TUPLES, SIDE_S, G, stream);
+    HWBRJ_CHECK(hipEventRecord(ev_[4], stream));
+    index(false, g.log2F, CH, nseg);
+    HWBRJ_CHECK(hipEventRecord(ev_[5], stream));
+    // ---------------------------------------------------------------- one bit per pass
+    const uint32_t PG = G;
+    ProbeParams    pb{};
+    pb.pool       = poolS.as<uint32_t>();
+    pb.list       = listS.as<uint32_t>();
+    pb.list_start = lstartS.as<uint32_t>();
+    pb.item_start = istartS.as<uint32_t>();
+    pb.slices     = slices.as<uint32_t>();
+    uint32_t* dz[2] = {dense.as<uint32_t>(), dense2.as<uint32_t>()};
+    for (uint32_t j = 0; j < g.k; j++) {
+        Geometry gb = g;
+        gb.bitj     = j;
+        if (j > 0) {  // the candidates of pass j - 1, by the slice of bit j
+            gb.mode       = MODE_BASIC_BITJ;
+            sp            = side(false);
+            sp.g          = gb;
+            sp.src        = dz[(j - 1) & 1];
+            sp.seg_cnt    = wgc[(j - 1) & 1];
+            sp.seg_stride = rw;
+            launch_scatter(sp, SRC_CODES, SIDE_S, G, stream);
+            index(false, g.log2F, CH, nseg);
+        }
+        pb.g               = gb;
+        pb.surv            = dz[j & 1];
+        pb.surv_seg_stride = rw;
+        pb.wg_cnt          = wgc[j & 1];
+        pb.filtered        = j + 1 < g.k ? cnt + j : d_filtered;
+        launch_probe_bitj(pb, PG, stream);
+    }
+    HWBRJ_CHECK(hipEventRecord(ev_[6], stream));
+    // ---------------------------------------------------------------- survivors: the join layout
+    {
+        Geometry gc = gj;
+        gc.mode     = MODE_CODE_OF_KEY;
+        sp          = side(false);
+        sp.g        = gc;
+        sp.src        = dz[(g.k - 1) & 1];
+        sp.seg_cnt    = wgc[(g.k - 1) & 1];
+        sp.seg_stride = rw;
+        launch_scatter(sp, SRC_CODES, SIDE_S, G, stream);
+        index(false, gj.log2F, CH, 1);
+    }
+    ProbeParams pp{};
+    pp.g               = gj;
+    pp.tabs            = d_tabs_;
+    pp.pool            = poolS.as<uint32_t>();
+    pp.list            = listS.as<uint32_t>();
+    pp.list_start      = lstartS.as<uint32_t>();
+    pp.item_start      = istartS.as<uint32_t>();
+    pp.surv            = surv.as<uint32_t>();
+    pp.surv_seg_stride = LS * 32;
+    pp.surv_cnt        = survcnt.as<uint32_t>();
+    pp.surv_off        = survoff.as<uint32_t>();
+    pp.filtered        = cnt + 63;  // (counted by the last bit pass)
+    pp.job_surv        = jparts.as<uint32_t>() + NJ;
+    const size_t   pl_lds = probe_lds_bytes(gj, nullptr);
+    launch_probe(pp, (uint32_t) cus_ * (uint32_t) std::max<size_t>(1, std::min<size_t>(2, 163840 / pl_lds)), stream);
+    HWBRJ_CHECK(hipEventRecord(ev_[7], stream));
+    // -------------------------------------------------------------------------- join
+    JoinParams jp{};
+    jp.r_codes         = rjoin.as<uint32_t>();
+    jp.r_sweep_start   = istartR.as<uint32_t>();
+    jp.r_cnt           = rrun.as<uint32_t>();
+    jp.r_off           = rrun.as<uint32_t>() + sweeps_max * NSUB;
+    jp.slot            = (uint32_t) SLOT;
+    jp.surv            = surv.as<uint32_t>();
+    jp.surv_cnt        = survcnt.as<uint32_t>();
+    jp.surv_off        = survoff.as<uint32_t>();
+    jp.item_start      = istartS.as<uint32_t>();
+    jp.list_start      = lstartS.as<uint32_t>();
+    jp.surv_seg_stride = LS * 32;
+    jp.nseg            = 1;
+    jp.CH              = CH;
+    jp.log2NSUB        = gj.log2NSUB;
+    jp.hash_shift      = gj.hash_shift;
+    jp.bitmap          = (gj.sub_shift > 0 && 32 - gj.hash_shift <= 18) ? 1u : 0u;
+    jp.result          = d_result;
+    jp.jsum            = (uint64_t*) ((char*) small.p + 128);
+    jp.nparts          = jparts.as<uint32_t>();
+    jp.extra           = jtask.as<uint2>();
+    jp.nextra          = jparts.as<uint32_t>() + 2 * NJ;
+    jp.jkind           = (uint32_t) jkind;
+    if (const char* e = getenv("HWBRJ_DEV_JOIN_SPLIT"))
+        jp.split_surv = (uint32_t) strtoul(e, nullptr, 10);
+    launch_join(jp, NJ, jparts.as<uint32_t>() + NJ, stream);
+    HWBRJ_CHECK(hipEventRecord(ev_[8], stream));
+    HWBRJ_CHECK(hipGetLastError());
+    pending_      = true;
+    pending_args_ = true;
+    pending_nS_   = nS;
+    have_filter_  = true;
+    last_g_       = g;
     return 0;
 }
 

@@ -82,6 +82,9 @@ class Engine {
     int          enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
                          const bloom_filter_args_t* args, hipStream_t stream, bool dbg, int jkind,
                          const MatReq* mat = nullptr);
+    // basic k >= 2 without materialization: the repartitioning pipeline (hwbrj_engine.cpp)
+    int          enqueue_basic_kk(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
+                                  const Geometry& g, hipStream_t stream, int jkind);
     CrcTables*   d_tabs_ = nullptr;
     GenPlan*     d_plan_ = nullptr;
     // R side
@@ -95,6 +98,7 @@ class Engine {
     // materializing pipeline: payload pools (chunk layout of poolR / poolS), R payloads of the
     // build sweeps, survivors' chunk positions
     DevBuf ppoolR, ppoolS, rpay, survpos;
+    DevBuf dense2, kkcnt;  // basic k >= 2: the second dense candidate buffer, per-pass counts
     DevBuf jtask, jparts;  // join task table; parts per job (+ the task count)
     // partitioned join: owned partitions' lists, tables and received survivor descriptors
     DevBuf pjList, pjLstart, pjSweep, pjTab, pjRegion, pjTot, pjSoff, pjIbase, pjCnt, pjOff, pjIstart, pjJobs;

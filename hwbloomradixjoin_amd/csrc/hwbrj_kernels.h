@@ -24,6 +24,8 @@ struct ScatterParams {
     uint32_t*        wgq_elems;    // [G][F] elements of partition q in workgroup wg's region
     uint64_t*        dbg;          // dev-only: per-workgroup phase cycles (HWBRJ_DBG), or nullptr
     uint64_t         cap;          // chunk capacity of one workgroup region
+    const uint32_t*  seg_cnt;      // SRC_CODES from per-workgroup segments: workgroup w partitions
+    uint64_t         seg_stride;   // src + w * seg_stride (elements), seg_cnt[w] of them; or nullptr
     Geometry         g;
     const CrcTables* tabs;
 };
@@ -62,6 +64,8 @@ struct ProbeParams {
     uint32_t         stage_cap;   // survivor stage words (set by launch_probe)
     uint32_t*        surv_pos;    // materialization: each survivor's chunk position (its payload's
                                   // index in the S payload pool), parallel to surv; or nullptr
+    uint32_t*        wg_cnt;      // k_probe_bitj: words appended to workgroup w's region
+                                  // (surv + w * surv_seg_stride)
     uint64_t*        dbg;         // dev-only: per-workgroup phase cycles (HWBRJ_DBG), or nullptr
 };
 
@@ -153,6 +157,10 @@ uint32_t build_chunks_per_sweep();  // R chunks per k_build sweep
 uint32_t build_sweep_slot();        // out_codes words per k_build sweep
 void   launch_build(const BuildParams& p, uint32_t F, hipStream_t st);
 void   launch_probe(const ProbeParams& p, uint32_t grid, hipStream_t st);
+// basic k >= 2 (k_probe_bitj): bit g.bitj of the words partitioned by its slice, passing words
+// appended densely to p.surv; p.filtered += their count
+size_t probe_bitj_lds_bytes(const Geometry& g);
+void   launch_probe_bitj(const ProbeParams& p, uint32_t grid, hipStream_t st);
 // splits skewed jobs (job_surv: survivors per job from k_probe, cleared here) and runs the join
 void   launch_join(const JoinParams& p, uint32_t jobs, uint32_t* job_surv, hipStream_t st);
 uint32_t join_extra_tasks();

@@ -418,9 +418,17 @@ template <int SRC, int MODE, int FMT>
 __device__ __forceinline__ void sc_word_lds0(uint32_t x, const Geometry& g, const uint32_t* tab,
                                              uint32_t& w, uint32_t& q) {
     const uint32_t F1 = (1u << g.log2F) - 1u;
-    if (SRC == SRC_CODES) {  // already a code (fallback survivors)
-        w = x;
-        q = x & F1;
+    if (SRC == SRC_CODES) {
+        if (MODE == MODE_BASIC_BITJ) {  // basic k >= 2 candidates: by the slice of their next bit
+            q = basic_bit(bunmix(x), g.bitj, (uint32_t) g.m) & F1;
+            w = x;
+        } else if (MODE == MODE_CODE_OF_KEY) {  // basic k >= 2 survivors: into the join layout
+            w = crc_nib(tab, bunmix(x));
+            q = w & F1;
+        } else {  // already a code (fallback survivors)
+            w = x;
+            q = x & F1;
+        }
         return;
     }
     const uint32_t key  = x;
@@ -541,10 +549,14 @@ __device__ __forceinline__ void scatter_body(const ScatterParams& P) {
     const uint64_t n     = P.n_dev ? *P.n_dev : P.n;
     const uint64_t units = (n + 3) >> 2;
     const uint64_t G = gridDim.x, wg = blockIdx.x;
-    const uint64_t e0  = 4 * (wg * units / G);
+    uint64_t       e0  = 4 * (wg * units / G);
     const uint64_t e1r = 4 * ((wg + 1) * units / G);
     const uint64_t e1  = e1r < n ? e1r : n;
-    const uint32_t len = __builtin_amdgcn_readfirstlane(e1 > e0 ? (uint32_t) (e1 - e0) : 0u);
+    uint32_t       len = __builtin_amdgcn_readfirstlane(e1 > e0 ? (uint32_t) (e1 - e0) : 0u);
+    if (SRC == SRC_CODES && P.seg_cnt) {  // this workgroup's segment of a probe pass's output
+        e0  = wg * P.seg_stride;
+        len = __builtin_amdgcn_readfirstlane(P.seg_cnt[wg]);
+    }
     constexpr uint32_t CW = FMT == FMT_C22 ? 22u : 32u;  // dwords per chunk
     uint32_t* __restrict__ pool = P.pool + wg * P.cap * CW;
     uint32_t* __restrict__ meta = P.meta + wg * P.cap;
@@ -1876,6 +1888,144 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
         for (int k = 0; k < 6; k++) P.dbg[blockIdx.x * 8 + k] = tph[k];
 }
 
+// ================================================ K7b: basic k >= 2, one bit per pass
+// The words (bmix(key)) are partitioned by the slice of add_basic's bit j (MODE_SLICE_BASIC's
+// scatter for j = 0, MODE_BASIC_BITJ's for j > 0); every item tests bit j of its words in the LDS
+// slice, and the passing words go to the workgroup's own region of surv (dense, no atomics;
+// wg_cnt[w] = its count, filtered += the sum). The next pass's scatter partitions workgroup w's
+// region by the slice of bit j + 1 in its workgroup w, so every bit of every key is tested in LDS
+// (bloom contains, src/bloom_filter.c:92-111), never by a random HBM read. Items are numbered as
+// in k_probe (segment-major inside a partition); the next item's chunks (and the one after's list
+// entries) are loaded while the current one is tested; one barrier per item (double-buffered
+// wave sums).
+__global__ __launch_bounds__(1024) void k_probe_bitj(ProbeParams P) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    constexpr uint32_t NT = 1024;
+    constexpr int      NW = kPC * 4;
+    const Geometry&    g  = P.g;
+    const uint32_t     F  = 1u << g.log2F, segw = g.seg_words, nseg = g.nseg;
+    uint32_t*          slice = lds;
+    uint32_t*          wsum  = slice + segw;  // 2 x 16, by item parity
+    const int      tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const uint32_t I   = P.item_start[F];
+    const uint32_t it0 = __builtin_amdgcn_readfirstlane((uint32_t) ((uint64_t) blockIdx.x * I / gridDim.x));
+    const uint32_t it1 = __builtin_amdgcn_readfirstlane((uint32_t) ((uint64_t) (blockIdx.x + 1) * I / gridDim.x));
+    uint32_t* __restrict__ out = P.surv + (uint64_t) blockIdx.x * P.surv_seg_stride;
+    uint32_t cursor = 0;  // words appended (uniform)
+    if (it0 < it1) {  // (uniform)
+        struct ItemG {
+            uint32_t q, seg, lb, le;
+            uint32_t qi0, qi1, lq0, lq1, npc;  // partition q's items and list range
+        };
+        auto at_q = [&](ItemG& r, uint32_t q) {
+            r.q   = q;
+            r.qi0 = __builtin_amdgcn_readfirstlane(P.item_start[q]);
+            r.qi1 = __builtin_amdgcn_readfirstlane(P.item_start[q + 1]);
+            r.lq0 = __builtin_amdgcn_readfirstlane(P.list_start[q]);
+            r.lq1 = __builtin_amdgcn_readfirstlane(P.list_start[q + 1]);
+            r.npc = (r.qi1 - r.qi0) / nseg;
+        };
+        auto place = [&](ItemG& r, uint32_t it) {
+            r.seg             = (it - r.qi0) / r.npc;
+            const uint32_t pc = (it - r.qi0) - r.seg * r.npc;
+            r.lb              = r.lq0 + pc * kProbeCH;
+            r.le              = min(r.lq1, r.lb + kProbeCH);
+        };
+        // item it's geometry from that of an earlier item (a binary search only for the first)
+        auto next = [&](const ItemG& prev, uint32_t it) {
+            ItemG r = prev;
+            if (it >= r.qi1) {  // (uniform) a later partition: step over empty ones
+                uint32_t q = r.q + 1;
+                while (__builtin_amdgcn_readfirstlane(P.item_start[q + 1]) <= it) q++;
+                at_q(r, q);
+            }
+            place(r, it);
+            return r;
+        };
+        ItemG g0;
+        at_q(g0, __builtin_amdgcn_readfirstlane(find_q(P.item_start, F, it0)));
+        place(g0, it0);
+        const uint32_t msz = (uint32_t) g.m, F1 = F - 1u;
+        ItemG      gA = g0, gB = next(gA, min(it0 + 1, it1 - 1)), gC = next(gB, min(it0 + 2, it1 - 1));
+        uint32_t   eA[kPC], eB[kPC], eC[kPC];
+        Sweep<kPC> SA, SB, SC;
+        load_list_u<kPC>(P.list, gA.lb, gA.le, eA);
+        load_list_u<kPC>(P.list, gB.lb, gB.le, eB);
+        load_list_u<kPC>(P.list, gC.lb, gC.le, eC);
+        load_chunks_u<kPC>(P.pool, eA, gA.lb, gA.le, SA);
+        load_chunks_u<kPC>(P.pool, eB, gB.lb, gB.le, SB);
+        uint32_t cq = 0xFFFFFFFFu, cs = 0xFFFFFFFFu, par = 0;  // the (partition, segment) in LDS
+        for (uint32_t it = it0; it < it1; it++) {
+            // prefetch: chunks of it + 2 (its list entries are in eC), list entries of it + 3
+            const ItemG gD = next(gC, min(it + 3, it1 - 1));
+            uint32_t    eD[kPC];
+            load_chunks_u<kPC>(P.pool, eC, gC.lb, gC.le, SC);
+            load_list_u<kPC>(P.list, gD.lb, gD.le, eD);
+            if (gA.q != cq || gA.seg != cs) {  // (uniform)
+                __syncthreads();  // every wave is done with the previous slice
+                const uint4* src = (const uint4*) (P.slices + ((uint64_t) gA.q * nseg + gA.seg) * segw);
+                uint4*       dst = (uint4*) slice;
+                for (uint32_t i = tid; i < segw / 4; i += NT) dst[i] = src[i];
+                cq = gA.q;
+                cs = gA.seg;
+                __syncthreads();
+            }
+            uint32_t pass = 0;
+#pragma unroll
+            for (int i = 0; i < NW; i++) {
+                const uint32_t w  = sweep_word(SA, i >> 2, i & 3);
+                const uint32_t b  = basic_bit(bunmix(w), g.bitj, msz);
+                const uint32_t lb = b >> g.log2F;
+                const bool     in = (uint32_t) (i & 3) < SA.n[i >> 2] && (b & F1) == gA.q && (lb >> g.log2seg) == gA.seg;
+                const uint32_t x  = lb & (g.seg_bits - 1u);
+                pass |= (in && ((slice[x >> 5] >> (x & 31u)) & 1u) ? 1u : 0u) << i;
+            }
+            const uint32_t c    = (uint32_t) __builtin_popcount(pass);
+            const uint32_t incl = wave_incl_scan_dpp(c);
+            uint32_t*      ws   = wsum + par * 16;
+            if (lane == 63) ws[wave] = incl;
+            __syncthreads();
+            uint32_t before = 0, total = 0;
+#pragma unroll
+            for (int w = 0; w < (int) (NT / 64); w++) {
+                const uint32_t x = ws[w];
+                before += w < wave ? x : 0u;
+                total += x;
+            }
+            uint32_t o = cursor + before + incl - c;
+#pragma unroll
+            for (int i = 0; i < NW; i++)
+                if ((pass >> i) & 1u) out[o++] = sweep_word(SA, i >> 2, i & 3);
+            cursor += __builtin_amdgcn_readfirstlane(total);
+            par ^= 1u;
+            // rotate the buffers
+            gA = gB;
+            gB = gC;
+            gC = gD;
+#pragma unroll
+            for (int j = 0; j < kPC; j++) {
+                SA.v[j] = SB.v[j];
+                SA.n[j] = SB.n[j];
+                SB.v[j] = SC.v[j];
+                SB.n[j] = SC.n[j];
+                eC[j]   = eD[j];
+            }
+        }
+    }
+    if (tid == 0) {
+        P.wg_cnt[blockIdx.x] = cursor;
+        if (cursor) atomicAdd((unsigned long long*) P.filtered, (unsigned long long) cursor);
+    }
+}
+
+size_t probe_bitj_lds_bytes(const Geometry& g) { return (g.seg_words + 32) * sizeof(uint32_t); }
+
+void launch_probe_bitj(const ProbeParams& p, uint32_t grid, hipStream_t st) {
+    const size_t lds = probe_bitj_lds_bytes(p.g);
+    (void) hipFuncSetAttribute((const void*) &k_probe_bitj, hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds);
+    k_probe_bitj<<<grid, 1024, lds, st>>>(p);
+}
+
 // ========================================================================= K10: join
 // One workgroup per (partition q, sub-partition s) job (bucket_chaining_join per task,
 // src/parallel_radix_join_bloom.c:259-329). The R codes of (q, s) are known to share their low
@@ -3069,7 +3219,11 @@ void launch_scatter(const ScatterParams& p, int src, int side, uint32_t grid, hi
             default: return scatter_pay_inst<MODE_NOBLOOM, FMT_CODE>(p, side, grid, st);
         }
     }
-    if (src == SRC_CODES) return scatter_inst<SRC_CODES, MODE_GLOBAL, FMT_CODE>(p, side, grid, st);
+    if (src == SRC_CODES) {
+        if (g.mode == MODE_BASIC_BITJ) return scatter_inst<SRC_CODES, MODE_BASIC_BITJ, FMT_CODE>(p, side, grid, st);
+        if (g.mode == MODE_CODE_OF_KEY) return scatter_inst<SRC_CODES, MODE_CODE_OF_KEY, FMT_CODE>(p, side, grid, st);
+        return scatter_inst<SRC_CODES, MODE_GLOBAL, FMT_CODE>(p, side, grid, st);
+    }
     switch (g.mode) {
         case MODE_SLICE_BLOCK:
             if (side == SIDE_S && g.s_format == FMT_C22)
