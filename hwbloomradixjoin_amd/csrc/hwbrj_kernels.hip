@@ -68,6 +68,24 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, uin
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int) bytes, 0x00020000);
 }
 
+// Copy a slice segment (words, a multiple of 4) from HBM into LDS with global_load_lds (16 bytes
+// per lane, no VGPR destination), all loads issued before any wait: one latency per slice instead
+// of one per 16 KiB (a register copy loop waits for each load before its ds_write). The caller's
+// __syncthreads() after it retires the loads (its fence waits vmcnt(0)). 1024 threads.
+__device__ __forceinline__ void slice_to_lds(uint32_t* dst, const uint32_t* src, uint32_t words) {
+    const uint4*   s4 = (const uint4*) src;
+    uint4*         d4 = (uint4*) dst;
+    const uint32_t n  = words / 4, wb = threadIdx.x & ~63u;
+    if (n % 64 != 0) {  // (small filters) a plain copy
+        for (uint32_t i = threadIdx.x; i < n; i += 1024) d4[i] = s4[i];
+        return;
+    }
+    for (uint32_t i0 = 0; i0 < n; i0 += 1024)
+        if (i0 + wb < n)  // (wave-uniform) the wave's 64 lanes fill d4[i0 + wb .. + 64)
+            __builtin_amdgcn_global_load_lds((const void*) (s4 + i0 + threadIdx.x),
+                                             (__attribute__((address_space(3))) void*) (d4 + i0 + wb), 16, 0, 0);
+}
+
 // Where an element's filter bits live inside its partition slice (KIND != KIND_PASS).
 struct Loc {
     uint32_t seg;   // slice segment
@@ -1653,9 +1671,7 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
         }
         if (slices) {
             __syncthreads();  // every wave is done with the previous slice
-            const uint4* src = (const uint4*) (P.slices + ((uint64_t) q * nseg + seg) * segw);
-            uint4*       dst = (uint4*) slice;
-            for (uint32_t i = tid; i < segw / 4; i += NT) dst[i] = src[i];
+            slice_to_lds(slice, P.slices + ((uint64_t) q * nseg + seg) * segw, segw);
             __syncthreads();
         }
         const uint32_t cq = zfmt ? z_const(zinv, q) : 0u;  // (zinv complete: the barriers above)
@@ -1946,39 +1962,58 @@ __global__ __launch_bounds__(1024) void k_probe_bitj(ProbeParams P) {
         at_q(g0, __builtin_amdgcn_readfirstlane(find_q(P.item_start, F, it0)));
         place(g0, it0);
         const uint32_t msz = (uint32_t) g.m, F1 = F - 1u;
-        ItemG      gA = g0, gB = next(gA, min(it0 + 1, it1 - 1)), gC = next(gB, min(it0 + 2, it1 - 1));
+        const auto     rout = buf_rsrc(out, (uint32_t) (P.surv_seg_stride * 4));
+        // geometry of items it .. it + 3 (gi[0] = it), rolled as the items advance (scalars)
+        ItemG gi[4];
+        gi[0] = g0;
+        gi[1] = next(gi[0], min(it0 + 1, it1 - 1));
+        gi[2] = next(gi[1], min(it0 + 2, it1 - 1));
+        gi[3] = next(gi[2], min(it0 + 3, it1 - 1));
         uint32_t   eA[kPC], eB[kPC], eC[kPC];
         Sweep<kPC> SA, SB, SC;
-        load_list_u<kPC>(P.list, gA.lb, gA.le, eA);
-        load_list_u<kPC>(P.list, gB.lb, gB.le, eB);
-        load_list_u<kPC>(P.list, gC.lb, gC.le, eC);
-        load_chunks_u<kPC>(P.pool, eA, gA.lb, gA.le, SA);
-        load_chunks_u<kPC>(P.pool, eB, gB.lb, gB.le, SB);
+        load_list_u<kPC>(P.list, gi[0].lb, gi[0].le, eA);
+        load_list_u<kPC>(P.list, gi[1].lb, gi[1].le, eB);
+        load_list_u<kPC>(P.list, gi[2].lb, gi[2].le, eC);
+        load_chunks_u<kPC>(P.pool, eA, gi[0].lb, gi[0].le, SA);
+        load_chunks_u<kPC>(P.pool, eB, gi[1].lb, gi[1].le, SB);
         uint32_t cq = 0xFFFFFFFFu, cs = 0xFFFFFFFFu, par = 0;  // the (partition, segment) in LDS
-        for (uint32_t it = it0; it < it1; it++) {
-            // prefetch: chunks of it + 2 (its list entries are in eC), list entries of it + 3
-            const ItemG gD = next(gC, min(it + 3, it1 - 1));
-            uint32_t    eD[kPC];
-            load_chunks_u<kPC>(P.pool, eC, gC.lb, gC.le, SC);
-            load_list_u<kPC>(P.list, gD.lb, gD.le, eD);
-            if (gA.q != cq || gA.seg != cs) {  // (uniform)
+        // Sc: chunks of item it (loaded); the chunks of it + 1 are in flight; en: list entries of
+        // it + 2 -> chunks into Sf; ef <- list entries of it + 3. Three buffers rotate (no load
+        // result is ever copied, so no wait is forced before its use).
+        auto step = [&](uint32_t it, Sweep<kPC>& Sc, Sweep<kPC>& Sf, const uint32_t (&en)[kPC], uint32_t (&ef)[kPC]) {
+            const ItemG ga = gi[0];
+            load_chunks_u<kPC>(P.pool, en, gi[2].lb, gi[2].le, Sf);
+            load_list_u<kPC>(P.list, gi[3].lb, gi[3].le, ef);
+            if (ga.q != cq || ga.seg != cs) {  // (uniform)
                 __syncthreads();  // every wave is done with the previous slice
-                const uint4* src = (const uint4*) (P.slices + ((uint64_t) gA.q * nseg + gA.seg) * segw);
-                uint4*       dst = (uint4*) slice;
-                for (uint32_t i = tid; i < segw / 4; i += NT) dst[i] = src[i];
-                cq = gA.q;
-                cs = gA.seg;
+                slice_to_lds(slice, P.slices + ((uint64_t) ga.q * nseg + ga.seg) * segw, segw);
+                cq = ga.q;
+                cs = ga.seg;
                 __syncthreads();
+            }
+            // bit j of every word: add_basic's sequence stepped j times (uniform loop)
+            uint32_t h[NW], y[NW];
+#pragma unroll
+            for (int i = 0; i < NW; i++) {
+                const uint32_t key = bunmix(sweep_word(Sc, i >> 2, i & 3));
+                h[i] = mod_m(crapwow(kSeed, key), msz);
+                y[i] = mod_m(key + kSeed, msz);
+            }
+            for (uint32_t t = 0; t < g.bitj; t++) {
+#pragma unroll
+                for (int i = 0; i < NW; i++) {
+                    h[i] = mod_m(h[i] + y[i], msz);
+                    y[i] = mod_m(y[i] + t + 1u, msz);
+                }
             }
             uint32_t pass = 0;
 #pragma unroll
             for (int i = 0; i < NW; i++) {
-                const uint32_t w  = sweep_word(SA, i >> 2, i & 3);
-                const uint32_t b  = basic_bit(bunmix(w), g.bitj, msz);
-                const uint32_t lb = b >> g.log2F;
-                const bool     in = (uint32_t) (i & 3) < SA.n[i >> 2] && (b & F1) == gA.q && (lb >> g.log2seg) == gA.seg;
+                const uint32_t lb = h[i] >> g.log2F;
                 const uint32_t x  = lb & (g.seg_bits - 1u);
-                pass |= (in && ((slice[x >> 5] >> (x & 31u)) & 1u) ? 1u : 0u) << i;
+                const uint32_t in = ((uint32_t) (i & 3) < Sc.n[i >> 2] ? 1u : 0u) & ((h[i] & F1) == ga.q ? 1u : 0u) &
+                                    ((lb >> g.log2seg) == ga.seg ? 1u : 0u);
+                pass |= (in & (slice[x >> 5] >> (x & 31u))) << i;
             }
             const uint32_t c    = (uint32_t) __builtin_popcount(pass);
             const uint32_t incl = wave_incl_scan_dpp(c);
@@ -1994,22 +2029,22 @@ __global__ __launch_bounds__(1024) void k_probe_bitj(ProbeParams P) {
             }
             uint32_t o = cursor + before + incl - c;
 #pragma unroll
-            for (int i = 0; i < NW; i++)
-                if ((pass >> i) & 1u) out[o++] = sweep_word(SA, i >> 2, i & 3);
+            for (int i = 0; i < NW; i++) {  // a fixed number of stores (the others are dropped)
+                const uint32_t pi = (pass >> i) & 1u;
+                __builtin_amdgcn_raw_buffer_store_b32(sweep_word(Sc, i >> 2, i & 3), rout, pi ? o * 4 : kOob, 0, 0);
+                o += pi;
+            }
             cursor += __builtin_amdgcn_readfirstlane(total);
             par ^= 1u;
-            // rotate the buffers
-            gA = gB;
-            gB = gC;
-            gC = gD;
-#pragma unroll
-            for (int j = 0; j < kPC; j++) {
-                SA.v[j] = SB.v[j];
-                SA.n[j] = SB.n[j];
-                SB.v[j] = SC.v[j];
-                SB.n[j] = SC.n[j];
-                eC[j]   = eD[j];
-            }
+            gi[0] = gi[1];
+            gi[1] = gi[2];
+            gi[2] = gi[3];
+            gi[3] = next(gi[2], min(it + 4, it1 - 1));
+        };
+        for (uint32_t it = it0; it < it1; it += 3) {
+            step(it, SA, SC, eC, eA);
+            if (it + 1 < it1) step(it + 1, SB, SA, eA, eB);
+            if (it + 2 < it1) step(it + 2, SC, SB, eB, eC);
         }
     }
     if (tid == 0) {
