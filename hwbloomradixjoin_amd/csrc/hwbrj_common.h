@@ -95,6 +95,8 @@ enum Mode : int {
     // scatter modes of basic k >= 2's repartitioning passes (words = bmix(key) in, SRC_CODES):
     MODE_BASIC_BITJ   = 4,  // partition = the slice of bit j (Geometry::bitj) of add_basic; word kept
     MODE_CODE_OF_KEY  = 5,  // partition = code & (F-1), word = code = crc32c(42, key) (join layout)
+    MODE_BASIC_POS    = 6,  // R tuples read as k * |R| elements (bit j of tuple t = element j |R| + t):
+                            // word = bit j's position, partition = its slice (the slice build)
 };
 
 enum Format : int {

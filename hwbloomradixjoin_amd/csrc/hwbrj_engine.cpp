@@ -649,7 +649,7 @@ int Engine::enqueue_basic_kk(const uint2* dR, uint64_t nR, const uint2* dS, uint
     const bool jnew = jparts.bytes < (size_t) (2 * NJ + 1) * 4 || NJ != last_nj_;
     last_nj_ = NJ;
     ok &= jtask.ensure((size_t) join_extra_tasks() * 8) && jparts.ensure((size_t) (2 * NJ + 1) * 4);
-    ok &= slices.ensure((uint64_t) F * nseg * g.seg_words * 4) && bpos.ensure(nRk * 4);
+    ok &= slices.ensure((uint64_t) F * nseg * g.seg_words * 4) && (g.k <= G || bpos.ensure(nRk * 4));
     ok &= dense.ensure(G * rw * 4) && dense2.ensure(G * rw * 4) && kkcnt.ensure(64 * 8 + 2 * G * 4);
     if (!ok) {
         set_last_error("hipMalloc failed (device memory)");
@@ -709,12 +709,22 @@ int Engine::enqueue_basic_kk(const uint2* dR, uint64_t nR, const uint2* dS, uint
     bp.run_off     = rrun.as<uint32_t>() + sweeps_max * NSUB;
     launch_build(bp, Fj, stream);
     // ---------------------------------------------------------------- the filter slices
-    launch_bitpos(dR, nR, g, bpos.as<uint32_t>(), stream);
-    sp     = side(false);
-    sp.g   = g;
-    sp.src = bpos.p;
-    sp.n   = nRk;
-    launch_scatter(sp, SRC_CODES, SIDE_R, G, stream);
+    sp = side(false);
+    if (g.k <= G) {  // R's k bit positions partitioned by slice straight from the tuples
+        Geometry gp = g;
+        gp.mode     = MODE_BASIC_POS;
+        sp.g        = gp;
+        sp.src      = dR;
+        sp.n        = nRk;
+        sp.vn       = nR;
+        launch_scatter(sp, SRC_TUPLES, SIDE_R, G, stream);
+    } else {
+        launch_bitpos(dR, nR, g, bpos.as<uint32_t>(), stream);
+        sp.g   = g;
+        sp.src = bpos.p;
+        sp.n   = nRk;
+        launch_scatter(sp, SRC_CODES, SIDE_R, G, stream);
+    }
     index(false, g.log2F, (uint32_t) BSW, 1);
     launch_slice_fill(poolS.as<uint32_t>(), listS.as<uint32_t>(), lstartS.as<uint32_t>(), g,
                       slices.as<uint32_t>(), stream);

@@ -26,6 +26,7 @@ struct ScatterParams {
     uint64_t         cap;          // chunk capacity of one workgroup region
     const uint32_t*  seg_cnt;      // SRC_CODES from per-workgroup segments: workgroup w partitions
     uint64_t         seg_stride;   // src + w * seg_stride (elements), seg_cnt[w] of them; or nullptr
+    uint64_t         vn;           // MODE_BASIC_POS: tuples of src (n = k * vn elements, k <= grid)
     Geometry         g;
     const CrcTables* tabs;
 };

@@ -529,6 +529,7 @@ template <int SRC>
 struct ScRaw {  // one round's raw loads of this thread (tuples: keys only; codes: 4 per uint4)
     uint32_t k[SRC == SRC_TUPLES ? kScE : 1];
     uint4    v[SRC == SRC_TUPLES ? 1 : kScE / 4];
+    uint32_t jb[SRC == SRC_TUPLES ? kScE : 1];  // MODE_BASIC_POS: which bit of the key
 };
 
 // LDS: static CRC nibble table (512 B, at 0, so its row offsets are immediates); dynamic (words):
@@ -584,10 +585,26 @@ __device__ __forceinline__ void scatter_body(const ScatterParams& P) {
     const auto rmeta = buf_rsrc(meta, (uint32_t) (P.cap * 4));
     __syncthreads();
 
+    // MODE_BASIC_POS: element e0 + i is bit jj of tuple e0 + i - jj |R| (a workgroup's range
+    // usually crosses at most one multiple of |R|; tiny relations step further)
+    const uint64_t vn  = MODE == MODE_BASIC_POS && P.vn ? P.vn : 1;  // (P.vn = 0: no elements)
+    const uint32_t jb0 = MODE == MODE_BASIC_POS ? (uint32_t) (e0 / vn) : 0u;
+    const uint64_t vb  = (uint64_t) (jb0 + 1) * vn;
     // Loads of the round at `base`: a full round of tuples takes the lane offset in voffset and the
     // round offset in soffset (no per-element VALU); a partial round checks every index.
     auto load_round = [&](uint32_t base, ScRaw<SRC>& R) {
-        if (SRC == SRC_TUPLES && base + kScRound <= len) {
+        if (MODE == MODE_BASIC_POS) {
+#pragma unroll
+            for (int j = 0; j < kScE; j++) {
+                const uint32_t i  = base + j * kScThreads + tid;
+                const uint64_t ev = e0 + (i < len ? i : 0u);  // (past the range: any valid tuple)
+                uint32_t       jj = jb0;
+                for (uint64_t b = vb; ev >= b; b += vn) jj++;  // (ev < k vn: at most k steps)
+                const uint64_t t = ev - (uint64_t) jj * vn;
+                R.k[j]  = len ? ((const uint32_t*) P.src)[2 * t] : 0u;  // (len = 0: R may be empty)
+                R.jb[j] = jj;
+            }
+        } else if (SRC == SRC_TUPLES && base + kScRound <= len) {
 #pragma unroll
             for (int j = 0; j < kScE; j++)
                 R.k[j] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, tid * EB, (base + j * kScThreads) * EB, 0);
@@ -710,7 +727,12 @@ __device__ __forceinline__ void scatter_body(const ScatterParams& P) {
         for (int j = 0; j < kScE; j++) {
             uint32_t x, idx;
             elem(R, base, j, x, idx);
-            sc_word_lds0<SRC, MODE, FMT>(x, P.g, crc_tab, w[j], q[j]);
+            if (MODE == MODE_BASIC_POS) {
+                w[j] = basic_bit(x, R.jb[j], (uint32_t) P.g.m);
+                q[j] = w[j] & (F - 1u);
+            } else {
+                sc_word_lds0<SRC, MODE, FMT>(x, P.g, crc_tab, w[j], q[j]);
+            }
 #ifndef HWBRJ_SC_SB
 #define HWBRJ_SC_SB 2
 #endif
@@ -3268,6 +3290,7 @@ void launch_scatter(const ScatterParams& p, int src, int side, uint32_t grid, hi
             return scatter_inst<SRC_TUPLES, MODE_SLICE_BLOCK, FMT_CODE>(p, side, grid, st);
         case MODE_SLICE_BASIC:
             return scatter_inst<SRC_TUPLES, MODE_SLICE_BASIC, FMT_CODE>(p, side, grid, st);
+        case MODE_BASIC_POS: return scatter_inst<SRC_TUPLES, MODE_BASIC_POS, FMT_CODE>(p, side, grid, st);
         default: return scatter_inst<SRC_TUPLES, MODE_NOBLOOM, FMT_CODE>(p, side, grid, st);
     }
 }
