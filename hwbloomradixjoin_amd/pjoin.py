@@ -44,8 +44,13 @@ class TorchExchange:
         self.gloo = self.on and dist.get_backend(group) == "gloo"
         self.slots = [None] * self.NSLOTS
         self.error = None
+        self.cuda = self.device.type == "cuda"
         self._c = _Exchange(None, _BUFFER(self._buffer), _A2A_U64(self._a2a_u64),
                             _A2AV(self._a2av), _AG(self._allgather))
+
+    def _sync(self):
+        if self.cuda:
+            self.torch.cuda.synchronize(self.device)
 
     # every callback returns 0 / a pointer, or records the exception and fails (the library then
     # returns an error code and join_partitioned raises it)
@@ -92,7 +97,7 @@ class TorchExchange:
             dst = self.slots[rslot][ro[0]: ro[-1] + rb[-1]]
             if W == 1:
                 dst.copy_(src)
-                self.torch.cuda.synchronize(self.device)  # (the library reads it on its own stream)
+                self._sync()  # (the library reads it on its own stream)
                 return 0
             if self.gloo:
                 out = self.torch.empty(dst.numel(), dtype=self.torch.uint8)
@@ -100,7 +105,7 @@ class TorchExchange:
                 dst.copy_(out)
             else:
                 self.dist.all_to_all_single(dst, src, rb, sb, group=self.group)
-            self.torch.cuda.synchronize(self.device)
+            self._sync()
             return 0
         return self._guard(go, 1)
 
@@ -117,7 +122,7 @@ class TorchExchange:
                 full.copy_(out)
             else:
                 self.dist.all_gather_into_tensor(full, mine.clone(), group=self.group)
-            self.torch.cuda.synchronize(self.device)
+            self._sync()
             return 0
         return self._guard(go, 1)
 
