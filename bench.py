@@ -91,7 +91,9 @@ def main():
     torch.cuda.set_device(local)
     hw.lib().hwbrj_set_device(local)
     dist = None
-    if world > 1:
+    # HWBRJ_BENCH_DIST=1: the process group (RCCL) even at world 1, so a one-GPU box runs the
+    # N > 1 code path's init, barriers and reductions over RCCL
+    if world > 1 or os.environ.get("HWBRJ_BENCH_DIST") == "1":
         import torch.distributed as dist
         if shared:
             dist.init_process_group("gloo")

@@ -352,6 +352,28 @@ def test_bench_two_ranks(hw):
     assert (line["parity"]["filtered"], line["parity"]["matches"]) == (g["rows"]["1024"][0], g["results"])
 
 
+def test_bench_rccl_process_group(hw):
+    """bench.py under torch.distributed.run with the RCCL ("nccl") process group on the one GPU
+    (HWBRJ_BENCH_DIST=1 at world 1): the init, barriers and reductions of the N > 1 path over RCCL."""
+    import socket
+    g = GOLD["F3_grid"]
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    root = os.path.dirname(HERE)
+    env = dict(os.environ, HWBRJ_BENCH_DIST="1")
+    env.pop("HWBRJ_BENCH_SHARED_GPU", None)
+    out = subprocess.run(["python", "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+                          "--master-addr", "127.0.0.1", "--master-port", str(port),
+                          os.path.join(root, "bench.py"), "--gpus", "1", "--steps", "2", "--warmup", "1",
+                          "-r", str(g["r"]), "-s", str(g["s"]), "-m", str(g["m"]), "--no-cpu-baseline"],
+                         capture_output=True, text=True, timeout=300, env=env, cwd=root)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-2000:]
+    line = json.loads([x for x in out.stdout.splitlines() if x.startswith("{")][-1])
+    assert (line["parity"]["filtered"], line["parity"]["matches"]) == (g["rows"]["1024"][0], g["results"])
+
+
 def _sorted_pairs(p):
     p = np.asarray(p).reshape(-1, 2)
     return p[np.lexsort((p[:, 1], p[:, 0]))]
