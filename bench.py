@@ -54,6 +54,7 @@ def parse():
                     help="N > 1: R replicated on every rank (no exchange), or R and the join "
                          "partitioned over the ranks (R and survivor all-to-alls, slice all-gather)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the PCIe-inclusive end-to-end time")
     ap.add_argument("--cpu-sample", type=int, default=0,
                     help="S tuples in the CPU baseline run (0: the full |S|, the same workload)")
     ap.add_argument("--cpu-threads", type=int, default=0,
@@ -72,6 +73,35 @@ def modeled_bytes(nR: int, nS: int, filtered: int, m: int, word_bytes: float) ->
         "survivors": 2.0 * 4.0 * filtered,            # k_probe writes, k_join reads
         "filter_slices": 2.0 * m / 8.0,               # k_build writes, k_probe loads
     }
+
+
+def e2e_time(hw, torch, dR, dS, args, nS, reps=3):
+    """SURVEY.md s8(d)'s t_e2e: H2D of R and S from pinned host memory, the join, and the counts'
+    D2H (hwbrj_join_device returns them on the host), median of `reps`. Reported beside the
+    headline, never as `value` (which has the inputs resident in HBM)."""
+    hR = torch.empty(dR.shape, dtype=torch.int32, pin_memory=True)
+    hS = torch.empty(dS.shape, dtype=torch.int32, pin_memory=True)
+    hR.copy_(dR)
+    hS.copy_(dS)
+    torch.cuda.synchronize()
+    tot, h2d = [], []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        dR.copy_(hR, non_blocking=True)
+        dS.copy_(hS, non_blocking=True)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        hw.join_device(dR, dS, args)
+        t2 = time.perf_counter()
+        tot.append(t2 - t0)
+        h2d.append(t1 - t0)
+    del hR, hS
+    ms = sorted(tot)[len(tot) // 2] * 1e3
+    hm = sorted(h2d)[len(h2d) // 2] * 1e3
+    nbytes = 8 * (dR.shape[0] + dS.shape[0])
+    return {"ms": round(ms, 3), "value": round(nS / (ms * 1e-3), 1), "unit": "probe-tuples/s",
+            "h2d_ms": round(hm, 3), "h2d_GBps": round(nbytes / (hm * 1e-3) / 1e9, 1),
+            "what": "H2D of R and S (pinned host memory) + join + counts D2H, median of 3; not value"}
 
 
 def main():
@@ -213,6 +243,9 @@ def main():
     cpu = None
     if world == 1 and not a.no_cpu_baseline:
         cpu = cpu_baseline(a, hw)
+    e2e = None
+    if world == 1 and not a.no_e2e:
+        e2e = e2e_time(hw, torch, dR, dS, args, nS)
 
     key = (nR, nS_total, a.s_sel, a.bloom_filter, a.bloom_size, a.bloom_hashes, a.bloom_block_size)
     gold = GOLDEN.get(key)
@@ -237,6 +270,7 @@ def main():
                    "B": a.bloom_block_size, "parallelism": f"S range-sharded x{world}, R replicated"},
         "roofline": roofline,
         "cpu_baseline": cpu,
+        "e2e": e2e,
         "parity": {"filtered": filtered, "matches": matches,
                    "golden": list(gold) if gold else None,
                    "ok": (gold == (filtered, matches)) if gold else None},

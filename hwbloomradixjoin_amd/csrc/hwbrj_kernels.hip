@@ -1554,8 +1554,12 @@ constexpr int      kPC      = HWBRJ_PC;       // chunk quads per thread per item
 constexpr uint32_t kProbeCH = 128u * kPC;     // chunks per probe item (1024 threads, 8 per chunk)
 // compacted survivors (first-bit candidates for KIND_BLOCK_PKK, whose rate is higher) per wave
 // and item in the LDS scratch, and the dense ranking rounds per wave
+#ifndef HWBRJ_SCRK
+#define HWBRJ_SCRK 256
+#endif
 template <int KIND> constexpr uint32_t scr_cap() {
-    return KIND == KIND_BLOCK_PKK || KIND == KIND_BASIC_KK || KIND == KIND_BLOCK_ZK ? 256u : (uint32_t) HWBRJ_SCR1;
+    return KIND == KIND_BLOCK_PKK || KIND == KIND_BASIC_KK || KIND == KIND_BLOCK_ZK ? (uint32_t) HWBRJ_SCRK
+                                                                                     : (uint32_t) HWBRJ_SCR1;
 }
 
 __device__ __forceinline__ uint32_t find_q(const uint32_t* item_start, uint32_t F, uint32_t it) {
