@@ -331,3 +331,19 @@ def test_histogram_joins_northstar(hw, full_R, cuda, algo):
     st = hw.join_device(full_R, S, hw.BloomFilterArgs(hw.BLOCKED, g["m"], 1, g["B"]), algorithm=algo)
     del S
     assert (st.filtered, st.matches) == (g["k1_filtered"], g["results"])
+
+
+def test_weak_scaling_ranks_reach_the_golden(hw, cuda):
+    """bench.py's default N > 1 run (weak scaling): rank r joins the whole |S| generated with seed
+    54321 + r. The seed orders the tuples only (the key multiset is the reference generator's), so
+    every rank's counts are the north-star golden."""
+    import torch
+    g = json.load(open(os.path.join(HERE, "golden", "survey_counts.json")))["F4_northstar"]
+    nR, nS = 128000000, 1024000000
+    dR = torch.empty((nR, 2), dtype=torch.int32, device="cuda")
+    dS = torch.empty((nS, 2), dtype=torch.int32, device="cuda")
+    hw.generate_device(dR, 2, nR, nR, 1.0, 12345)
+    for rank in (1, 7):
+        hw.generate_device(dS, 2, INT_MAX, nR, g["q"], 54321 + rank)
+        st = hw.join_device(dR, dS, hw.BloomFilterArgs(hw.BLOCKED, g["m"], 1, g["B"]))
+        assert (st.filtered, st.matches) == (g["k1_filtered"], g["results"])

@@ -111,7 +111,7 @@ def test_northstar_golden(hw, full_scale):
 
 @pytest.mark.parametrize("world", [2, 8])
 def test_northstar_rank_shards_sum_to_golden(hw, full_scale, cuda, world):
-    """What every rank of `bench.py --gpus N` computes (strong scaling): the replicated R and the
+    """What every rank of `bench.py --gpus N --scaling strong` computes: the replicated R and the
     rank's S range regenerated on the device (generate_device_range, shard_range); the per-rank
     counts summed over ranks (the all_reduce) must be the single-GPU golden."""
     g = GOLD["F4_northstar"]
