@@ -650,15 +650,16 @@ int Engine::enqueue_basic_kk(const uint2* dR, uint64_t nR, const uint2* dS, uint
     last_nj_ = NJ;
     ok &= jtask.ensure((size_t) join_extra_tasks() * 8) && jparts.ensure((size_t) (2 * NJ + 1) * 4);
     ok &= slices.ensure((uint64_t) F * nseg * g.seg_words * 4) && (g.k <= G || bpos.ensure(nRk * 4));
-    ok &= dense.ensure(G * rw * 4) && dense2.ensure(G * rw * 4) && kkcnt.ensure(64 * 8 + 2 * G * 4);
+    const uint32_t NC = (g.k + 64) & ~63u;  // pass counters [0, k - 1) + the dummy [NC - 1]
+    ok &= dense.ensure(G * rw * 4) && dense2.ensure(G * rw * 4) && kkcnt.ensure(NC * 8 + 2 * G * 4);
     if (!ok) {
         set_last_error("hipMalloc failed (device memory)");
         return 4;
     }
     uint64_t* d_result   = small.as<uint64_t>();
     uint64_t* d_filtered = small.as<uint64_t>() + 2;
-    uint64_t* cnt        = kkcnt.as<uint64_t>();  // [j]: candidates after pass j (j < k - 1); [63]: dummy
-    uint32_t* wgc[2]     = {(uint32_t*) (cnt + 64), (uint32_t*) (cnt + 64) + G};  // per-workgroup counts
+    uint64_t* cnt        = kkcnt.as<uint64_t>();  // [j]: candidates after pass j (j < k - 1); [NC - 1]: dummy
+    uint32_t* wgc[2]     = {(uint32_t*) (cnt + NC), (uint32_t*) (cnt + NC) + G};  // per-workgroup counts
     HWBRJ_CHECK(hipMemsetAsync(small.p, 0, 64, stream));
     HWBRJ_CHECK(hipMemsetAsync(kkcnt.p, 0, kkcnt.bytes, stream));
     if (jnew) HWBRJ_CHECK(hipMemsetAsync(jparts.p, 0, jparts.bytes, stream));
@@ -791,7 +792,7 @@ int Engine::enqueue_basic_kk(const uint2* dR, uint64_t nR, const uint2* dS, uint
     pp.surv_seg_stride = LS * 32;
     pp.surv_cnt        = survcnt.as<uint32_t>();
     pp.surv_off        = survoff.as<uint32_t>();
-    pp.filtered        = cnt + 63;  // (counted by the last bit pass)
+    pp.filtered        = cnt + NC - 1;  // (counted by the last bit pass)
     pp.job_surv        = jparts.as<uint32_t>() + NJ;
     const size_t   pl_lds = probe_lds_bytes(gj, nullptr);
     launch_probe(pp, (uint32_t) cus_ * (uint32_t) std::max<size_t>(1, std::min<size_t>(2, 163840 / pl_lds)), stream);

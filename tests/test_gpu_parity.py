@@ -208,6 +208,21 @@ def test_skewed_probe_side(hw, cuda, orc, a):
     assert st.matches == Sk1.size
 
 
+@pytest.mark.parametrize("m,k", [(1 << 20, 5), (1 << 24, 8), (1 << 16, 17), (1 << 20, 256),
+                                 (1 << 20, 257), (1 << 16, 300), (64, 9), (1 << 32, 4)], ids=str)
+def test_basic_multi_pass_bits(hw, cuda, orc, m, k):
+    """Basic k >= 2 (one bit per pass, Engine::enqueue_basic_kk): odd and even pass counts, k at and
+    above the scatter grid (k > 256: the bit positions come from k_bitpos, not the fused position
+    scatter), and tiny R whose k * |R| position ranges cross several multiples of |R| per workgroup."""
+    args = hw.BloomFilterArgs(hw.BASIC, m, k, 1024)
+    rng = np.random.default_rng(k)
+    for nR, nS in [(0, 3000), (1, 1), (3, 5000), (37, 101), (4097, 40999), (100003, 400009)]:
+        Rk = rng.permutation(nR).astype(np.int64) + 1
+        Sk = rng.integers(0, 3 * max(nR, 1) + 2, size=nS)
+        oracle_check(hw, cuda, orc, Rk, Sk, args)
+    assert hw.join_device(to_dev(cuda, np.zeros((8, 2))), to_dev(cuda, np.zeros((8, 2))), args).mode == 2
+
+
 def test_hot_build_key_chunked_join(hw, cuda, orc):
     """One key repeated in R beyond the LDS table capacity: the join processes R in pieces."""
     Rk = np.concatenate([np.full(20000, 5), np.arange(100, 50000)])
