@@ -86,6 +86,18 @@ def test_pairs_skewed_partitions(hw, cuda, orc, name):
     _check(hw, cuda, orc, R, S, _args(hw)[name])
 
 
+@pytest.mark.parametrize("name", ["blocked_packed", "blocked_k3", "basic_k3", "two_segments", "nobloom"])
+def test_pairs_edge_sizes(hw, cuda, orc, name):
+    """Empty and ragged relations (no pairs, one pair, sizes off every chunk / workgroup multiple)."""
+    rng = np.random.default_rng(13)
+    for nR, nS in [(0, 1000), (1000, 0), (1, 1), (1, 5000), (7, 33), (4097, 4099), (100003, 400009)]:
+        Rk = rng.permutation(nR).astype(np.int64) + 1
+        Sk = rng.integers(0, 2 * max(nR, 1) + 2, size=nS)
+        R = np.stack([Rk, rng.integers(-2**31, 2**31, size=nR)], 1).astype(np.int32).reshape(-1, 2)
+        S = np.stack([Sk, rng.integers(-2**31, 2**31, size=nS)], 1).astype(np.int32).reshape(-1, 2)
+        _check(hw, cuda, orc, R, S, _args(hw)[name])
+
+
 def test_pairs_zipf_and_nonunique(hw, cuda, orc, gen3):
     for mode in ("zipf", "nonunique"):
         R, S = gen3[mode]
