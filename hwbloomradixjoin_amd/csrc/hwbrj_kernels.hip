@@ -533,7 +533,7 @@ struct ScRaw {  // one round's raw loads of this thread (tuples: keys only; code
 };
 
 // LDS: static CRC nibble table (512 B, at 0, so its row offsets are immediates); dynamic (words):
-// stage F x 32 | 64 dummy slots | fill F + 4 | ncb 2F | tch F | tel F | flq F | misc 8
+// stage F x 32 | 64 dummy slots | fill F + 4 | ncb 2F | flq F | misc 8 (per-partition totals: registers of the plan thread)
 template <int SRC, int MODE, int FMT>
 __device__ __forceinline__ void scatter_body(const ScatterParams& P) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -543,17 +543,12 @@ __device__ __forceinline__ void scatter_body(const ScatterParams& P) {
     uint32_t*      stage = lds;                  // F * 32, then 64 per-lane dummy slots
     uint32_t*      fill  = stage + F * 32 + 64;  // F + 1 (entry F: invalid elements)
     uint32_t*      ncb   = fill + F + 4;         // 2 x F: plan by round parity (chunk base | nchunks << 22)
-    uint32_t*      tch   = ncb + 2 * F;          // F: chunks of q (this workgroup)
-    uint32_t*      tel   = tch + F;              // F: elements of q (this workgroup)
-    uint32_t*      flq   = tel + F;              // F: partitions flushed by the last plan
+    uint32_t*      flq   = ncb + 2 * F;          // F: partitions flushed by the last plan
     uint32_t*      misc  = flq + F;  // [0] chunks used, [1 + parity] flushes of a plan, [3 + parity] skew
     const int      tid   = threadIdx.x, lane = tid & 63;
     const uint32_t dummy = F * 32 + lane;        // stage index of this lane's dummy slot
     for (uint32_t i = tid; i < F + 1; i += kScThreads) fill[i] = 0;
-    for (uint32_t i = tid; i < F; i += kScThreads) {
-        tch[i] = 0;
-        tel[i] = 0;
-    }
+    uint32_t my_tch = 0, my_tel = 0;  // chunks / elements of partition tid (its plan thread) here
     if (tid < 128) {  // nibble table; f(kSeed) folded into row 0
         const uint32_t* src = &P.tabs->fwd[0][0];
         uint32_t        v   = src[tid];
@@ -733,6 +728,11 @@ __device__ __forceinline__ void scatter_body(const ScatterParams& P) {
             } else {
                 sc_word_lds0<SRC, MODE, FMT>(x, P.g, crc_tab, w[j], q[j]);
             }
+#ifndef HWBRJ_SC_NOPINW
+            // the word (CrapWow) computed here, among the CRC reads, not after the barrier where the
+            // compiler would sink it (phase B is the longer one: 2.66 -> 2.56 ms at the north star)
+            asm volatile("" : "+v"(w[j]));
+#endif
 #ifndef HWBRJ_SC_SB
 #define HWBRJ_SC_SB 2
 #endif
@@ -748,6 +748,11 @@ __device__ __forceinline__ void scatter_body(const ScatterParams& P) {
         }
         stamp(0);
         load_round(base + kScPre * kScRound, R);
+#ifndef HWBRJ_SC_NOORD
+        uint32_t slot[kScE];  // ranks issued first: their returns overlap the copy-out
+#pragma unroll
+        for (int j = 0; j < kScE; j++) slot[j] = atomicAdd(&fill[q[j]], 1u);
+#endif
         flush_copy();
         if (tid == 0) {
             misc[1 + par]        = 0;  // (last read by the previous round's flush_copy)
@@ -757,7 +762,11 @@ __device__ __forceinline__ void scatter_body(const ScatterParams& P) {
         bool sk = false;  // a slot >= 63: some partition reaches 64 words this round
 #pragma unroll
         for (int j = 0; j < kScE; j++) {
+#ifndef HWBRJ_SC_NOORD
+            q[j] |= slot[j] << 11;
+#else
             q[j] |= atomicAdd(&fill[q[j]], 1u) << 11;  // q | slot << 11
+#endif
             sk |= q[j] >= (63u << 11) && (q[j] & 2047u) < F;
         }
         if (__builtin_amdgcn_ballot_w64(sk) != 0 && lane == 0) misc[3 + par] = 1u;
@@ -799,8 +808,8 @@ __device__ __forceinline__ void scatter_body(const ScatterParams& P) {
                 ncb[par * F + qq] = cb | (nch << kCbBits);
                 flq[wbf + (incl >> 16) - 1] = qq;
                 fill[qq]          = f & 31u;
-                tch[qq] += nch;
-                tel[qq] += nch * 32;
+                my_tch += nch;
+                my_tel += nch * 32;
                 for (uint32_t c = 1; c < nch; c++) {  // direct chunks
                     meta[cb + c] = qq | (32u << 16);
                     if (FMT == FMT_C22)  // filled by atomic adds after the next barriers
@@ -842,8 +851,8 @@ __device__ __forceinline__ void scatter_body(const ScatterParams& P) {
                 const uint32_t cb = wb + incl - 1u;
                 ncb[qq]  = cb;
                 meta[cb] = qq | (f << 16);
-                tch[qq] += 1;
-                tel[qq] += f;
+                my_tch += 1;
+                my_tel += f;
             }
         }
         __syncthreads();
@@ -868,9 +877,9 @@ __device__ __forceinline__ void scatter_body(const ScatterParams& P) {
             for (int k = 0; k < 6; k++) P.dbg[wg * 8 + k] = tph[k];
         // this workgroup's row of the (workgroup x partition) chunk / element matrices (k_plan
         // scans them column-wise: no global atomics)
-        for (uint32_t qq = tid; qq < F; qq += kScThreads) {
-            P.wgq_chunks[wg * F + qq] = tch[qq];
-            P.wgq_elems[wg * F + qq]  = tel[qq];
+        if ((uint32_t) tid < F) {
+            P.wgq_chunks[wg * F + tid] = my_tch;
+            P.wgq_elems[wg * F + tid]  = my_tel;
         }
     }
 }
@@ -3231,7 +3240,7 @@ void launch_probe_global(const uint2* S, uint64_t n, const Geometry& g, const Cr
 
 size_t scatter_lds_bytes(uint32_t log2F) {
     const size_t F = 1u << log2F;
-    return (F * 32 + 64 + F + 4 + 5 * F + 8) * sizeof(uint32_t);  // stage, dummies, fill, ncb x2, 3 arrays, misc (+512 B static)
+    return (F * 32 + 64 + F + 4 + 3 * F + 8) * sizeof(uint32_t);  // stage, dummies, fill, ncb x2, flq, misc (+512 B static)
 }
 
 // The R and S scatters are one body under two kernel names, so per-kernel profiles (rocprofv3
