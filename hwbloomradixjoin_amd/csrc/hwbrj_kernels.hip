@@ -599,6 +599,21 @@ __device__ __forceinline__ void scatter_body(const ScatterParams& P) {
                 R.k[j]  = len ? ((const uint32_t*) P.src)[2 * t] : 0u;  // (len = 0: R may be empty)
                 R.jb[j] = jj;
             }
+#ifndef HWBRJ_SC_LD32  // (dev A/B: one 4-byte key load per tuple)
+        } else if (SRC == SRC_TUPLES && base + kScRound <= len) {  // two tuples per 16-byte load
+#pragma unroll
+            for (int h = 0; h < kScE / 2; h++) {
+                const v4u x = __builtin_amdgcn_raw_buffer_load_b128(rsrc, 2 * tid * EB, (base + h * 2 * kScThreads) * EB, 0);
+                R.k[2 * h]     = x.x;
+                R.k[2 * h + 1] = x.z;
+            }
+        } else if (SRC == SRC_TUPLES) {
+#pragma unroll
+            for (int j = 0; j < kScE; j++) {
+                const uint32_t i = base + (j >> 1) * 2 * kScThreads + 2 * tid + (j & 1);
+                R.k[j] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, i < len ? i * EB : kOob, 0, 0);
+            }
+#else
         } else if (SRC == SRC_TUPLES && base + kScRound <= len) {
 #pragma unroll
             for (int j = 0; j < kScE; j++)
@@ -609,6 +624,7 @@ __device__ __forceinline__ void scatter_body(const ScatterParams& P) {
                 const uint32_t i = base + j * kScThreads + tid;
                 R.k[j] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, i < len ? i * EB : kOob, 0, 0);
             }
+#endif
         } else {
 #pragma unroll
             for (int h = 0; h < NL; h++) {
@@ -622,7 +638,11 @@ __device__ __forceinline__ void scatter_body(const ScatterParams& P) {
     auto elem = [&](const ScRaw<SRC>& R, uint32_t base, int j, uint32_t& x, uint32_t& idx) {
         if (SRC == SRC_TUPLES) {
             x   = R.k[j];
+#ifndef HWBRJ_SC_LD32  // (dev A/B: one 4-byte key load per tuple)
+            idx = MODE == MODE_BASIC_POS ? base + j * kScThreads + tid : base + (j >> 1) * 2 * kScThreads + 2 * tid + (j & 1);
+#else
             idx = base + j * kScThreads + tid;
+#endif
         } else {
             const int h = j >> 2, t = j & 3;
             x   = t == 0 ? R.v[h].x : t == 1 ? R.v[h].y : t == 2 ? R.v[h].z : R.v[h].w;
