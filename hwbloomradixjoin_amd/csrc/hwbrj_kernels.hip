@@ -365,6 +365,12 @@ constexpr int      kScThreads = 1024;
 #ifndef HWBRJ_SC_PRE
 #define HWBRJ_SC_PRE 1
 #endif
+#ifndef HWBRJ_SC_LAUX
+#define HWBRJ_SC_LAUX 2  // cache policy of the tuple loads: nt (read once; 0 measured 2 % slower)
+#endif
+#ifndef HWBRJ_SC_SAUX
+#define HWBRJ_SC_SAUX 2  // cache policy of the chunk stores: nt (16 = sc1 measured slower)
+#endif
 constexpr int      kScPre     = HWBRJ_SC_PRE;             // rounds of loads in flight (1 or 2)
 constexpr int      kScE       = HWBRJ_SC_E;                        // elements per thread per round
 constexpr uint32_t kScRound   = kScThreads * kScE;        // elements per workgroup round
@@ -603,7 +609,7 @@ __device__ __forceinline__ void scatter_body(const ScatterParams& P) {
         } else if (SRC == SRC_TUPLES && base + kScRound <= len) {  // two tuples per 16-byte load
 #pragma unroll
             for (int h = 0; h < kScE / 2; h++) {
-                const v4u x = __builtin_amdgcn_raw_buffer_load_b128(rsrc, 2 * tid * EB, (base + h * 2 * kScThreads) * EB, 0);
+                const v4u x = __builtin_amdgcn_raw_buffer_load_b128(rsrc, 2 * tid * EB, (base + h * 2 * kScThreads) * EB, HWBRJ_SC_LAUX);
                 R.k[2 * h]     = x.x;
                 R.k[2 * h + 1] = x.z;
             }
@@ -672,7 +678,7 @@ __device__ __forceinline__ void scatter_body(const ScatterParams& P) {
 #ifdef HWBRJ_ABL_NOSTORE
             if (v.x == 0x12345678u && v.y == 0x9abcdef0u)  // dev ablation: practically never stores
 #endif
-            __builtin_amdgcn_raw_buffer_store_b128(v, rpool, ok ? (cb * 32 + l8 * 4) * 4 : kOob, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b128(v, rpool, ok ? (cb * 32 + l8 * 4) * 4 : kOob, 0, HWBRJ_SC_SAUX);
             }
             __builtin_amdgcn_raw_buffer_store_b32(qq | (32u << 16), rmeta, ok && l8 == 0 ? cb * 4 : kOob, 0, 0);
         };
