@@ -2152,6 +2152,33 @@ __device__ __forceinline__ uint32_t join_slot(uint32_t v) {
     return (v * 0x9E3779B1u) >> (32 - kJoinLog2T);
 }
 
+// The table is probed by buckets of 4 slots (one 16-byte LDS read compares four keys): a key lives
+// in the first bucket from its home that had a free slot when it was inserted. Slots are never
+// freed, so every bucket before it stays full, and a lookup can stop at the first bucket that
+// has a free slot (every copy of a key lies at or before it).
+#ifndef HWBRJ_JSLOT1
+__device__ __forceinline__ uint32_t join_count(const uint32_t* keys, uint32_t v) {
+    uint32_t b = join_slot(v) & ~3u, cnt = 0;
+    for (;;) {
+        const uint4 k = *(const uint4*) &keys[b];
+        cnt += (k.x == v) + (k.y == v) + (k.z == v) + (k.w == v);
+        if (k.x == kEmpty || k.y == kEmpty || k.z == kEmpty || k.w == kEmpty) return cnt;
+        b = (b + 4u) & (kJoinT - 1u);
+    }
+}
+
+__device__ __forceinline__ void join_insert(uint32_t* keys, uint32_t v) {
+    uint32_t b = join_slot(v) & ~3u;
+    for (;;) {
+        const uint4 k = *(const uint4*) &keys[b];  // (a free slot may be taken meanwhile: then CAS fails)
+        if (k.x == kEmpty && atomicCAS(&keys[b], kEmpty, v) == kEmpty) return;
+        if (k.y == kEmpty && atomicCAS(&keys[b + 1], kEmpty, v) == kEmpty) return;
+        if (k.z == kEmpty && atomicCAS(&keys[b + 2], kEmpty, v) == kEmpty) return;
+        if (k.w == kEmpty && atomicCAS(&keys[b + 3], kEmpty, v) == kEmpty) return;
+        b = (b + 4u) & (kJoinT - 1u);
+    }
+}
+#else  // (dev A/B: slot-by-slot linear probing)
 __device__ __forceinline__ uint32_t join_count(const uint32_t* keys, uint32_t v) {
     uint32_t h = join_slot(v), cnt = 0;
     for (uint32_t k = keys[h]; k != kEmpty; k = keys[h]) {
@@ -2165,6 +2192,7 @@ __device__ __forceinline__ void join_insert(uint32_t* keys, uint32_t v) {
     uint32_t h = join_slot(v);
     while (atomicCAS(&keys[h], kEmpty, v) != kEmpty) h = (h + 1u) & (kJoinT - 1u);
 }
+#endif
 
 // Join tasks. A (q, sub) job whose survivors exceed kJoinTaskSurv (probe-side skew, e.g. the
 // hot keys of a Zipf S) is split into parts over q's probe items; every part rebuilds the job's
