@@ -2378,11 +2378,23 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
         // a job costs two memory latencies (descriptors, data) instead of one per batch.
         for (uint32_t i = tid; i < kJoinWords / 4; i += kJoinThreads) ((uint4*) tab)[i] = make_uint4(0, 0, 0, 0);
         if (tid == 0) dupflag = 0;
+#ifndef HWBRJ_JDUPRTN
+        uint32_t rc = 0;
+#endif
         if ((uint32_t) tid < nRd) {
             const uint64_t r = (uint64_t) (w0 + tid) * NSUB + s;
             rcnt[tid]        = P.r_cnt[r];
             rbase[tid]       = (uint64_t) (w0 + tid) * P.slot + P.r_off[r];
+#ifndef HWBRJ_JDUPRTN
+            rc = rcnt[tid];
+#endif
         }
+#ifndef HWBRJ_JDUPRTN
+        if (wave == 0) {  // the job's R keys (nRd <= 64: every R descriptor is in wave 0)
+            const uint32_t t = __builtin_amdgcn_readlane(wave_incl_scan_dpp(rc), 63);
+            if (lane == 0) npieces = t;
+        }
+#endif
         if ((uint32_t) tid < nSd) {
             const uint32_t it    = i0 + tid;
             const uint32_t local = it - qi0;
@@ -2424,11 +2436,17 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
                 sv[r][j]         = o < sn[r] ? P.surv[bb + o] : 0u;
             }
         }
+#ifndef HWBRJ_JDUPRTN
+        // bits set without returns (no wave waits on them); a duplicate R key shows as fewer set
+        // bits than the job's R keys (popcount after the barrier)
+        auto set = [&](uint32_t x) { __hip_atomic_fetch_or(&tab[x >> 5], 1u << (x & 31u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); };
+#else
         uint32_t dup = 0;
         auto     set = [&](uint32_t x) {
             const uint32_t bit = 1u << (x & 31u);
             dup |= atomicOr(&tab[x >> 5], bit) & bit;
         };
+#endif
 #pragma unroll
         for (int r = 0; r < FR; r++) {
 #pragma unroll
@@ -2439,9 +2457,24 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
                 tail_run(P.r_codes, bb, 64u * FW, rn[r], set);
             }
         }
+#ifndef HWBRJ_JDUPRTN
+        __syncthreads();
+        {
+            uint32_t pc = 0;
+            for (uint32_t i = tid; i < kJoinWords / 4; i += kJoinThreads) {
+                const uint4 v = ((const uint4*) tab)[i];
+                pc += __builtin_popcount(v.x) + __builtin_popcount(v.y) + __builtin_popcount(v.z) + __builtin_popcount(v.w);
+            }
+            pc = __builtin_amdgcn_readlane(wave_incl_scan_dpp(pc), 63);
+            if (lane == 0 && pc) atomicAdd(&dupflag, pc);  // (dupflag: the set bits)
+        }
+        __syncthreads();
+        hashed = dupflag != npieces;  // uniform
+#else
         if (dup) dupflag = 1;
         __syncthreads();
         hashed = dupflag != 0;  // uniform
+#endif
         if (!hashed) {
             probe_begin();
             auto test = [&](uint32_t x) { cnt += (tab[x >> 5] >> (x & 31u)) & 1u; };
