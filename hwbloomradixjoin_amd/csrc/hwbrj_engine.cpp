@@ -596,6 +596,19 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
             for (int k = 0; k < 6; k++) ss[k] += (double) hs[b * 8 + k] / G;
         fprintf(stderr, "[dbg] S scatter cyc/WG: hash %.0f load+flush %.0f rank %.0f b1 %.0f write+plan %.0f b2 %.0f\n",
                 ss[0], ss[1], ss[2], ss[3], ss[4], ss[5]);
+        {  // workgroup start/end spread (100 MHz real-time clock): the kernel's tail
+            uint64_t t0 = ~0ull;
+            std::vector<double> st(G), en(G);
+            for (uint32_t b = 0; b < G; b++) t0 = std::min<uint64_t>(t0, hs[b * 8 + 6]);
+            for (uint32_t b = 0; b < G; b++) {
+                st[b] = (hs[b * 8 + 6] - t0) / 100.0;
+                en[b] = (hs[b * 8 + 7] - t0) / 100.0;
+            }
+            std::sort(st.begin(), st.end());
+            std::sort(en.begin(), en.end());
+            fprintf(stderr, "[dbg] S scatter WG start us: max %.1f | end us: min %.1f p10 %.1f p50 %.1f p90 %.1f max %.1f\n",
+                    st[G - 1], en[0], en[G / 10], en[G / 2], en[G * 9 / 10], en[G - 1]);
+        }
         fprintf(stderr, "[dbg] probe cyc/WG: top %.0f test %.0f b1 %.0f scan+b2 %.0f write %.0f b3+copy %.0f\n",
                 sp_[0], sp_[1], sp_[2], sp_[3], sp_[4], sp_[5]);
     }

@@ -566,6 +566,7 @@ __device__ __forceinline__ void scatter_body(const ScatterParams& P) {
     }
     if (tid < 8) misc[tid] = 0;
 
+    if (P.dbg && tid == 0) P.dbg[blockIdx.x * 8 + 6] = __builtin_amdgcn_s_memrealtime();  // dev-only: start
     const uint64_t n     = P.n_dev ? *P.n_dev : P.n;
     const uint64_t units = (n + 3) >> 2;
     const uint64_t G = gridDim.x, wg = blockIdx.x;
@@ -899,8 +900,10 @@ __device__ __forceinline__ void scatter_body(const ScatterParams& P) {
         }
         __syncthreads();
         if (tid == 0) P.wg_used[wg] = misc[0];
-        if (P.dbg && tid == 0)
+        if (P.dbg && tid == 0) {
             for (int k = 0; k < 6; k++) P.dbg[wg * 8 + k] = tph[k];
+            P.dbg[wg * 8 + 7] = __builtin_amdgcn_s_memrealtime();  // dev-only: end (100 MHz clock)
+        }
         // this workgroup's row of the (workgroup x partition) chunk / element matrices (k_plan
         // scans them column-wise: no global atomics)
         if ((uint32_t) tid < F) {
