@@ -1782,12 +1782,15 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
                     if (!SEG1) ok &= locate<KIND>(sweep_word(Sc, i >> 2, i & 3), g, inv, q).seg == seg ? 1u : 0u;
                     pass |= ok << i;
                 }
-                nsv = __builtin_amdgcn_readlane(wave_incl_scan_dpp((uint32_t) __builtin_popcount(pass)), 63);
+                const uint32_t pcnt = (uint32_t) __builtin_popcount(pass);
+                const uint32_t pinc = wave_incl_scan_dpp(pcnt);
+                nsv = __builtin_amdgcn_readlane(pinc, 63);
                 // pass 2, only when they fit the wave's scratch (dense ranking below): per slot, the
                 // wave ballot compacts the survivors there (no exec masking: the others write a
                 // shared garbage slot). Otherwise no scratch write at all (high selectivity: the
                 // words are ranked one by one, and 12 LDS writes per thread would buy nothing)
                 if (!PAY && kScrCap > 0 && nsv <= kScrCap) {  // wave-uniform
+#ifdef HWBRJ_PR_BALLOT  // (dev A/B: slot-major compaction by wave ballots)
                     uint32_t at0 = 0;
 #pragma unroll
                     for (int i = 0; i < NW; i++) {
@@ -1798,6 +1801,17 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
                         *(ok ? &scr[at0 + pre] : &scrdum[lane]) = sweep_word(Sc, i >> 2, i & 3);  // others: garbage slot
                         at0 += (uint32_t) __builtin_popcountll(m);
                     }
+#else
+                    // lane-major: this lane's survivors at its exclusive prefix (the scan above) plus
+                    // their rank among its own (one v_bcnt with the base as addend)
+                    const uint32_t pbase = pinc - pcnt;
+#pragma unroll
+                    for (int i = 0; i < NW; i++) {
+                        const bool     ok = (pass >> i) & 1u;
+                        const uint32_t r  = pbase + (uint32_t) __builtin_popcount(pass & ((1u << i) - 1u));
+                        *(ok ? &scr[r] : &scrdum[lane]) = sweep_word(Sc, i >> 2, i & 3);  // others: garbage slot
+                    }
+#endif
                 }
             } else {
 #pragma unroll
