@@ -101,7 +101,7 @@ enum Mode : int {
 
 enum Format : int {
     FMT_CODE   = 0,  // element word = code = crc32c(42, key) (MODE_SLICE_BASIC: bmix(key))
-    FMT_PACKED = 1,  // blocked, log2B <= log2F: (code >> log2F) | (first bit-in-block << (32 - log2F))
+    FMT_PACKED = 1,  // blocked, log2B <= log2F: (first bit-in-block) | (code >> log2F) << log2B (low bits: the slice bit)
     FMT_C22    = 2,  // S side, blocked, log2F = 10: the 22-bit code >> 10 alone, 32 elements packed
                      // into a 22-dword (88-byte) chunk; the probe recomputes the bit-in-block from
                      // the key (inverse CRC + CrapWow)

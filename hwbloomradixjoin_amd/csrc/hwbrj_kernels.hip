@@ -94,7 +94,7 @@ struct Loc {
 };
 
 template <int KIND>
-__device__ __forceinline__ uint32_t decode_k(uint32_t w, uint32_t q, uint32_t log2F);
+__device__ __forceinline__ uint32_t decode_k(uint32_t w, uint32_t q, const Geometry& g);
 
 // q: the element's partition (packed kinds recover the code from it).
 template <int KIND>
@@ -111,14 +111,14 @@ __device__ __forceinline__ Loc locate(uint32_t w, const Geometry& g, const uint3
     }
     uint32_t lb;
     if (KIND == KIND_BLOCK_Z1 || KIND == KIND_BLOCK_ZK) {  // FMT_C22: the key from the code
-        const uint32_t key = code_key(inv, decode_k<KIND>(w, q, g.log2F));
+        const uint32_t key = code_key(inv, decode_k<KIND>(w, q, g));
         lb  = w & g.lbmask;
         L.h = crapwow(kSeed, key) & (g.B - 1u);
         L.y = (key + kSeed) & (g.B - 1u);
     } else if (KIND == KIND_BLOCK_PK1 || KIND == KIND_BLOCK_PKK) {
-        lb  = w & g.lbmask;           // (code >> log2F) & (nblocks/F - 1)
-        L.h = w >> (32u - g.log2F);   // crapwow(key) & (B-1), stored by the scatter
-        L.y = KIND == KIND_BLOCK_PKK ? (code_key(inv, decode_k<KIND>(w, q, g.log2F)) + kSeed) & (g.B - 1u) : 0u;
+        lb  = (w >> g.log2B) & g.lbmask;  // (code >> log2F) & (nblocks/F - 1)
+        L.h = w & (g.B - 1u);             // crapwow(key) & (B-1), stored by the scatter
+        L.y = KIND == KIND_BLOCK_PKK ? (code_key(inv, decode_k<KIND>(w, q, g)) + kSeed) & (g.B - 1u) : 0u;
     } else {
         const uint32_t key = code_key(inv, w);
         lb  = (w >> g.log2F) & g.lbmask;
@@ -163,9 +163,9 @@ __device__ __forceinline__ bool apply_bits(const Loc& L, const Geometry& g, uint
 }
 
 template <int KIND>
-__device__ __forceinline__ uint32_t decode_k(uint32_t w, uint32_t q, uint32_t log2F) {
-    if (KIND == KIND_BLOCK_PK1 || KIND == KIND_BLOCK_PKK) return (w << log2F) | q;  // drops the h bits
-    if (KIND == KIND_BLOCK_Z1 || KIND == KIND_BLOCK_ZK) return (w << log2F) | q;
+__device__ __forceinline__ uint32_t decode_k(uint32_t w, uint32_t q, const Geometry& g) {
+    if (KIND == KIND_BLOCK_PK1 || KIND == KIND_BLOCK_PKK) return ((w >> g.log2B) << g.log2F) | q;  // drops the h bits
+    if (KIND == KIND_BLOCK_Z1 || KIND == KIND_BLOCK_ZK) return (w << g.log2F) | q;
     return w;
 }
 
@@ -472,9 +472,9 @@ __device__ __forceinline__ void sc_word_lds0(uint32_t x, const Geometry& g, cons
     } else if (MODE == MODE_SLICE_BLOCK && FMT == FMT_PACKED) {
         q = code & F1;
 #ifdef HWBRJ_ABL_NOCRAP
-        w = (code >> g.log2F) | (key << (32u - g.log2F));  // dev ablation (results invalid)
+        w = (key & (g.B - 1u)) | ((code >> g.log2F) << g.log2B);  // dev ablation (results invalid)
 #else
-        w = (code >> g.log2F) | ((crapwow(kSeed, key) & (g.B - 1u)) << (32u - g.log2F));
+        w = (crapwow(kSeed, key) & (g.B - 1u)) | ((code >> g.log2F) << g.log2B);
 #endif
     } else {
         q = code & F1;
@@ -1510,7 +1510,7 @@ __global__ __launch_bounds__(1024) void k_build(BuildParams P) {
                         if (L.seg == seg) apply_bits<KIND, true>(L, g, slice);
                     }
 #endif
-                    c[t]  = decode_k<KIND>(w, q, g.log2F);
+                    c[t]  = decode_k<KIND>(w, q, g);
                     rk[t] = 0xFFFFFFFFu;
 #ifndef HWBRJ_ABL_BNOSORT
                     if (last && ok) rk[t] = atomicAdd(&cnt[(nsw & 1u) * 64 + ((c[t] >> g.sub_shift) & (NSUB - 1u))], 1u);
@@ -1761,11 +1761,16 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
             uint32_t nsv  = 0;  // survivors of this wave (uniform)
             if (onebit) {
                 uint32_t wv[NW], bb[NW];  // slice word, bit index inside the segment
+                // packed words: the low log2(m / F) bits are the first bit's position in the slice
+                // (block in slice << log2B | bit in block), so its byte in LDS is one shift and mask
+                const uint32_t pkb = ((g.slice_bits - 1u) >> 3) & ~3u;
 #pragma unroll
                 for (int i = 0; i < NW; i++) {
                     const uint32_t w = sweep_word(Sc, i >> 2, i & 3);
                     if ((KIND == KIND_BLOCK_PK1 || KIND == KIND_BLOCK_PKK) && SEG1) {
-                        bb[i] = ((w & g.lbmask) << g.log2B) + (w >> (32u - g.log2F));
+                        bb[i] = w;  // (the test below uses only its low 5 bits)
+                        wv[i] = *(const uint32_t*) ((const char*) slice + ((w >> 3) & pkb));
+                        continue;
                     } else if (zfmt && SEG1) {  // first bit = crapwow(key) & (B - 1) (add_generic)
                         const uint32_t key = z_key(zinv, w, q, cq);
                         bb[i] = ((w & g.lbmask) << g.log2B) + (crapwow(kSeed, key) & (g.B - 1u));
@@ -1868,7 +1873,7 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
                 for (int k = 0; k < kDense; k++) {
                     const uint32_t j  = lane + 64u * k;
                     const uint32_t w  = scr[j];
-                    const uint32_t c  = decode_k<KIND>(w, q, g.log2F);
+                    const uint32_t c  = decode_k<KIND>(w, q, g);
                     const uint32_t s  = (c >> g.sub_shift) & (NSUB - 1u);
                     bool           ok = j < nsv;
                     if (KIND == KIND_BASIC_KK)
@@ -1898,7 +1903,7 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
                     uint32_t r[2] = {0, 0};
 #pragma unroll
                     for (int u = 0; u < 2; u++) {
-                        const uint32_t c = decode_k<KIND>(sweep_word(Sc, (i + u) >> 2, (i + u) & 3), q, g.log2F);
+                        const uint32_t c = decode_k<KIND>(sweep_word(Sc, (i + u) >> 2, (i + u) & 3), q, g);
                         const uint32_t s = (c >> g.sub_shift) & (NSUB - 1u);
                         if ((pass >> (i + u)) & 1u) r[u] = atomicAdd(&cnt[s], 1u);
                     }
@@ -1931,7 +1936,7 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
 #pragma unroll
                 for (int k = 0; k < kDense; k++) {
                     const bool     ok = dr[k] != kNoRank;
-                    const uint32_t c  = decode_k<KIND>(scr[lane + 64u * k], q, g.log2F);
+                    const uint32_t c  = decode_k<KIND>(scr[lane + 64u * k], q, g);
                     const uint32_t o  = subo[dr[k] & 0xFFFFu] + (dr[k] >> 16);
                     if (staged) stg[ok ? o : scap + lane] = c;
                     else __builtin_amdgcn_raw_buffer_store_b32(c, ro, ok ? o * 4 : 0x7FFFFFF0u, 0, 0);
@@ -1939,7 +1944,7 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
             } else if (staged) {  // LDS stage (copied out coalesced at the next piece)
 #pragma unroll
                 for (int i = 0; i < NW; i++) {
-                    const uint32_t c = decode_k<KIND>(sweep_word(Sc, i >> 2, i & 3), q, g.log2F);
+                    const uint32_t c = decode_k<KIND>(sweep_word(Sc, i >> 2, i & 3), q, g);
                     const uint32_t o = subo[(c >> g.sub_shift) & (NSUB - 1u)] + ((rank2[i / 2] >> (16 * (i & 1))) & 0xFFFFu);
                     stg[(pass >> i) & 1u ? o : scap + lane] = c;
                     if (PAY)  // the survivor's chunk position beside it
@@ -1950,7 +1955,7 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
                 const auto rpo = buf_rsrc(PAY ? P.surv_pos + (out - P.surv) : nullptr, PAY ? total * 4 : 0u);
 #pragma unroll
                 for (int i = 0; i < NW; i++) {
-                    const uint32_t c  = decode_k<KIND>(sweep_word(Sc, i >> 2, i & 3), q, g.log2F);
+                    const uint32_t c  = decode_k<KIND>(sweep_word(Sc, i >> 2, i & 3), q, g);
                     const uint32_t o  = subo[(c >> g.sub_shift) & (NSUB - 1u)] + ((rank2[i / 2] >> (16 * (i & 1))) & 0xFFFFu);
                     const uint32_t oo = ((pass >> i) & 1u) ? o * 4 : 0x7FFFFFF0u;
                     __builtin_amdgcn_raw_buffer_store_b32(c, ro, oo, 0, 0);
