@@ -182,6 +182,19 @@ def test_edge_sizes(hw, cuda, orc, a):
         oracle_check(hw, cuda, orc, Rk, Sk, args)
 
 
+@pytest.mark.parametrize("variant", ["blocked", "sectorized"])
+@pytest.mark.parametrize("B", [8, 16, 32, 64, 256, 1024])
+@pytest.mark.parametrize("k", [1, 2, 3])
+def test_packed_words_every_block_size(hw, cuda, orc, variant, B, k):
+    """Packed partition words (FMT_PACKED: first bit-in-block in the low log2B bits, code digits
+    above, so the low log2(m/F) bits are the slice bit) for every block size the slice path takes
+    (8 <= B <= F), k = 1 (KIND_BLOCK_PK1) and k >= 2 (KIND_BLOCK_PKK), against the oracle."""
+    rng = np.random.default_rng(11 + B + k)
+    Rk = rng.permutation(60000).astype(np.int64) + 1
+    Sk = rng.integers(0, 240000, size=300000)
+    oracle_check(hw, cuda, orc, Rk, Sk, hw.BloomFilterArgs.from_flag(variant, 1 << 21, k, B))
+
+
 @pytest.mark.parametrize("a", ARGS[:6], ids=str)
 def test_duplicates_negatives_and_extremes(hw, cuda, orc, a):
     args = mk(hw, a)
