@@ -1763,13 +1763,14 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
                 uint32_t wv[NW], bb[NW];  // slice word, bit index inside the segment
                 // packed words: the low log2(m / F) bits are the first bit's position in the slice
                 // (block in slice << log2B | bit in block), so its byte in LDS is one shift and mask
-                const uint32_t pkb = ((g.slice_bits - 1u) >> 3) & ~3u;
+                constexpr bool pk = (KIND == KIND_BLOCK_PK1 || KIND == KIND_BLOCK_PKK) && SEG1;
+                const uint32_t lw = (uint32_t) __builtin_ctz(g.slice_bits) - 5u;  // slice words: 2^lw
 #pragma unroll
                 for (int i = 0; i < NW; i++) {
                     const uint32_t w = sweep_word(Sc, i >> 2, i & 3);
-                    if ((KIND == KIND_BLOCK_PK1 || KIND == KIND_BLOCK_PKK) && SEG1) {
+                    if (pk) {
                         bb[i] = w;  // (the test below uses only its low 5 bits)
-                        wv[i] = *(const uint32_t*) ((const char*) slice + ((w >> 3) & pkb));
+                        wv[i] = slice[__builtin_amdgcn_ubfe(w, 5u, lw)];
                         continue;
                     } else if (zfmt && SEG1) {  // first bit = crapwow(key) & (B - 1) (add_generic)
                         const uint32_t key = z_key(zinv, w, q, cq);
@@ -1781,11 +1782,20 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
                     wv[i] = slice[bb[i] >> 5];
                 }
                 // pass 1: this lane's survivor bits; the wave's survivor count by one DPP sum
+                if (pk) {  // bit = one bfe at the word's low 5 bits; the chunk quads' fill as one mask each
 #pragma unroll
-                for (int i = 0; i < NW; i++) {
-                    uint32_t ok = (wv[i] >> (bb[i] & 31u)) & ((uint32_t) (i & 3) < Sc.n[i >> 2] ? 1u : 0u);
-                    if (!SEG1) ok &= locate<KIND>(sweep_word(Sc, i >> 2, i & 3), g, inv, q).seg == seg ? 1u : 0u;
-                    pass |= ok << i;
+                    for (int i = 0; i < NW; i++) pass |= __builtin_amdgcn_ubfe(wv[i], bb[i], 1u) << i;
+                    uint32_t vm = 0;
+#pragma unroll
+                    for (int j = 0; j < kPC; j++) vm |= ((1u << Sc.n[j]) - 1u) << (4 * j);
+                    pass &= vm;
+                } else {
+#pragma unroll
+                    for (int i = 0; i < NW; i++) {
+                        uint32_t ok = (wv[i] >> (bb[i] & 31u)) & ((uint32_t) (i & 3) < Sc.n[i >> 2] ? 1u : 0u);
+                        if (!SEG1) ok &= locate<KIND>(sweep_word(Sc, i >> 2, i & 3), g, inv, q).seg == seg ? 1u : 0u;
+                        pass |= ok << i;
+                    }
                 }
                 const uint32_t pcnt = (uint32_t) __builtin_popcount(pass);
                 const uint32_t pinc = wave_incl_scan_dpp(pcnt);
