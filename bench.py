@@ -11,12 +11,12 @@ once, as a pipeline of joins runs; the phase breakdown comes from K synchronous 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (N > 1)
 
-N > 1: one rank per GPU (RCCL backend). Weak scaling by default: every rank joins the named
-workload (|R| = 128M replicated, its own |S| = 1024M, the same key multiset in a rank-seeded
-order), so the units all ranks process grow with N and the data path has no collective; every
-rank's counts must equal the golden. --scaling strong range-shards one |S| over the ranks instead
-(total |S| fixed). R is replicated and every rank builds the filter from it. Counts are reduced
-after the timed region.
+N > 1: one rank per GPU (RCCL backend). Strong scaling by default (BASELINE config 4): one
+|S| = 1024M range-sharded over the ranks (the reference's per-thread chunking of S,
+src/parallel_radix_join_bloom.c:1646-1672), R replicated, every rank builds the filter from its
+copy of R, so the data path has no collective; value = |S| / the slowest rank's time, and the
+per-rank counts summed over the ranks must equal the golden. --scaling weak (every rank its own
+full |S|) is an A/B option, never the default. Counts are reduced after the timed region.
 
 Prints ONE JSON line (rank 0) with roofline (dominant kernel, HIP-event timed) and cpu_baseline
 (the oracle's multithreaded restatement of the reference, "port", on a bounded sample).
@@ -51,12 +51,19 @@ def parse():
     ap.add_argument("-k", "--bloom-hashes", type=int, default=1)
     ap.add_argument("-B", "--bloom-block-size", type=int, default=1024)
     ap.add_argument("-n", "--nthreads", type=int, default=2, help="generator threads (multiset)")
-    ap.add_argument("--scaling", choices=("strong", "weak"), default="weak",
-                    help="weak: every rank a full |S| (the path shards with no data-path collective); "
-                         "strong: one |S| range-sharded over the ranks")
+    ap.add_argument("--scaling", choices=("strong", "weak"), default="strong",
+                    help="strong (default, BASELINE config 4): one |S| range-sharded over the ranks; "
+                         "weak (A/B only): every rank joins its own full |S|")
     ap.add_argument("--design", choices=("replicated", "partitioned"), default="replicated",
                     help="N > 1: R replicated on every rank (no exchange), or R and the join "
                          "partitioned over the ranks (R and survivor all-to-alls, slice all-gather)")
+    ap.add_argument("--transport", choices=("native", "torch"), default="native",
+                    help="--design partitioned: the library's own RCCL communicator (collectives on "
+                         "the join stream), or torch.distributed callbacks (the only choice when "
+                         "ranks share a GPU)")
+    ap.add_argument("--filter-bcast", action="store_true",
+                    help="replicated design: rank 0 builds the filter, ncclBroadcast sends it to "
+                         "every rank (the north_star's bitmap broadcast) instead of a rebuild per rank")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the PCIe-inclusive end-to-end time")
     ap.add_argument("--cpu-sample", type=int, default=0,
@@ -159,13 +166,23 @@ def main():
 
     if a.design == "partitioned":
         return run_partitioned(a, hw, torch, dist, rank, world, local, dR, dS, args, shared)
+    if a.filter_bcast:
+        if shared:
+            raise SystemExit("--filter-bcast needs one GPU per rank (RCCL)")
+        from hwbloomradixjoin_amd import pjoin
+        pjoin.comm_init()
+        pjoin.set_filter_broadcast(True)
 
     # one untimed parity run (counts reduced over ranks)
     st = hw.join_device(dR, dS, args)
     cdev = "cpu" if shared else "cuda"  # where the count / time reductions live
     counts = torch.tensor([st.filtered, st.matches], dtype=torch.int64, device=cdev)
     lo_c, hi_c = counts.clone(), counts.clone()
-    if dist:
+    per_rank = [[int(x) for x in counts.tolist()]]
+    if dist:  # every rank's own (filtered, matches), before the sum
+        gathered = [torch.empty_like(counts) for _ in range(world)]
+        dist.all_gather(gathered, counts.clone())
+        per_rank = [[int(x) for x in t.tolist()] for t in gathered]
         dist.all_reduce(counts)
         dist.all_reduce(lo_c, op=dist.ReduceOp.MIN)
         dist.all_reduce(hi_c, op=dist.ReduceOp.MAX)
@@ -279,7 +296,9 @@ def main():
                    "bloom": a.bloom_filter, "m": a.bloom_size, "k": a.bloom_hashes,
                    "B": a.bloom_block_size,
                    "parallelism": (f"dp{world}: every rank the whole |S| (own order), R replicated"
-                                   if a.scaling == "weak" else f"S range-sharded x{world}, R replicated")},
+                                   if a.scaling == "weak" else f"S range-sharded x{world}, R replicated"),
+                   "filter": ("built on rank 0, ncclBroadcast to every rank" if a.filter_bcast
+                              else "rebuilt from R on every rank")},
         "roofline": roofline,
         "cpu_baseline": cpu,
         "e2e": e2e,
@@ -289,7 +308,11 @@ def main():
                    "ranks_agree": ranks_agree if a.scaling == "weak" else None,
                    "golden": list(gold) if gold else None,
                    "ok": (gold == (filtered, matches) and (ranks_agree or a.scaling != "weak"))
-                         if gold else None},
+                         if gold else None,
+                   "per_rank": per_rank},
+        "dist": {"world_size_seen": dist.get_world_size() if dist else 1,
+                 "backend": dist.get_backend() if dist else None,
+                 "shared_gpu_rehearsal": shared},
         "phase_ms": {k[3:]: round(v, 4) for k, v in mean.items()},
         "published_ref": {"value": 3.98e8, "config": "blocked B=512 k=1 m=2^30, 2x Xeon Gold 6226 "
                           "48 threads (thesis data, BASELINE.md)"},
@@ -305,22 +328,33 @@ def run_partitioned(a, hw, torch, dist, rank, world, local, dR, dS, args, shared
     so a step is timed by wall clock between barriers + synchronize)."""
     from hwbloomradixjoin_amd import pjoin
     nR, nS_total = a.r_size, a.s_size
-    x = pjoin.TorchExchange(torch.device("cuda", local))
+    native = a.transport == "native" and not shared
+    if native:  # the library's own RCCL communicator, collectives on the join stream
+        pjoin.comm_init()
+
+        def join():
+            return pjoin.join_partitioned_rccl(dR, dS, nR, args)
+    else:  # torch.distributed callbacks (HWBRJ_PJ_FORCE_COLL=1: collectives even at world 1)
+        x = pjoin.TorchExchange(torch.device("cuda", local),
+                                force_collectives=os.environ.get("HWBRJ_PJ_FORCE_COLL") == "1")
+
+        def join():
+            return pjoin.join_partitioned(dR, dS, nR, args, x)
     cdev = "cpu" if shared else "cuda"
-    st = pjoin.join_partitioned(dR, dS, nR, args, x)
+    st = join()
     counts = torch.tensor([st.filtered, st.matches], dtype=torch.int64, device=cdev)
     if dist:
         dist.all_reduce(counts)
     filtered, matches = (int(v) for v in counts.tolist())
     for _ in range(a.warmup):
-        pjoin.join_partitioned(dR, dS, nR, args, x)
+        join()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     sums = {}
     for _ in range(a.steps):
-        st = pjoin.join_partitioned(dR, dS, nR, args, x)
+        st = join()
         for f in ("ms_total", "ms_r_scatter", "ms_r_index", "ms_build", "ms_s_scatter", "ms_surv",
                   "ms_join"):
             sums[f] = sums.get(f, 0.0) + getattr(st, f)
@@ -333,6 +367,8 @@ def run_partitioned(a, hw, torch, dist, rank, world, local, dR, dS, args, shared
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     if rank != 0:
+        if native:
+            pjoin.comm_destroy()
         if dist:
             dist.destroy_process_group()
         return
@@ -353,7 +389,8 @@ def run_partitioned(a, hw, torch, dist, rank, world, local, dR, dS, args, shared
                    "bloom": a.bloom_filter, "m": a.bloom_size, "k": a.bloom_hashes,
                    "B": a.bloom_block_size,
                    "parallelism": f"R and S range-sharded x{world}, partitions owned by ranks "
-                                  "(R + survivor all-to-all, slice all-gather)"},
+                                  "(R + survivor all-to-all, slice all-gather)",
+                   "transport": "native RCCL (join stream)" if native else "torch.distributed callbacks"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS * world,
                      "unit": "GB/s", "frac": round(achieved / (HBM_PEAK_GBS * world), 4),
                      "traffic": None, "algorithmic_bytes": alg_bytes,
@@ -362,9 +399,13 @@ def run_partitioned(a, hw, torch, dist, rank, world, local, dR, dS, args, shared
         "cpu_baseline": None,
         "parity": {"filtered": filtered, "matches": matches, "golden": list(gold) if gold else None,
                    "ok": (gold == (filtered, matches)) if gold else None},
+        "dist": {"world_size_seen": dist.get_world_size() if dist else 1,
+                 "backend": dist.get_backend() if dist else None, "shared_gpu_rehearsal": shared},
         "stage_ms_rank0": {k[3:]: round(v / K, 4) for k, v in sums.items()},
     }
     print(json.dumps(out), flush=True)
+    if native:
+        pjoin.comm_destroy()
     if dist:
         dist.destroy_process_group()
 

@@ -156,6 +156,7 @@ def lib() -> ctypes.CDLL:
         L.hwbrj_set_device.argtypes = [ctypes.c_int]
         L.hwbrj_last_error.restype = ctypes.c_char_p
         L.hwbrj_version.restype = ctypes.c_char_p
+        L.hwbrj_tsc_hz.restype = ctypes.c_uint64
         L.hwbrj_release.restype = None
         _LIB = L
     return _LIB

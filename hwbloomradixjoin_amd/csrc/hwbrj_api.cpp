@@ -47,6 +47,20 @@ void hwbrj_release(void) {
     if (e) e->release();
 }
 
+// The rate of the cycle counter behind "RUNTIME TOTAL, BUILD, PART (cycles)" (the reference's
+// rdtsc timers, src/rdtsc.h:35-68), measured once against the steady clock over 50 ms.
+uint64_t hwbrj_tsc_hz(void) {
+    static const uint64_t hz = [] {
+        const auto     t0 = std::chrono::steady_clock::now();
+        const uint64_t c0 = __rdtsc();
+        std::this_thread::sleep_for(std::chrono::milliseconds(50));
+        const uint64_t c1 = __rdtsc();
+        const double   s  = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        return (uint64_t) ((double) (c1 - c0) / s);
+    }();
+    return hz;
+}
+
 uint32_t hwbrj_hash_crc(uint32_t seed, int32_t key) { return crc_f_bitwise(seed ^ (uint32_t) key); }
 uint32_t hwbrj_hash_crapwow(uint32_t seed, int32_t key) { return crapwow(seed, (uint32_t) key); }
 
@@ -331,50 +345,84 @@ struct Shard {
     uint64_t      s0 = 0, s1 = 0;
     hwbrj_stats_t st{};
     double        h2d_usec = 0;
+    tuple_t*      dS = nullptr;  // this shard's S rows in HBM (staged before the timed region)
 };
 
-// Shards first, first + step, ... on device `dev`, one after the other on its Engine: H2D of R
-// once, then per shard H2D of its S rows and the join. Returns 0 or an error code.
-static int run_device_shards(int dev, int first, int step, const relation_t* relR,
-                             const relation_t* relS, const bloom_filter_args_t* args,
-                             std::vector<Shard>& shards, int algo) {
-    if (hipSetDevice(dev) != hipSuccess) {
+// The device copies of one device's shards (first, first + step, ...): R once, every shard's S.
+struct DeviceStage {
+    int      dev = 0;
+    tuple_t* dR  = nullptr;
+};
+
+static void free_stage(DeviceStage& ds, std::vector<Shard>& shards, int first, int step) {
+    (void) hipSetDevice(ds.dev);
+    (void) hipFree(ds.dR);
+    ds.dR = nullptr;
+    for (size_t g = first; g < shards.size(); g += step) {
+        (void) hipFree(shards[g].dS);
+        shards[g].dS = nullptr;
+    }
+}
+
+// Everything the reference does before its timer starts (src/parallel_radix_join_bloom.c:1560-1640:
+// allocations, the zeroed bitmap and tmp buffers): device allocations, the H2D copies of R and of
+// every shard's S rows, and the join's scratch (Engine::reserve). Returns 0 or an error code.
+static int stage_device_shards(DeviceStage& ds, int first, int step, const relation_t* relR,
+                               const relation_t* relS, const bloom_filter_args_t* args,
+                               std::vector<Shard>& shards, int algo) {
+    if (hipSetDevice(ds.dev) != hipSuccess) {
         set_last_error("hipSetDevice failed");
         return 11;
     }
     const uint64_t nR = relR->num_tuples;
-    uint64_t       smax = 0;
-    for (size_t g = first; g < shards.size(); g += step) smax = std::max(smax, shards[g].s1 - shards[g].s0);
-    tuple_t *dR = nullptr, *dS = nullptr;
-    if (hipMalloc((void**) &dR, (nR ? nR : 1) * sizeof(tuple_t)) != hipSuccess ||
-        hipMalloc((void**) &dS, (smax ? smax : 1) * sizeof(tuple_t)) != hipSuccess) {
+    if (hipMalloc((void**) &ds.dR, (nR ? nR : 1) * sizeof(tuple_t)) != hipSuccess) {
         set_last_error("hipMalloc of the input relations failed");
         return 12;
     }
-    int rc = 0;
-    // H2D outside the timed region (the reference's timer starts after its allocations).
     const auto h0 = std::chrono::steady_clock::now();
-    if (nR && hipMemcpy(dR, relR->tuples, nR * sizeof(tuple_t), hipMemcpyHostToDevice) != hipSuccess) {
+    if (nR && hipMemcpy(ds.dR, relR->tuples, nR * sizeof(tuple_t), hipMemcpyHostToDevice) != hipSuccess) {
         set_last_error("H2D copy failed");
-        rc = 13;
+        return 13;
     }
     double h2d_r = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - h0).count();
-    for (size_t g = first; g < shards.size() && rc == 0; g += step) {
+    for (size_t g = first; g < shards.size(); g += step) {
         Shard&         sh = shards[g];
         const uint64_t n  = sh.s1 - sh.s0;
-        const auto     h1 = std::chrono::steady_clock::now();
-        if (n && hipMemcpy(dS, relS->tuples + sh.s0, n * sizeof(tuple_t), hipMemcpyHostToDevice) != hipSuccess) {
+        if (hipMalloc((void**) &sh.dS, (n ? n : 1) * sizeof(tuple_t)) != hipSuccess) {
+            set_last_error("hipMalloc of the input relations failed");
+            return 12;
+        }
+        const auto h1 = std::chrono::steady_clock::now();
+        if (n && hipMemcpy(sh.dS, relS->tuples + sh.s0, n * sizeof(tuple_t), hipMemcpyHostToDevice) != hipSuccess) {
             set_last_error("H2D copy failed");
-            rc = 13;
-            break;
+            return 13;
         }
         sh.h2d_usec = h2d_r + std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - h1).count();
         h2d_r       = 0;
-        rc          = hwbrj_join_device_algo(dR, nR, dS, n, args, algo, nullptr, &sh.st);
     }
-    (void) hipFree(dR);
-    (void) hipFree(dS);
-    return rc;
+    Engine* e = engine_for_current_device();
+    if (!e) return 10;
+    for (size_t g = first; g < shards.size(); g += step) {  // grow-only: the largest shard decides
+        const int rc = e->reserve((const uint2*) ds.dR, nR, (const uint2*) shards[g].dS,
+                                  shards[g].s1 - shards[g].s0, args, algo);
+        if (rc) return rc;
+    }
+    return hipDeviceSynchronize() == hipSuccess ? 0 : 14;
+}
+
+// The timed part: the device's shards joined one after the other on its Engine.
+static int join_device_shards(const DeviceStage& ds, int first, int step, uint64_t nR,
+                              const bloom_filter_args_t* args, std::vector<Shard>& shards, int algo) {
+    if (hipSetDevice(ds.dev) != hipSuccess) {
+        set_last_error("hipSetDevice failed");
+        return 11;
+    }
+    for (size_t g = first; g < shards.size(); g += step) {
+        Shard&    sh = shards[g];
+        const int rc = hwbrj_join_device_algo(ds.dR, nR, sh.dS, sh.s1 - sh.s0, args, algo, nullptr, &sh.st);
+        if (rc) return rc;
+    }
+    return 0;
 }
 
 // algo: the per-partition join (HWBRJ_ALGO_PRO / PRH / PRHO, the reference's join_init_run
@@ -400,26 +448,39 @@ static result_t* run_host_join(relation_t* relR, relation_t* relS, int nthreads,
     }
     std::vector<int> rcs(nuse, 0);
     std::vector<std::string> errs(nuse);
-    const uint64_t c0 = __rdtsc();
-    if (nuse == 1) {
-        rcs[0] = run_device_shards(cur, 0, 1, relR, relS, args, shards, algo);
-        errs[0] = hwbrj_last_error();
-    } else {  // one host thread per device (the reference's nthreads workers, one per GPU)
-        std::vector<std::thread> th;
-        for (int d = 0; d < nuse; d++)
-            th.emplace_back([&, d] {
-                rcs[d]  = run_device_shards(d, d, nuse, relR, relS, args, shards, algo);
-                errs[d] = hwbrj_last_error();
-            });
-        for (auto& t : th) t.join();
-    }
-    const uint64_t c1 = __rdtsc();
-    (void) hipSetDevice(cur);
-    for (int d = 0; d < nuse; d++)
-        if (rcs[d]) {
-            set_last_error(errs[d]);
-            fatal("BPRO");
+    std::vector<DeviceStage> stage(nuse);
+    for (int d = 0; d < nuse; d++) stage[d].dev = nuse == 1 ? cur : d;
+    // one host thread per device (the reference's nthreads workers, one per GPU); phase 0 stages
+    // the inputs and scratch, phase 1 is the timed join
+    auto each_device = [&](int phase) {
+        auto work = [&](int d) {
+            rcs[d] = phase == 0 ? stage_device_shards(stage[d], d, nuse, relR, relS, args, shards, algo)
+                                : join_device_shards(stage[d], d, nuse, nR, args, shards, algo);
+            errs[d] = hwbrj_last_error();
+        };
+        if (nuse == 1) {
+            work(0);
+        } else {
+            std::vector<std::thread> th;
+            for (int d = 0; d < nuse; d++) th.emplace_back(work, d);
+            for (auto& t : th) t.join();
         }
+        for (int d = 0; d < nuse; d++)
+            if (rcs[d]) {
+                for (int d2 = 0; d2 < nuse; d2++) free_stage(stage[d2], shards, d2, nuse);
+                (void) hipSetDevice(cur);
+                set_last_error(errs[d]);
+                fatal("BPRO");
+            }
+    };
+    each_device(0);
+    // The timed region (src/parallel_radix_join_bloom.c:1107-1131 to :1477-1484): the joins only,
+    // so RUNTIME TOTAL (cycles) and TOTAL-TIME-USECS cover the same work.
+    const uint64_t c0 = __rdtsc();
+    each_device(1);
+    const uint64_t c1 = __rdtsc();
+    for (int d = 0; d < nuse; d++) free_stage(stage[d], shards, d, nuse);
+    (void) hipSetDevice(cur);
     // counts summed over shards; device times: the slowest device (its shards back to back)
     hwbrj_stats_t st{};
     std::vector<double> dev_ms(nuse, 0.0), dev_join(nuse, 0.0), dev_probe(nuse, 0.0);

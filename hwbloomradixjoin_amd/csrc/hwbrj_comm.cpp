@@ -1,0 +1,270 @@
+// hwbrj_comm.cpp -- the native RCCL transport of the multi-GPU joins.
+//
+// One RCCL communicator per device (one rank per GPU, one process or thread per rank), created from
+// a unique id the caller distributes (hwbrj_comm_unique_id on one rank, any side channel to the
+// others: torch.distributed, MPI, a file). Two users:
+//   * the partitioned join (hwbrj_join_partitioned_rccl): its R-chunk and survivor all-to-alls are
+//     grouped ncclSend / ncclRecv and its slice all-gather an in-place ncclAllGather, all enqueued
+//     on the join's own stream, so the kernels around them need no host synchronisation; only the
+//     per-destination counts cross to the host (they size the variable all-to-alls);
+//   * the replicated design's opt-in filter broadcast (hwbrj_set_filter_broadcast): rank 0 builds
+//     the slices and ncclBroadcast sends them to every rank over xGMI (the north_star's bitmap
+//     broadcast), instead of every rank rebuilding them from its copy of R.
+// librccl.so.1 is bound with dlopen at the first communicator, so a single-GPU process never maps
+// it (HWBRJ_RCCL_LIB overrides the path).
+#include <dlfcn.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <mutex>
+#include <string>
+#include <type_traits>
+#include <vector>
+
+#include <rccl/rccl.h>
+
+#include "hwbrj_engine.h"
+
+namespace hwbrj {
+
+namespace {
+
+struct Rccl {
+    bool        ok = false;
+    std::string err;
+    ncclResult_t (*GetUniqueId)(ncclUniqueId*)                                          = nullptr;
+    ncclResult_t (*CommInitRank)(ncclComm_t*, int, ncclUniqueId, int)                   = nullptr;
+    ncclResult_t (*CommDestroy)(ncclComm_t)                                             = nullptr;
+    ncclResult_t (*GroupStart)()                                                        = nullptr;
+    ncclResult_t (*GroupEnd)()                                                          = nullptr;
+    ncclResult_t (*Send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*Recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t)   = nullptr;
+    ncclResult_t (*AllGather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*Broadcast)(const void*, void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    const char* (*GetErrorString)(ncclResult_t)                                         = nullptr;
+};
+
+const Rccl& rccl() {
+    static Rccl      r;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        const char* path = getenv("HWBRJ_RCCL_LIB");
+        void*       h    = dlopen(path ? path : "librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+        if (!h && !path) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+        if (!h) {
+            const char* e = dlerror();
+            r.err = std::string("cannot load librccl.so.1: ") + (e ? e : "?");
+            return;
+        }
+        bool all = true;
+        auto sym = [&](auto& fn, const char* name) {
+            fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(dlsym(h, name));
+            if (!fn) {
+                all   = false;
+                r.err = std::string("librccl.so.1 lacks ") + name;
+            }
+        };
+        sym(r.GetUniqueId, "ncclGetUniqueId");
+        sym(r.CommInitRank, "ncclCommInitRank");
+        sym(r.CommDestroy, "ncclCommDestroy");
+        sym(r.GroupStart, "ncclGroupStart");
+        sym(r.GroupEnd, "ncclGroupEnd");
+        sym(r.Send, "ncclSend");
+        sym(r.Recv, "ncclRecv");
+        sym(r.AllGather, "ncclAllGather");
+        sym(r.Broadcast, "ncclBroadcast");
+        sym(r.GetErrorString, "ncclGetErrorString");
+        r.ok = all;
+    });
+    return r;
+}
+
+int fail_rccl(const char* what, ncclResult_t e) {
+    set_last_error(std::string(what) + ": " + rccl().GetErrorString(e));
+    return 30;
+}
+
+int need_rccl() {
+    if (rccl().ok) return 0;
+    set_last_error(rccl().err);
+    return 31;
+}
+
+#define RC_CALL(expr, what)                                     \
+    do {                                                        \
+        const ncclResult_t r_ = (expr);                         \
+        if (r_ != ncclSuccess) return fail_rccl(what, r_);      \
+    } while (0)
+
+// ------------------------------------------------------------ the native hwbrj_exchange_t
+// ctx is the Engine; every collective runs on its stream (the join's).
+void* nx_buffer(void* ctx, int slot, uint64_t bytes) {
+    Engine* e = (Engine*) ctx;
+    if (slot < 0 || slot >= HWBRJ_PJ_NSLOTS) return nullptr;
+    DevBuf* b = e->xslot(slot);
+    return b->ensure(bytes) ? b->p : nullptr;
+}
+
+int nx_alltoall_u64(void* ctx, const uint64_t* send, uint64_t* recv, uint64_t n) {
+    Engine*        e  = (Engine*) ctx;
+    const Rccl&    R  = rccl();
+    const int      W  = e->comm_world();
+    hipStream_t    st = e->stream();
+    ncclComm_t     c  = (ncclComm_t) e->comm();
+    const uint64_t nb = (uint64_t) W * n * 8;
+    if (!e->xcnt()->ensure(2 * nb)) {
+        set_last_error("hipMalloc failed (exchange counts)");
+        return 4;
+    }
+    uint64_t* ds = e->xcnt()->as<uint64_t>();
+    uint64_t* dr = ds + (uint64_t) W * n;
+    if (hipMemcpyAsync(ds, send, nb, hipMemcpyHostToDevice, st) != hipSuccess) return 1;
+    RC_CALL(R.GroupStart(), "ncclGroupStart");
+    for (int j = 0; j < W; j++) {
+        RC_CALL(R.Send(ds + (uint64_t) j * n, n, ncclUint64, j, c, st), "ncclSend (counts)");
+        RC_CALL(R.Recv(dr + (uint64_t) j * n, n, ncclUint64, j, c, st), "ncclRecv (counts)");
+    }
+    RC_CALL(R.GroupEnd(), "ncclGroupEnd");
+    if (hipMemcpyAsync(recv, dr, nb, hipMemcpyDeviceToHost, st) != hipSuccess) return 1;
+    return hipStreamSynchronize(st) == hipSuccess ? 0 : 1;
+}
+
+int nx_alltoallv(void* ctx, int sslot, const uint64_t* soff, const uint64_t* sbytes, int rslot,
+                 const uint64_t* roff, const uint64_t* rbytes) {
+    Engine*       e  = (Engine*) ctx;
+    const Rccl&   R  = rccl();
+    const int     W  = e->comm_world();
+    ncclComm_t    c  = (ncclComm_t) e->comm();
+    const uint8_t* s = (const uint8_t*) e->xslot(sslot)->p;
+    uint8_t*      d  = (uint8_t*) e->xslot(rslot)->p;
+    // a block of 0 bytes is neither sent nor received (its peer sees the same 0 in its counts)
+    RC_CALL(R.GroupStart(), "ncclGroupStart");
+    for (int j = 0; j < W; j++) {
+        if (sbytes[j]) RC_CALL(R.Send(s + soff[j], sbytes[j], ncclUint8, j, c, e->stream()), "ncclSend");
+        if (rbytes[j]) RC_CALL(R.Recv(d + roff[j], rbytes[j], ncclUint8, j, c, e->stream()), "ncclRecv");
+    }
+    RC_CALL(R.GroupEnd(), "ncclGroupEnd");
+    return 0;
+}
+
+int nx_allgather(void* ctx, int slot, uint64_t bytes) {
+    Engine*  e    = (Engine*) ctx;
+    uint8_t* base = (uint8_t*) e->xslot(slot)->p;
+    // in place: rank r's block already sits at r * bytes
+    RC_CALL(rccl().AllGather(base + (uint64_t) e->comm_rank() * bytes, base, bytes, ncclUint8,
+                             (ncclComm_t) e->comm(), e->stream()),
+            "ncclAllGather (filter slices)");
+    return 0;
+}
+
+}  // namespace
+
+int rccl_broadcast(void* comm, void* buf, size_t bytes, int root, hipStream_t stream) {
+    if (int rc = need_rccl()) return rc;
+    RC_CALL(rccl().Broadcast(buf, buf, bytes, ncclUint8, root, (ncclComm_t) comm, stream),
+            "ncclBroadcast (filter slices)");
+    return 0;
+}
+
+int Engine::comm_init(const uint8_t* unique_id, int world, int rank) {
+    if (int rc = need_rccl()) return rc;
+    if (world < 1 || rank < 0 || rank >= world) {
+        set_last_error("rank must lie in [0, world)");
+        return 2;
+    }
+    if (hipSetDevice(device_) != hipSuccess) {
+        set_last_error("hipSetDevice failed");
+        return 1;
+    }
+    comm_destroy();
+    ncclUniqueId id;
+    static_assert(sizeof(id.internal) == NCCL_UNIQUE_ID_BYTES, "unique id size");
+    memcpy(id.internal, unique_id, NCCL_UNIQUE_ID_BYTES);
+    ncclComm_t c = nullptr;
+    RC_CALL(rccl().CommInitRank(&c, world, id, rank), "ncclCommInitRank");
+    comm_       = c;
+    comm_world_ = world;
+    comm_rank_  = rank;
+    return 0;
+}
+
+int Engine::comm_destroy() {
+    if (!comm_) return 0;
+    (void) hipSetDevice(device_);
+    (void) hipStreamSynchronize(own_stream_);
+    const ncclResult_t e = rccl().CommDestroy((ncclComm_t) comm_);
+    comm_       = nullptr;
+    comm_world_ = 1;
+    comm_rank_  = 0;
+    return e == ncclSuccess ? 0 : fail_rccl("ncclCommDestroy", e);
+}
+
+int Engine::join_partitioned_rccl(const uint2* dR, uint64_t nR, uint64_t nR_total, const uint2* dS,
+                                  uint64_t nS, const bloom_filter_args_t* args, hwbrj_stats_t* st) {
+    if (!comm_) {
+        set_last_error("no communicator on this device (hwbrj_comm_init)");
+        return 32;
+    }
+    hwbrj_exchange_t x;
+    x.ctx          = this;
+    x.buffer       = nx_buffer;
+    x.alltoall_u64 = nx_alltoall_u64;
+    x.alltoallv    = nx_alltoallv;
+    x.allgather    = nx_allgather;
+    return join_partitioned(&x, comm_rank_, comm_world_, dR, nR, nR_total, dS, nS, args, st, true);
+}
+
+}  // namespace hwbrj
+
+using namespace hwbrj;
+
+extern "C" {
+
+int hwbrj_comm_unique_id(uint8_t* out) {
+    if (int rc = need_rccl()) return rc;
+    ncclUniqueId id;
+    RC_CALL(rccl().GetUniqueId(&id), "ncclGetUniqueId");
+    memcpy(out, id.internal, NCCL_UNIQUE_ID_BYTES);
+    return 0;
+}
+
+int hwbrj_comm_init(const uint8_t* unique_id, int world, int rank) {
+    Engine* e = engine_for_current_device();
+    if (!e) return 10;
+    return e->comm_init(unique_id, world, rank);
+}
+
+int hwbrj_comm_destroy(void) {
+    Engine* e = engine_for_current_device();
+    if (!e) return 10;
+    return e->comm_destroy();
+}
+
+int hwbrj_comm_info(int* world, int* rank) {
+    Engine* e = engine_for_current_device();
+    if (!e) return 10;
+    if (!e->has_comm()) {
+        set_last_error("no communicator on this device (hwbrj_comm_init)");
+        return 32;
+    }
+    if (world) *world = e->comm_world();
+    if (rank) *rank = e->comm_rank();
+    return 0;
+}
+
+int hwbrj_set_filter_broadcast(int on) {
+    Engine* e = engine_for_current_device();
+    if (!e) return 10;
+    e->set_filter_broadcast(on != 0);
+    return 0;
+}
+
+int hwbrj_join_partitioned_rccl(const tuple_t* d_R, uint64_t nR, uint64_t nR_total, const tuple_t* d_S,
+                                uint64_t nS, const bloom_filter_args_t* args, hwbrj_stats_t* stats) {
+    Engine* e = engine_for_current_device();
+    if (!e) return 10;
+    return e->join_partitioned_rccl((const uint2*) d_R, nR, nR_total, (const uint2*) d_S, nS, args, stats);
+}
+
+}  // extern "C"

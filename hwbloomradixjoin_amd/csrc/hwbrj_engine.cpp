@@ -260,8 +260,9 @@ void Engine::release() {
                       &istartS, &listS, &slices, &bitmap, &rjoin, &rrun, &surv, &survcnt, &survoff,
                       &dense, &small, &bpos, &colR, &colS, &mtab, &mcount, &jtask, &jparts, &pjList,
                       &pjLstart, &pjSweep, &pjTab, &pjRegion, &pjTot, &pjSoff, &pjIbase, &pjCnt, &pjOff,
-                      &pjIstart, &pjJobs, &ppoolR, &ppoolS, &rpay, &survpos, &dense2, &kkcnt})
+                      &pjIstart, &pjJobs, &ppoolR, &ppoolS, &rpay, &survpos, &dense2, &kkcnt, &xcnt_})
         b->release();
+    for (DevBuf& b : xslot_) b.release();
     have_filter_ = false;
 }
 
@@ -280,6 +281,15 @@ int Engine::run(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
 int Engine::run_async(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
                       const bloom_filter_args_t* args, hipStream_t stream, int jkind) {
     return enqueue(dR, nR, dS, nS, args, stream, false, jkind);
+}
+
+int Engine::reserve(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
+                    const bloom_filter_args_t* args, int jkind) {
+    alloc_only_  = true;
+    const int rc = enqueue(dR, nR, dS, nS, args, nullptr, false, jkind);
+    alloc_only_  = false;
+    last_nj_     = 0;  // buffers may be new: the next join clears its job table
+    return rc;
 }
 
 int Engine::run_mat(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
@@ -307,7 +317,8 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
         set_last_error("global-bitmap mode: materialized by the side pass");
         return kRcMatGlobal;
     }
-    if (!mat && g.mode == MODE_SLICE_BASIC && g.k > 1 && (uint64_t) g.k * nR <= (1ull << 31) &&
+    const bool kk1 = getenv("HWBRJ_DEV_KK1") != nullptr;  // A/B: basic k = 1 on the bit-pass path
+    if (!mat && g.mode == MODE_SLICE_BASIC && (g.k > 1 || kk1) && (uint64_t) g.k * nR <= (1ull << 31) &&
         !getenv("HWBRJ_DEV_KK_GATHER")) {
         if (!stream) stream = own_stream_;
         if (pending_) HWBRJ_CHECK(hipStreamWaitEvent(stream, ev_[8], 0));
@@ -376,6 +387,7 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
         set_last_error("hipMalloc failed (device memory)");
         return 4;
     }
+    if (alloc_only_) return 0;
     uint64_t* d_result   = small.as<uint64_t>();      // [0] matches
     uint64_t* d_dcount   = small.as<uint64_t>() + 1;  // [1] dense survivor count (global mode)
     uint64_t* d_filtered = small.as<uint64_t>() + 2;  // [2] S-tuples after filter
@@ -428,7 +440,15 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     bp.run_off     = rrun.as<uint32_t>() + sweeps_max * NSUB;
     bp.ppool       = mat ? ppoolR.as<uint32_t>() : nullptr;
     bp.out_pay     = mat ? rpay.as<uint32_t>() : nullptr;
+    // the north_star's bitmap broadcast (opt-in, hwbrj_set_filter_broadcast): rank 0 builds the
+    // slices, the other ranks only sub-partition R for the join and receive them over RCCL
+    const bool bcast = bcast_ && comm_ && slice_mode && !basic_kk;
+    bp.no_slices     = bcast && comm_rank_ != 0 ? 1u : 0u;
     launch_build(bp, F, stream);
+    if (bcast) {
+        const int rc = rccl_broadcast(comm_, slices.p, (size_t) F * nseg * g.seg_words * 4, 0, stream);
+        if (rc) return rc;
+    }
     if (basic_kk) {
         // basic k >= 2: the k bit positions of every R key, partitioned by slice with the S-side
         // scatter buffers (free until the S pass), then one LDS slice build per partition
@@ -669,6 +689,7 @@ int Engine::enqueue_basic_kk(const uint2* dR, uint64_t nR, const uint2* dS, uint
         set_last_error("hipMalloc failed (device memory)");
         return 4;
     }
+    if (alloc_only_) return 0;
     uint64_t* d_result   = small.as<uint64_t>();
     uint64_t* d_filtered = small.as<uint64_t>() + 2;
     uint64_t* cnt        = kkcnt.as<uint64_t>();  // [j]: candidates after pass j (j < k - 1); [NC - 1]: dummy

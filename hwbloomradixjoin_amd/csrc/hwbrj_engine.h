@@ -47,6 +47,10 @@ class Engine {
     int  run_async(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
                    const bloom_filter_args_t* args, hipStream_t stream, int jkind = 0);
     int  wait(hwbrj_stats_t* st);
+    // Allocates every buffer a join of these inputs needs, without launching it (the host BPRO
+    // stages this before its timed region, like the reference's allocations before its timer).
+    int  reserve(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
+                 const bloom_filter_args_t* args, int jkind = 0);
     int  export_filter(uint8_t* host_out, uint64_t nbytes);
     // The materializing join (the partitioned pipeline carrying payloads): st->matches = pairs
     // (all of them, also beyond cap). kRcMatGlobal: not for the global-bitmap mode.
@@ -61,13 +65,36 @@ class Engine {
                   uint64_t maxid, uint64_t threshold, double selectivity, uint64_t seed,
                   hipStream_t stream);
     // The partitioned multi-GPU join of rank `rank` (include/hwbrj.h hwbrj_join_partitioned).
+    // native: x is the library's own RCCL exchange, whose collectives are enqueued on this
+    // engine's stream (no host synchronisation before them).
     int  join_partitioned(const hwbrj_exchange_t* x, int rank, int world, const uint2* dR,
                           uint64_t nR, uint64_t nR_total, const uint2* dS, uint64_t nS,
-                          const bloom_filter_args_t* args, hwbrj_stats_t* st);
+                          const bloom_filter_args_t* args, hwbrj_stats_t* st, bool native = false);
     void release();
     int  device() const { return device_; }
 
+    // ---- native RCCL transport (hwbrj_comm.cpp) ----
+    int  comm_init(const uint8_t* unique_id, int world, int rank);
+    int  comm_destroy();
+    bool has_comm() const { return comm_ != nullptr; }
+    int  comm_world() const { return comm_world_; }
+    int  comm_rank() const { return comm_rank_; }
+    // the partitioned join over this engine's communicator
+    int  join_partitioned_rccl(const uint2* dR, uint64_t nR, uint64_t nR_total, const uint2* dS,
+                               uint64_t nS, const bloom_filter_args_t* args, hwbrj_stats_t* st);
+    // replicated design: the filter slices built on rank 0 only and broadcast (ncclBroadcast on the
+    // join stream) instead of rebuilt from R on every rank
+    void set_filter_broadcast(bool on) { bcast_ = on; }
+    hipStream_t stream() const { return own_stream_; }
+    DevBuf*     xslot(int s) { return &xslot_[s]; }
+    DevBuf*     xcnt() { return &xcnt_; }
+    void*       comm() const { return comm_; }
+
   private:
+    void*        comm_       = nullptr;  // ncclComm_t of this device's rank (hwbrj_comm_init)
+    int          comm_world_ = 1, comm_rank_ = 0;
+    bool         bcast_      = false;
+    DevBuf       xslot_[HWBRJ_PJ_NSLOTS], xcnt_;  // the native exchange's buffers
     int          device_;
     int          cus_ = 256;
     hipStream_t  own_stream_ = nullptr;
@@ -79,6 +106,7 @@ class Engine {
     bool         pending_args_ = false;
     uint64_t     pending_nS_   = 0;
     uint32_t     last_nj_      = 0;  // join jobs of the last enqueue (job_surv layout)
+    bool         alloc_only_   = false;  // reserve(): enqueue returns after its allocations
     int          enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
                          const bloom_filter_args_t* args, hipStream_t stream, bool dbg, int jkind,
                          const MatReq* mat = nullptr);
@@ -106,6 +134,10 @@ class Engine {
 
 Engine* engine_for_current_device();
 void    set_last_error(const std::string& s);
+
+// RCCL entry points used by the engine (hwbrj_comm.cpp; librccl is bound at first use). Return 0 or
+// an error code with the message in set_last_error.
+int rccl_broadcast(void* comm, void* buf, size_t bytes, int root, hipStream_t stream);
 
 // glibc's rand() (stdlib/random_r.c TYPE_3) with private state (hwbrj_gen.cpp).
 struct GlibcRand {

@@ -46,6 +46,7 @@ struct BuildParams {
     uint32_t         q_base;      // partition of workgroup 0 (list/sweep tables indexed from it)
     const uint32_t*  ppool;       // payloads of pool's words (materialization), or nullptr
     uint32_t*        out_pay;     // [sweeps][kBSlot]: the payloads of out_codes (ppool set)
+    uint32_t         no_slices;   // 1: join runs only (the slices arrive by broadcast from rank 0)
 };
 
 struct ProbeParams {

@@ -1463,6 +1463,7 @@ __global__ __launch_bounds__(1024) void k_build(BuildParams P) {
     const Geometry& g      = P.g;
     const uint32_t  NSUB   = 1u << g.log2NSUB;
     constexpr bool  slices = KIND != KIND_PASS;
+    const bool      wr     = slices && !P.no_slices;  // this rank builds the slices (uniform)
     const uint32_t  segw   = slices ? g.seg_words : 0;  // multiple of 4
     uint32_t*       slice  = lds;
     uint32_t*       inv    = slice + segw;
@@ -1476,7 +1477,7 @@ __global__ __launch_bounds__(1024) void k_build(BuildParams P) {
     uint32_t nsw = 0;  // sweeps sorted so far (selects the counter buffer)
     const uint32_t l0 = P.list_start[ql], l1 = P.list_start[ql + 1];
     const uint32_t sw0  = P.sweep_start[ql];
-    const uint32_t nseg = slices ? g.nseg : 1;
+    const uint32_t nseg = wr ? g.nseg : 1;
     constexpr uint32_t GRP = kBSweep * kBPQ;
     for (uint32_t seg = 0; seg < nseg; seg++) {
         for (uint32_t i = tid; i < segw; i += blockDim.x) slice[i] = 0;
@@ -1505,7 +1506,7 @@ __global__ __launch_bounds__(1024) void k_build(BuildParams P) {
                     const bool     ok = (uint32_t) t < SA.n[jj];
                     const uint32_t w  = sweep_word(SA, jj, t);
 #ifndef HWBRJ_ABL_BNOBITS
-                    if (slices && ok) {
+                    if (wr && ok) {
                         const Loc L = locate<KIND>(w, g, inv, q);
                         if (L.seg == seg) apply_bits<KIND, true>(L, g, slice);
                     }
@@ -1567,7 +1568,7 @@ __global__ __launch_bounds__(1024) void k_build(BuildParams P) {
             }
         }
         __syncthreads();
-        if (slices) {
+        if (wr) {
             uint4*       dst = (uint4*) (P.slices + ((uint64_t) q * g.nseg + seg) * segw);
             const uint4* src = (const uint4*) slice;
             for (uint32_t i = tid; i < segw / 4; i += blockDim.x) dst[i] = src[i];

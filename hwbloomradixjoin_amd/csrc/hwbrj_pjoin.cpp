@@ -13,7 +13,10 @@
 //      all-to-all), with their per-sub counts;
 //   7. the owner joins its partitions (k_join over the received runs, item_base).
 // The exchanges are the caller's (hwbrj_exchange_t: RCCL through torch.distributed, gloo, peer
-// copies); each is synchronous, so the host tables between them are built from finished data.
+// copies; each synchronous) or the library's own RCCL transport (hwbrj_comm.cpp: collectives on the
+// join stream). Host tables between them are built from counts the host has waited for. Before
+// every collective the ranks agree on their statuses, so a rank that fails alone (an oversized
+// shard, an allocation) makes every rank return instead of leaving its peers in the collective.
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -84,9 +87,10 @@ static bool pj_check_on() {
 
 int Engine::join_partitioned(const hwbrj_exchange_t* x, int rank, int world, const uint2* dR,
                              uint64_t nR, uint64_t nR_total, const uint2* dS, uint64_t nS,
-                             const bloom_filter_args_t* args, hwbrj_stats_t* st) {
+                             const bloom_filter_args_t* args, hwbrj_stats_t* st, bool native) {
     PJ_CHECK(hipSetDevice(device_));
     const auto t_start = std::chrono::steady_clock::now();
+    // Errors every rank sees alike (arguments, geometry): returned at once, on every rank.
     Geometry    g;
     std::string err;
     if (!plan_geometry(args, nR_total, &g, &err)) {
@@ -104,6 +108,7 @@ int Engine::join_partitioned(const hwbrj_exchange_t* x, int rank, int world, con
         return 9;
     }
     const uint32_t QL = F / (uint32_t) world, q0 = (uint32_t) rank * QL;
+    const uint32_t W  = (uint32_t) world;
     const bool     slice_mode = g.mode == MODE_SLICE_BLOCK || g.mode == MODE_SLICE_BASIC;
     const uint32_t nseg       = slice_mode ? g.nseg : 1;
     const uint32_t CH         = probe_chunks_per_item();
@@ -111,106 +116,153 @@ int Engine::join_partitioned(const hwbrj_exchange_t* x, int rank, int world, con
     const size_t   sc_lds = scatter_lds_bytes(g.log2F);
     const uint32_t G      = (uint32_t) cus_ * (uint32_t) std::max<size_t>(1, std::min<size_t>(2, 163840 / sc_lds));
     hipStream_t    stream = own_stream_;
-    if (pending_) PJ_CHECK(hipStreamWaitEvent(stream, ev_[8], 0));
-    const uint64_t capR = pj_region_cap(nR, G, F), capS = pj_region_cap(nS, G, F);
-    const uint64_t LR = (uint64_t) G * capR, LS = (uint64_t) G * capS;
-    if (G > 512 || LS > (1ull << 27) || LR > (1ull << 27) || capS >= (1u << 22) || capR >= (1u << 22)) {
-        set_last_error("shard too large for 27-bit chunk ids");
-        return 3;
-    }
-    const uint64_t GF = (uint64_t) G * F;
-    bool ok = true;
-    ok &= poolR.ensure(LR * 128) && metaR.ensure(LR * 4) && listR.ensure(LR * 4);
-    ok &= usedR.ensure(G * 4) && wgqcR.ensure(GF * 4) && wgqeR.ensure(GF * 4) && wgqoR.ensure(GF * 4);
-    ok &= lstartR.ensure((F + 1) * 4) && estartR.ensure((F + 1) * 8) && istartR.ensure((F + 1) * 4);
-    ok &= poolS.ensure(LS * 128) && metaS.ensure(LS * 4) && listS.ensure(LS * 4);
-    ok &= usedS.ensure(G * 4) && wgqcS.ensure(GF * 4) && wgqeS.ensure(GF * 4) && wgqoS.ensure(GF * 4);
-    ok &= lstartS.ensure((F + 1) * 4) && estartS.ensure((F + 1) * 8) && istartS.ensure((F + 1) * 4);
-    const uint64_t items_max = (LS / CH + F + 1) * nseg;
-    ok &= surv.ensure(nseg * LS * 128) && survcnt.ensure(items_max * NSUB * 4) && survoff.ensure(items_max * NSUB * 4);
-    ok &= small.ensure(128 + 64 * 128) && colR.ensure(F * 12) && colS.ensure(F * 12);
-    ok &= jtask.ensure((size_t) join_extra_tasks() * 8) && jparts.ensure((size_t) (2 * F * NSUB + 1) * 4);
-    if (!ok) {
-        set_last_error("hipMalloc failed (device memory)");
-        return 4;
-    }
-    const uint64_t slice_bytes = slice_mode ? (uint64_t) F * nseg * g.seg_words * 4 : 16;
-    uint32_t* d_slices = (uint32_t*) x->buffer(x->ctx, HWBRJ_PJ_SLICES, slice_bytes);
-    if (!d_slices) {
-        set_last_error("exchange buffer (slices) unavailable");
-        return 20;
-    }
-    uint64_t* d_result   = small.as<uint64_t>();
-    uint64_t* d_filtered = small.as<uint64_t>() + 2;
-    PJ_CHECK(hipMemsetAsync(small.p, 0, 64, stream));
-    PJ_CHECK(hipMemsetAsync(jparts.p, 0, jparts.bytes, stream));  // the probe adds into job_surv
+    // A callback transport runs its collectives on its own stream: the join stream is drained
+    // before each (the native RCCL transport enqueues them on the join stream itself).
+    auto drain = [&]() -> int {
+        if (!native) PJ_CHECK(hipStreamSynchronize(stream));
+        return 0;
+    };
+    // Errors of one rank only (its shard's capacity, an allocation, a launch, a table check) must
+    // not leave the others blocked in a collective it never enters: before every collective the
+    // ranks agree on their statuses (carried by the counts exchanges, else one u64 all-to-all),
+    // and all of them return together.
+    auto peers = [&](const uint64_t* status, uint64_t stride, int rc) -> int {
+        if (rc) return rc;  // (this rank's own message stays)
+        for (uint32_t j = 0; j < W; j++)
+            if (status[(uint64_t) j * stride]) {
+                set_last_error("partitioned join: rank " + std::to_string(j) + " failed (code " +
+                               std::to_string(status[(uint64_t) j * stride]) + ")");
+                return 22;
+            }
+        return 0;
+    };
+    auto agree = [&](int rc) -> int {
+        std::vector<uint64_t> s(W, (uint64_t) (uint32_t) rc), r(W, 0);
+        if (x->alltoall_u64(x->ctx, s.data(), r.data(), 1) != 0) {
+            set_last_error("exchange failed: status");
+            return 20;
+        }
+        return peers(r.data(), 1, rc);
+    };
+    const uint32_t NC = QL + 2;  // counts exchanges: QL partition counts, a total, the status
     std::vector<double> ms(8, 0.0);
     auto lap = [&, t = std::chrono::steady_clock::now()](int k) mutable {
         const auto n = std::chrono::steady_clock::now();
         ms[k] += std::chrono::duration<double, std::milli>(n - t).count();
         t = n;
     };
+    uint64_t capR = 0, capS = 0, LS = 0;
+    uint32_t* d_slices = nullptr;
+    void *sendC = nullptr, *recvC = nullptr;
+    uint32_t *sendE = nullptr, *recvE = nullptr, *sendS = nullptr, *sendM = nullptr, *recvS = nullptr,
+             *recvM = nullptr;
+    uint64_t* d_result   = nullptr;
+    uint64_t* d_filtered = nullptr;
+    std::vector<uint32_t> ls(F + 1, 0), lsS(F + 1, 0), isS(F + 1, 0);
+    std::vector<uint64_t> scnt((size_t) W * NC, 0), rcnt((size_t) W * NC, 0);
+    std::vector<uint64_t> soff(W), sbytes(W), roff(W), rbytes(W);
+    uint64_t              RC = 0, sweeps = 0, RI = 0, RW = 0;
+    std::vector<uint64_t> ritems(W), rwords(W), sofs;
+    ScatterParams sp{};
 
     // ------------------------------------------------------------- 1. R shard: local partitions
-    ScatterParams sp{};
-    sp.tabs       = d_tabs_;
-    sp.g          = g;
-    sp.src        = dR;
-    sp.n          = nR;
-    sp.pool       = poolR.as<uint32_t>();
-    sp.meta       = metaR.as<uint32_t>();
-    sp.wg_used    = usedR.as<uint32_t>();
-    sp.wgq_chunks = wgqcR.as<uint32_t>();
-    sp.wgq_elems  = wgqeR.as<uint32_t>();
-    sp.cap        = capR;
-    launch_scatter(sp, SRC_TUPLES, SIDE_R, G, stream);
-    launch_plan(wgqcR.as<uint32_t>(), wgqeR.as<uint32_t>(), G, g.log2F, wgqoR.as<uint32_t>(),
-                colR.as<uint32_t>() + 2 * F, colR.as<uint64_t>(), stream);
-    launch_list_fill(metaR.as<uint32_t>(), usedR.as<uint32_t>(), capR, g.log2F, wgqoR.as<uint32_t>(),
-                     colR.as<uint32_t>() + 2 * F, colR.as<uint64_t>(), (uint32_t) BSW, 1, lstartR.as<uint32_t>(),
-                     estartR.as<uint64_t>(), istartR.as<uint32_t>(), listR.as<uint32_t>(), G, stream);
-    std::vector<uint32_t> ls(F + 1);
-    PJ_CHECK(hipMemcpyAsync(ls.data(), lstartR.p, (F + 1) * 4, hipMemcpyDeviceToHost, stream));
-    PJ_CHECK(hipStreamSynchronize(stream));
-    const uint32_t nch = ls[F];
-    // ------------------------------------------------------------- 2. R exchange
-    void*     sendC = x->buffer(x->ctx, HWBRJ_PJ_R_SEND, std::max<uint64_t>(16, (uint64_t) nch * 128));
-    uint32_t* sendE = (uint32_t*) x->buffer(x->ctx, HWBRJ_PJ_R_SEND_ENT, std::max<uint64_t>(16, (uint64_t) nch * 4));
-    if (!sendC || !sendE) {
-        set_last_error("exchange buffer (R send) unavailable");
-        return 20;
-    }
-    PJ_STAGE("R scatter");
-    launch_pj_gather(poolR.as<uint32_t>(), listR.as<uint32_t>(), nch, sendC, sendE, stream);
-    PJ_STAGE("k_pj_gather");
-    // per destination j: chunks of its QL partitions, then the position of its block's first chunk
-    const uint32_t        W = (uint32_t) world;
-    std::vector<uint64_t> scnt((size_t) W * (QL + 1)), rcnt((size_t) W * (QL + 1));
-    for (uint32_t j = 0; j < W; j++) {
-        for (uint32_t i = 0; i < QL; i++) scnt[j * (QL + 1) + i] = ls[j * QL + i + 1] - ls[j * QL + i];
-        scnt[j * (QL + 1) + QL] = ls[j * QL];
-    }
-    PJ_CHECK(hipStreamSynchronize(stream));
+    const int rc1 = [&]() -> int {
+        if (pending_) PJ_CHECK(hipStreamWaitEvent(stream, ev_[8], 0));
+        capR = pj_region_cap(nR, G, F), capS = pj_region_cap(nS, G, F);
+        const uint64_t LR = (uint64_t) G * capR;
+        LS = (uint64_t) G * capS;
+        // (HWBRJ_DEV_PJ_FAIL_RANK=r, tests: rank r fails this check, as an oversized shard would)
+        const char* fr = getenv("HWBRJ_DEV_PJ_FAIL_RANK");
+        if (G > 512 || LS > (1ull << 27) || LR > (1ull << 27) || capS >= (1u << 22) || capR >= (1u << 22) ||
+            (fr && atoi(fr) == rank)) {
+            set_last_error("shard too large for 27-bit chunk ids");
+            return 3;
+        }
+        const uint64_t GF = (uint64_t) G * F;
+        bool ok = true;
+        ok &= poolR.ensure(LR * 128) && metaR.ensure(LR * 4) && listR.ensure(LR * 4);
+        ok &= usedR.ensure(G * 4) && wgqcR.ensure(GF * 4) && wgqeR.ensure(GF * 4) && wgqoR.ensure(GF * 4);
+        ok &= lstartR.ensure((F + 1) * 4) && estartR.ensure((F + 1) * 8) && istartR.ensure((F + 1) * 4);
+        ok &= poolS.ensure(LS * 128) && metaS.ensure(LS * 4) && listS.ensure(LS * 4);
+        ok &= usedS.ensure(G * 4) && wgqcS.ensure(GF * 4) && wgqeS.ensure(GF * 4) && wgqoS.ensure(GF * 4);
+        ok &= lstartS.ensure((F + 1) * 4) && estartS.ensure((F + 1) * 8) && istartS.ensure((F + 1) * 4);
+        const uint64_t items_max = (LS / CH + F + 1) * nseg;
+        ok &= surv.ensure(nseg * LS * 128) && survcnt.ensure(items_max * NSUB * 4) && survoff.ensure(items_max * NSUB * 4);
+        ok &= small.ensure(128 + 64 * 128) && colR.ensure(F * 12) && colS.ensure(F * 12);
+        ok &= jtask.ensure((size_t) join_extra_tasks() * 8) && jparts.ensure((size_t) (2 * F * NSUB + 1) * 4);
+        if (!ok) {
+            set_last_error("hipMalloc failed (device memory)");
+            return 4;
+        }
+        const uint64_t slice_bytes = slice_mode ? (uint64_t) F * nseg * g.seg_words * 4 : 16;
+        d_slices = (uint32_t*) x->buffer(x->ctx, HWBRJ_PJ_SLICES, slice_bytes);
+        if (!d_slices) {
+            set_last_error("exchange buffer (slices) unavailable");
+            return 20;
+        }
+        d_result   = small.as<uint64_t>();
+        d_filtered = small.as<uint64_t>() + 2;
+        PJ_CHECK(hipMemsetAsync(small.p, 0, 64, stream));
+        PJ_CHECK(hipMemsetAsync(jparts.p, 0, jparts.bytes, stream));  // the probe adds into job_surv
+        sp.tabs       = d_tabs_;
+        sp.g          = g;
+        sp.src        = dR;
+        sp.n          = nR;
+        sp.pool       = poolR.as<uint32_t>();
+        sp.meta       = metaR.as<uint32_t>();
+        sp.wg_used    = usedR.as<uint32_t>();
+        sp.wgq_chunks = wgqcR.as<uint32_t>();
+        sp.wgq_elems  = wgqeR.as<uint32_t>();
+        sp.cap        = capR;
+        launch_scatter(sp, SRC_TUPLES, SIDE_R, G, stream);
+        launch_plan(wgqcR.as<uint32_t>(), wgqeR.as<uint32_t>(), G, g.log2F, wgqoR.as<uint32_t>(),
+                    colR.as<uint32_t>() + 2 * F, colR.as<uint64_t>(), stream);
+        launch_list_fill(metaR.as<uint32_t>(), usedR.as<uint32_t>(), capR, g.log2F, wgqoR.as<uint32_t>(),
+                         colR.as<uint32_t>() + 2 * F, colR.as<uint64_t>(), (uint32_t) BSW, 1, lstartR.as<uint32_t>(),
+                         estartR.as<uint64_t>(), istartR.as<uint32_t>(), listR.as<uint32_t>(), G, stream);
+        PJ_CHECK(hipMemcpyAsync(ls.data(), lstartR.p, (F + 1) * 4, hipMemcpyDeviceToHost, stream));
+        PJ_CHECK(hipStreamSynchronize(stream));
+        const uint32_t nch = ls[F];
+        sendC = x->buffer(x->ctx, HWBRJ_PJ_R_SEND, std::max<uint64_t>(16, (uint64_t) nch * 128));
+        sendE = (uint32_t*) x->buffer(x->ctx, HWBRJ_PJ_R_SEND_ENT, std::max<uint64_t>(16, (uint64_t) nch * 4));
+        if (!sendC || !sendE) {
+            set_last_error("exchange buffer (R send) unavailable");
+            return 20;
+        }
+        PJ_STAGE("R scatter");
+        launch_pj_gather(poolR.as<uint32_t>(), listR.as<uint32_t>(), nch, sendC, sendE, stream);
+        PJ_STAGE("k_pj_gather");
+        // per destination j: chunks of its QL partitions, then the position of its block's first chunk
+        for (uint32_t j = 0; j < W; j++) {
+            for (uint32_t i = 0; i < QL; i++) scnt[j * NC + i] = ls[j * QL + i + 1] - ls[j * QL + i];
+            scnt[j * NC + QL] = ls[j * QL];
+        }
+        return drain();
+    }();
     lap(0);
-    PJ_XCHG(x->alltoall_u64(x->ctx, scnt.data(), rcnt.data(), QL + 1), "R chunk counts");
-    std::vector<uint64_t> soff(W), sbytes(W), roff(W), rbytes(W), rchunks(W);
-    uint64_t              RC = 0;
-    for (uint32_t j = 0; j < W; j++) {
-        soff[j]   = (uint64_t) ls[j * QL] * 128;
-        sbytes[j] = (uint64_t) (ls[(j + 1) * QL] - ls[j * QL]) * 128;
-        uint64_t c = 0;
-        for (uint32_t i = 0; i < QL; i++) c += rcnt[j * (QL + 1) + i];
-        rchunks[j] = c;
-        roff[j]    = RC * 128;
-        rbytes[j]  = c * 128;
-        RC += c;
-    }
-    void*     recvC = x->buffer(x->ctx, HWBRJ_PJ_R_RECV, std::max<uint64_t>(16, RC * 128 + 16));
-    uint32_t* recvE = (uint32_t*) x->buffer(x->ctx, HWBRJ_PJ_R_RECV_ENT, std::max<uint64_t>(16, RC * 4));
-    if (!recvC || !recvE) {
-        set_last_error("exchange buffer (R receive) unavailable");
-        return 20;
-    }
+    // ------------------------------------------------------------- 2. R exchange
+    for (uint32_t j = 0; j < W; j++) scnt[j * NC + QL + 1] = (uint64_t) (uint32_t) rc1;
+    PJ_XCHG(x->alltoall_u64(x->ctx, scnt.data(), rcnt.data(), NC), "R chunk counts");
+    if (const int rc = peers(rcnt.data() + QL + 1, NC, rc1)) return rc;
+    const int rc2 = [&]() -> int {
+        for (uint32_t j = 0; j < W; j++) {
+            soff[j]   = (uint64_t) ls[j * QL] * 128;
+            sbytes[j] = (uint64_t) (ls[(j + 1) * QL] - ls[j * QL]) * 128;
+            uint64_t c = 0;
+            for (uint32_t i = 0; i < QL; i++) c += rcnt[j * NC + i];
+            roff[j]   = RC * 128;
+            rbytes[j] = c * 128;
+            RC += c;
+        }
+        recvC = x->buffer(x->ctx, HWBRJ_PJ_R_RECV, std::max<uint64_t>(16, RC * 128 + 16));
+        recvE = (uint32_t*) x->buffer(x->ctx, HWBRJ_PJ_R_RECV_ENT, std::max<uint64_t>(16, RC * 4));
+        if (!recvC || !recvE) {
+            set_last_error("exchange buffer (R receive) unavailable");
+            return 20;
+        }
+        return 0;
+    }();
+    if (const int rc = agree(rc2)) return rc;
     PJ_XCHG(x->alltoallv(x->ctx, HWBRJ_PJ_R_SEND, soff.data(), sbytes.data(), HWBRJ_PJ_R_RECV, roff.data(), rbytes.data()),
             "R chunks");
     for (uint32_t j = 0; j < W; j++) soff[j] /= 32, sbytes[j] /= 32, roff[j] /= 32, rbytes[j] /= 32;
@@ -218,188 +270,200 @@ int Engine::join_partitioned(const hwbrj_exchange_t* x, int rank, int world, con
             "R chunk entries");
     lap(1);
     // ------------------------------------------------------------- 3. owned partitions: lists, build
-    // list of owned partition i = its chunks from source 0, 1, ...; sweeps of BSW chunks
-    std::vector<uint32_t> lsO(QL + 1, 0), swO(QL + 1, 0);
-    std::vector<int64_t>  tab((size_t) 4 * QL * W);
-    {
-        std::vector<uint64_t> inblk(W, 0);  // entries of source j already assigned (partition order)
-        uint64_t              pos = 0;
-        for (uint32_t i = 0; i < QL; i++) {
-            lsO[i] = (uint32_t) pos;
-            for (uint32_t j = 0; j < W; j++) {
-                const uint64_t c  = rcnt[j * (QL + 1) + i];
-                int64_t*       t  = &tab[4 * ((size_t) i * W + j)];
-                const uint64_t rb = roff[j] / 4;  // source j's first chunk / entry (roff: entry bytes)
-                t[0]               = (int64_t) (rb + inblk[j]);                       // first received entry
-                t[1]               = (int64_t) c;
-                t[2]               = (int64_t) pos;                                   // list position
-                t[3]               = (int64_t) rb - (int64_t) rcnt[j * (QL + 1) + QL];  // id adjustment
-                inblk[j] += c;
-                pos += c;
+    const int rc3 = [&]() -> int {
+        // list of owned partition i = its chunks from source 0, 1, ...; sweeps of BSW chunks
+        std::vector<uint32_t> lsO(QL + 1, 0), swO(QL + 1, 0);
+        std::vector<int64_t>  tab((size_t) 4 * QL * W);
+        {
+            std::vector<uint64_t> inblk(W, 0);  // entries of source j already assigned (partition order)
+            uint64_t              pos = 0;
+            for (uint32_t i = 0; i < QL; i++) {
+                lsO[i] = (uint32_t) pos;
+                for (uint32_t j = 0; j < W; j++) {
+                    const uint64_t c  = rcnt[j * NC + i];
+                    int64_t*       t  = &tab[4 * ((size_t) i * W + j)];
+                    const uint64_t rb = roff[j] / 4;  // source j's first chunk / entry (roff: entry bytes)
+                    t[0]               = (int64_t) (rb + inblk[j]);                // first received entry
+                    t[1]               = (int64_t) c;
+                    t[2]               = (int64_t) pos;                            // list position
+                    t[3]               = (int64_t) rb - (int64_t) rcnt[j * NC + QL];  // id adjustment
+                    inblk[j] += c;
+                    pos += c;
+                }
+                swO[i + 1] = swO[i] + (uint32_t) ((pos - lsO[i] + BSW - 1) / BSW);
             }
-            swO[i + 1] = swO[i] + (uint32_t) ((pos - lsO[i] + BSW - 1) / BSW);
+            lsO[QL] = (uint32_t) pos;
         }
-        lsO[QL] = (uint32_t) pos;
-    }
-    const uint64_t sweeps = swO[QL];
-    ok = pjList.ensure(std::max<uint64_t>(16, RC * 4)) && rjoin.ensure(std::max<uint64_t>(16, sweeps * SLOT * 4)) &&
-         rrun.ensure(std::max<uint64_t>(16, 2 * sweeps * NSUB * 4));
-    if (!ok) {
-        set_last_error("hipMalloc failed (device memory)");
-        return 4;
-    }
-    if (to_dev(pjTab, tab, stream) || to_dev(pjLstart, lsO, stream) || to_dev(pjSweep, swO, stream)) {
-        set_last_error("host tables to the device failed");
-        return 4;
-    }
-    if (pj_check_on()) {
-        for (size_t k = 0; k < (size_t) QL * W; k++) {
-            const int64_t* t = &tab[4 * k];
-            if (t[0] < 0 || t[1] < 0 || (uint64_t) (t[0] + t[1]) > RC || (uint64_t) (t[2] + t[1]) > RC)
-                PJ_FAIL("relist pair " + std::to_string(k) + " outside the received entries");
+        sweeps = swO[QL];
+        const bool ok = pjList.ensure(std::max<uint64_t>(16, RC * 4)) &&
+                        rjoin.ensure(std::max<uint64_t>(16, sweeps * SLOT * 4)) &&
+                        rrun.ensure(std::max<uint64_t>(16, 2 * sweeps * NSUB * 4));
+        if (!ok) {
+            set_last_error("hipMalloc failed (device memory)");
+            return 4;
         }
-        if (lsO[QL] != RC) PJ_FAIL("owned lists do not cover the received chunks");
-        std::vector<uint32_t> re(RC);
-        if (RC) PJ_CHECK(hipMemcpy(re.data(), recvE, RC * 4, hipMemcpyDeviceToHost));
-        for (size_t k = 0; k < (size_t) QL * W; k++) {
-            const int64_t* t = &tab[4 * k];
-            for (int64_t i = 0; i < t[1]; i++) {
-                const int64_t id = (int64_t) (re[t[0] + i] & ((1u << 27) - 1u)) + t[3];
-                if (id < 0 || (uint64_t) id >= RC)
-                    PJ_FAIL("received entry " + std::to_string(t[0] + i) + " maps to chunk " +
-                            std::to_string(id) + " of " + std::to_string(RC));
+        if (to_dev(pjTab, tab, stream) || to_dev(pjLstart, lsO, stream) || to_dev(pjSweep, swO, stream)) {
+            set_last_error("host tables to the device failed");
+            return 4;
+        }
+        if (pj_check_on()) {
+            for (size_t k = 0; k < (size_t) QL * W; k++) {
+                const int64_t* t = &tab[4 * k];
+                if (t[0] < 0 || t[1] < 0 || (uint64_t) (t[0] + t[1]) > RC || (uint64_t) (t[2] + t[1]) > RC)
+                    PJ_FAIL("relist pair " + std::to_string(k) + " outside the received entries");
+            }
+            if (lsO[QL] != RC) PJ_FAIL("owned lists do not cover the received chunks");
+            std::vector<uint32_t> re(RC);
+            PJ_CHECK(hipStreamSynchronize(stream));
+            if (RC) PJ_CHECK(hipMemcpy(re.data(), recvE, RC * 4, hipMemcpyDeviceToHost));
+            for (size_t k = 0; k < (size_t) QL * W; k++) {
+                const int64_t* t = &tab[4 * k];
+                for (int64_t i = 0; i < t[1]; i++) {
+                    const int64_t id = (int64_t) (re[t[0] + i] & ((1u << 27) - 1u)) + t[3];
+                    if (id < 0 || (uint64_t) id >= RC)
+                        PJ_FAIL("received entry " + std::to_string(t[0] + i) + " maps to chunk " +
+                                std::to_string(id) + " of " + std::to_string(RC));
+                }
             }
         }
-    }
-    launch_pj_relist(recvE, pjTab.as<int64_t>(), QL * W, pjList.as<uint32_t>(), stream);
-    PJ_STAGE("k_pj_relist");
-    BuildParams bp{};
-    bp.g           = g;
-    bp.tabs        = d_tabs_;
-    bp.pool        = (const uint32_t*) recvC;
-    bp.list        = pjList.as<uint32_t>();
-    bp.list_start  = pjLstart.as<uint32_t>();
-    bp.elem_start  = nullptr;
-    bp.slices      = slice_mode ? d_slices : nullptr;
-    bp.sweep_start = pjSweep.as<uint32_t>();
-    bp.out_codes   = rjoin.as<uint32_t>();
-    bp.run_cnt     = rrun.as<uint32_t>();
-    bp.run_off     = rrun.as<uint32_t>() + sweeps * NSUB;
-    bp.q_base      = q0;
-    launch_build(bp, QL, stream);
-    PJ_STAGE("k_build");
-    PJ_CHECK(hipGetLastError());
-    PJ_CHECK(hipStreamSynchronize(stream));
+        launch_pj_relist(recvE, pjTab.as<int64_t>(), QL * W, pjList.as<uint32_t>(), stream);
+        PJ_STAGE("k_pj_relist");
+        BuildParams bp{};
+        bp.g           = g;
+        bp.tabs        = d_tabs_;
+        bp.pool        = (const uint32_t*) recvC;
+        bp.list        = pjList.as<uint32_t>();
+        bp.list_start  = pjLstart.as<uint32_t>();
+        bp.elem_start  = nullptr;
+        bp.slices      = slice_mode ? d_slices : nullptr;
+        bp.sweep_start = pjSweep.as<uint32_t>();
+        bp.out_codes   = rjoin.as<uint32_t>();
+        bp.run_cnt     = rrun.as<uint32_t>();
+        bp.run_off     = rrun.as<uint32_t>() + sweeps * NSUB;
+        bp.q_base      = q0;
+        launch_build(bp, QL, stream);
+        PJ_STAGE("k_build");
+        PJ_CHECK(hipGetLastError());
+        return drain();
+    }();
     lap(2);
+    if (const int rc = agree(rc3)) return rc;
     // ------------------------------------------------------------- 4. the whole filter on every rank
     if (slice_mode && W > 1)
         PJ_XCHG(x->allgather(x->ctx, HWBRJ_PJ_SLICES, (uint64_t) QL * nseg * g.seg_words * 4), "filter slices");
     lap(3);
     // ------------------------------------------------------------- 5. S shard: partition, probe
-    sp.src        = dS;
-    sp.n          = nS;
-    sp.pool       = poolS.as<uint32_t>();
-    sp.meta       = metaS.as<uint32_t>();
-    sp.wg_used    = usedS.as<uint32_t>();
-    sp.wgq_chunks = wgqcS.as<uint32_t>();
-    sp.wgq_elems  = wgqeS.as<uint32_t>();
-    sp.cap        = capS;
-    launch_scatter(sp, SRC_TUPLES, SIDE_S, G, stream);
-    launch_plan(wgqcS.as<uint32_t>(), wgqeS.as<uint32_t>(), G, g.log2F, wgqoS.as<uint32_t>(),
-                colS.as<uint32_t>() + 2 * F, colS.as<uint64_t>(), stream);
-    launch_list_fill(metaS.as<uint32_t>(), usedS.as<uint32_t>(), capS, g.log2F, wgqoS.as<uint32_t>(),
-                     colS.as<uint32_t>() + 2 * F, colS.as<uint64_t>(), CH, nseg, lstartS.as<uint32_t>(),
-                     estartS.as<uint64_t>(), istartS.as<uint32_t>(), listS.as<uint32_t>(), G, stream);
-    ProbeParams pp{};
-    pp.g               = g;
-    pp.tabs            = d_tabs_;
-    pp.pool            = poolS.as<uint32_t>();
-    pp.list            = listS.as<uint32_t>();
-    pp.list_start      = lstartS.as<uint32_t>();
-    pp.item_start      = istartS.as<uint32_t>();
-    pp.slices          = slice_mode ? d_slices : nullptr;
-    pp.surv            = surv.as<uint32_t>();
-    pp.surv_seg_stride = LS * 32;
-    pp.surv_cnt        = survcnt.as<uint32_t>();
-    pp.surv_off        = survoff.as<uint32_t>();
-    pp.filtered        = d_filtered;
-    pp.job_surv        = jparts.as<uint32_t>() + F * NSUB;
-    const size_t   pl_lds = probe_lds_bytes(g, nullptr);
-    const uint32_t PG     = (uint32_t) cus_ * (uint32_t) std::max<size_t>(1, std::min<size_t>(2, 163840 / pl_lds));
-    launch_probe(pp, PG, stream);
-    PJ_STAGE("S scatter + probe");
-    std::vector<uint32_t> lsS(F + 1), isS(F + 1);
-    PJ_CHECK(hipMemcpyAsync(lsS.data(), lstartS.p, (F + 1) * 4, hipMemcpyDeviceToHost, stream));
-    PJ_CHECK(hipMemcpyAsync(isS.data(), istartS.p, (F + 1) * 4, hipMemcpyDeviceToHost, stream));
-    PJ_CHECK(hipStreamSynchronize(stream));
-    const uint32_t        I = isS[F];
-    std::vector<uint32_t> scntS((size_t) I * NSUB);
-    if (I) PJ_CHECK(hipMemcpy(scntS.data(), survcnt.p, (size_t) I * NSUB * 4, hipMemcpyDeviceToHost));
-    lap(4);
-    // ------------------------------------------------------------- 6. survivor exchange
-    std::vector<uint64_t> region(I), sofs(I + 1, 0);
-    std::vector<uint32_t> tot(I);
-    for (uint32_t q = 0; q < F; q++) {
-        const uint32_t npc = (isS[q + 1] - isS[q]) / nseg;
-        for (uint32_t it = isS[q]; it < isS[q + 1]; it++) {
-            const uint32_t local = it - isS[q], seg = local / npc, piece = local - seg * npc;
-            region[it] = (uint64_t) seg * (LS * 32) + (uint64_t) (lsS[q] + piece * CH) * 32;
-            uint32_t t = 0;
-            for (uint32_t s = 0; s < NSUB; s++) t += scntS[(size_t) it * NSUB + s];
-            tot[it]      = t;
-            sofs[it + 1] = sofs[it] + t;
+    std::vector<uint32_t> scntS;
+    uint32_t I = 0;
+    const int rc5 = [&]() -> int {
+        sp.src        = dS;
+        sp.n          = nS;
+        sp.pool       = poolS.as<uint32_t>();
+        sp.meta       = metaS.as<uint32_t>();
+        sp.wg_used    = usedS.as<uint32_t>();
+        sp.wgq_chunks = wgqcS.as<uint32_t>();
+        sp.wgq_elems  = wgqeS.as<uint32_t>();
+        sp.cap        = capS;
+        launch_scatter(sp, SRC_TUPLES, SIDE_S, G, stream);
+        launch_plan(wgqcS.as<uint32_t>(), wgqeS.as<uint32_t>(), G, g.log2F, wgqoS.as<uint32_t>(),
+                    colS.as<uint32_t>() + 2 * F, colS.as<uint64_t>(), stream);
+        launch_list_fill(metaS.as<uint32_t>(), usedS.as<uint32_t>(), capS, g.log2F, wgqoS.as<uint32_t>(),
+                         colS.as<uint32_t>() + 2 * F, colS.as<uint64_t>(), CH, nseg, lstartS.as<uint32_t>(),
+                         estartS.as<uint64_t>(), istartS.as<uint32_t>(), listS.as<uint32_t>(), G, stream);
+        ProbeParams pp{};
+        pp.g               = g;
+        pp.tabs            = d_tabs_;
+        pp.pool            = poolS.as<uint32_t>();
+        pp.list            = listS.as<uint32_t>();
+        pp.list_start      = lstartS.as<uint32_t>();
+        pp.item_start      = istartS.as<uint32_t>();
+        pp.slices          = slice_mode ? d_slices : nullptr;
+        pp.surv            = surv.as<uint32_t>();
+        pp.surv_seg_stride = LS * 32;
+        pp.surv_cnt        = survcnt.as<uint32_t>();
+        pp.surv_off        = survoff.as<uint32_t>();
+        pp.filtered        = d_filtered;
+        pp.job_surv        = jparts.as<uint32_t>() + F * NSUB;
+        const size_t   pl_lds = probe_lds_bytes(g, nullptr);
+        const uint32_t PG     = (uint32_t) cus_ * (uint32_t) std::max<size_t>(1, std::min<size_t>(2, 163840 / pl_lds));
+        launch_probe(pp, PG, stream);
+        PJ_STAGE("S scatter + probe");
+        PJ_CHECK(hipMemcpyAsync(lsS.data(), lstartS.p, (F + 1) * 4, hipMemcpyDeviceToHost, stream));
+        PJ_CHECK(hipMemcpyAsync(isS.data(), istartS.p, (F + 1) * 4, hipMemcpyDeviceToHost, stream));
+        PJ_CHECK(hipStreamSynchronize(stream));
+        I = isS[F];
+        scntS.resize((size_t) I * NSUB);
+        if (I) PJ_CHECK(hipMemcpy(scntS.data(), survcnt.p, (size_t) I * NSUB * 4, hipMemcpyDeviceToHost));
+        lap(4);
+        // ------------------------------------------------------------- 6. survivor exchange
+        std::vector<uint64_t> region(I);
+        std::vector<uint32_t> tot(I);
+        sofs.assign(I + 1, 0);
+        for (uint32_t q = 0; q < F; q++) {
+            const uint32_t npc = (isS[q + 1] - isS[q]) / nseg;
+            for (uint32_t it = isS[q]; it < isS[q + 1]; it++) {
+                const uint32_t local = it - isS[q], seg = local / npc, piece = local - seg * npc;
+                region[it] = (uint64_t) seg * (LS * 32) + (uint64_t) (lsS[q] + piece * CH) * 32;
+                uint32_t t = 0;
+                for (uint32_t s = 0; s < NSUB; s++) t += scntS[(size_t) it * NSUB + s];
+                tot[it]      = t;
+                sofs[it + 1] = sofs[it] + t;
+            }
         }
-    }
-    uint32_t* sendS = (uint32_t*) x->buffer(x->ctx, HWBRJ_PJ_S_SEND, std::max<uint64_t>(16, sofs[I] * 4));
-    uint32_t* sendM = (uint32_t*) x->buffer(x->ctx, HWBRJ_PJ_M_SEND, std::max<uint64_t>(16, (uint64_t) I * NSUB * 4));
-    if (!sendS || !sendM) {
-        set_last_error("exchange buffer (survivor send) unavailable");
-        return 20;
-    }
-    if (to_dev(pjRegion, region, stream) || to_dev(pjTot, tot, stream) || to_dev(pjSoff, sofs, stream)) {
-        set_last_error("host tables to the device failed");
-        return 4;
-    }
-    if (pj_check_on())
-        for (uint32_t it = 0; it < I; it++)
-            if (region[it] + tot[it] > nseg * LS * 32) PJ_FAIL("item region outside the survivor buffer");
-    launch_pj_surv_pack(surv.as<uint32_t>(), pjRegion.as<uint64_t>(), pjTot.as<uint32_t>(), pjSoff.as<uint64_t>(),
-                        I, sendS, stream);
-    PJ_STAGE("k_pj_surv_pack");
-    if (I) PJ_CHECK(hipMemcpyAsync(sendM, survcnt.p, (size_t) I * NSUB * 4, hipMemcpyDeviceToDevice, stream));
-    // per destination j: items of each of its partitions, then its survivor words
-    for (uint32_t j = 0; j < W; j++) {
-        for (uint32_t i = 0; i < QL; i++) scnt[j * (QL + 1) + i] = isS[j * QL + i + 1] - isS[j * QL + i];
-        scnt[j * (QL + 1) + QL] = sofs[isS[(j + 1) * QL]] - sofs[isS[j * QL]];
-    }
-    PJ_CHECK(hipStreamSynchronize(stream));
+        sendS = (uint32_t*) x->buffer(x->ctx, HWBRJ_PJ_S_SEND, std::max<uint64_t>(16, sofs[I] * 4));
+        sendM = (uint32_t*) x->buffer(x->ctx, HWBRJ_PJ_M_SEND, std::max<uint64_t>(16, (uint64_t) I * NSUB * 4));
+        if (!sendS || !sendM) {
+            set_last_error("exchange buffer (survivor send) unavailable");
+            return 20;
+        }
+        if (to_dev(pjRegion, region, stream) || to_dev(pjTot, tot, stream) || to_dev(pjSoff, sofs, stream)) {
+            set_last_error("host tables to the device failed");
+            return 4;
+        }
+        if (pj_check_on())
+            for (uint32_t it = 0; it < I; it++)
+                if (region[it] + tot[it] > nseg * LS * 32) PJ_FAIL("item region outside the survivor buffer");
+        launch_pj_surv_pack(surv.as<uint32_t>(), pjRegion.as<uint64_t>(), pjTot.as<uint32_t>(), pjSoff.as<uint64_t>(),
+                            I, sendS, stream);
+        PJ_STAGE("k_pj_surv_pack");
+        if (I) PJ_CHECK(hipMemcpyAsync(sendM, survcnt.p, (size_t) I * NSUB * 4, hipMemcpyDeviceToDevice, stream));
+        // per destination j: items of each of its partitions, then its survivor words
+        for (uint32_t j = 0; j < W; j++) {
+            for (uint32_t i = 0; i < QL; i++) scnt[j * NC + i] = isS[j * QL + i + 1] - isS[j * QL + i];
+            scnt[j * NC + QL] = sofs[isS[(j + 1) * QL]] - sofs[isS[j * QL]];
+        }
+        return drain();
+    }();
     lap(4);
-    PJ_XCHG(x->alltoall_u64(x->ctx, scnt.data(), rcnt.data(), QL + 1), "survivor counts");
-    std::vector<uint64_t> ritems(W), rwords(W);
-    uint64_t              RI = 0, RW = 0;
-    for (uint32_t j = 0; j < W; j++) {
-        uint64_t c = 0;
-        for (uint32_t i = 0; i < QL; i++) c += rcnt[j * (QL + 1) + i];
-        ritems[j] = c;
-        rwords[j] = rcnt[j * (QL + 1) + QL];
-        RI += c;
-        RW += rwords[j];
-    }
-    uint32_t* recvS = (uint32_t*) x->buffer(x->ctx, HWBRJ_PJ_S_RECV, std::max<uint64_t>(16, RW * 4));
-    uint32_t* recvM = (uint32_t*) x->buffer(x->ctx, HWBRJ_PJ_M_RECV, std::max<uint64_t>(16, RI * NSUB * 4));
-    if (!recvS || !recvM) {
-        set_last_error("exchange buffer (survivor receive) unavailable");
-        return 20;
-    }
+    for (uint32_t j = 0; j < W; j++) scnt[j * NC + QL + 1] = (uint64_t) (uint32_t) rc5;
+    PJ_XCHG(x->alltoall_u64(x->ctx, scnt.data(), rcnt.data(), NC), "survivor counts");
+    if (const int rc = peers(rcnt.data() + QL + 1, NC, rc5)) return rc;
+    const int rc6 = [&]() -> int {
+        for (uint32_t j = 0; j < W; j++) {
+            uint64_t c = 0;
+            for (uint32_t i = 0; i < QL; i++) c += rcnt[j * NC + i];
+            ritems[j] = c;
+            rwords[j] = rcnt[j * NC + QL];
+            RI += c;
+            RW += rwords[j];
+        }
+        recvS = (uint32_t*) x->buffer(x->ctx, HWBRJ_PJ_S_RECV, std::max<uint64_t>(16, RW * 4));
+        recvM = (uint32_t*) x->buffer(x->ctx, HWBRJ_PJ_M_RECV, std::max<uint64_t>(16, RI * NSUB * 4));
+        if (!recvS || !recvM) {
+            set_last_error("exchange buffer (survivor receive) unavailable");
+            return 20;
+        }
+        return 0;
+    }();
+    if (const int rc = agree(rc6)) return rc;
     {
-        uint64_t so = 0, ro = 0;
+        uint64_t ro = 0;
         for (uint32_t j = 0; j < W; j++) {
             soff[j]   = sofs[isS[j * QL]] * 4;
             sbytes[j] = (sofs[isS[(j + 1) * QL]] - sofs[isS[j * QL]]) * 4;
             roff[j]   = ro * 4;
             rbytes[j] = rwords[j] * 4;
             ro += rwords[j];
-            (void) so;
         }
     }
     PJ_XCHG(x->alltoallv(x->ctx, HWBRJ_PJ_S_SEND, soff.data(), sbytes.data(), HWBRJ_PJ_S_RECV, roff.data(), rbytes.data()),
@@ -418,9 +482,13 @@ int Engine::join_partitioned(const hwbrj_exchange_t* x, int rank, int world, con
             "survivor run counts");
     lap(5);
     // ------------------------------------------------------------- 7. join of the owned partitions
+    // (no collective follows: a failure here is this rank's alone)
     // items of owned partition i: those of source 0, 1, ... (each source's block is in partition order)
     std::vector<uint32_t> rm((size_t) RI * NSUB);
-    if (RI) PJ_CHECK(hipMemcpy(rm.data(), recvM, (size_t) RI * NSUB * 4, hipMemcpyDeviceToHost));
+    if (RI) {  // (on the join stream: a native transport's receive is still in flight)
+        PJ_CHECK(hipMemcpyAsync(rm.data(), recvM, (size_t) RI * NSUB * 4, hipMemcpyDeviceToHost, stream));
+        PJ_CHECK(hipStreamSynchronize(stream));
+    }
     std::vector<uint64_t> ibase(RI);
     std::vector<uint32_t> icnt((size_t) RI * NSUB), ioff((size_t) RI * NSUB), istart(QL + 1, 0), jobs((size_t) QL * NSUB, 0);
     {
@@ -434,7 +502,7 @@ int Engine::join_partitioned(const hwbrj_exchange_t* x, int rank, int world, con
         for (uint32_t i = 0; i < QL; i++) {
             istart[i] = out;
             for (uint32_t j = 0; j < W; j++) {
-                for (uint64_t k = 0; k < rcnt[j * (QL + 1) + i]; k++) {
+                for (uint64_t k = 0; k < rcnt[j * NC + i]; k++) {
                     const uint64_t src = jitem[j] + jpos[j]++;
                     ibase[out]         = jword[j] + wpos[j];
                     uint32_t o = 0;
@@ -500,6 +568,7 @@ int Engine::join_partitioned(const hwbrj_exchange_t* x, int rank, int world, con
     lap(6);
     pending_ = false;
     have_filter_ = false;  // (the slices live in the caller's exchange buffer)
+    last_nj_     = 0;      // job_surv holds this join's counts: the next enqueue clears the table
     if (st) {
         memset(st, 0, sizeof(*st));
         st->filtered       = args ? small_h[2] : nS;
@@ -509,8 +578,9 @@ int Engine::join_partitioned(const hwbrj_exchange_t* x, int rank, int world, con
         st->partitions     = F;
         st->subparts       = NSUB;
         st->slice_segments = nseg;
-        // host wall time per stage (the exchanges are synchronous): R pass, R exchange, build,
-        // slice all-gather, S pass (scatter + probe), survivor exchange, join
+        // host wall time per stage: R pass, R exchange, build, slice all-gather, S pass (scatter +
+        // probe), survivor exchange, join. With the native transport a stage's kernels may finish
+        // inside the next stage's host wait (the stream is only drained where counts are read).
         st->ms_r_scatter = ms[0];
         st->ms_r_index   = ms[1];  // R exchange
         st->ms_build     = ms[2];

@@ -1,6 +1,8 @@
-"""The partitioned multi-GPU join (include/hwbrj.h hwbrj_join_partitioned) driven over
-torch.distributed: one process per GPU, RCCL ("nccl") over xGMI, or gloo (host copies) for
-rehearsals on fewer GPUs than ranks.
+"""The multi-GPU joins over torch.distributed: one process per GPU. The partitioned join
+(include/hwbrj.h) runs either over the library's own RCCL communicator (comm_init +
+join_partitioned_rccl: collectives on the join stream) or over torch.distributed callbacks
+(TorchExchange: RCCL ("nccl") or gloo through host memory, for rehearsals with several ranks on one
+GPU). set_filter_broadcast switches the replicated design to the north_star's bitmap broadcast.
 
 SURVEY.md s8f row 3. Rank r of G owns radix partitions [r F / G, (r + 1) F / G): R chunks and
 S survivors travel to the owner (variable all-to-alls), the owners' filter slices are all-gathered
@@ -33,7 +35,9 @@ class TorchExchange:
 
     NSLOTS = 9
 
-    def __init__(self, device, group=None):
+    def __init__(self, device, group=None, force_collectives: bool = False):
+        """force_collectives: run the process group's collectives even at world 1 (where every
+        exchange is otherwise a local copy), so a one-GPU run exercises the RCCL branches."""
         import torch
         import torch.distributed as dist
         self.torch, self.dist, self.group = torch, dist, group
@@ -42,6 +46,7 @@ class TorchExchange:
         self.world = dist.get_world_size(group) if self.on else 1
         self.rank = dist.get_rank(group) if self.on else 0
         self.gloo = self.on and dist.get_backend(group) == "gloo"
+        self.local = self.world == 1 and not (force_collectives and self.on)
         self.slots = [None] * self.NSLOTS
         self.error = None
         self.cuda = self.device.type == "cuda"
@@ -74,7 +79,7 @@ class TorchExchange:
         def go():
             W = self.world
             s = np.ctypeslib.as_array(send, shape=(W * n,)).astype(np.int64)
-            if W == 1:
+            if self.local:
                 np.ctypeslib.as_array(recv, shape=(n,))[:] = s
                 return 0
             st = self.torch.from_numpy(s)
@@ -91,11 +96,11 @@ class TorchExchange:
             W = self.world
             so, sb = [soff[j] for j in range(W)], [sbytes[j] for j in range(W)]
             ro, rb = [roff[j] for j in range(W)], [rbytes[j] for j in range(W)]
-            for j in range(W - 1):  # the blocks are consecutive (one all_to_all_single)
-                assert so[j] + sb[j] == so[j + 1] and ro[j] + rb[j] == ro[j + 1]
+            # the library lays the blocks out consecutively (one all_to_all_single); it agrees on
+            # every rank's status before each exchange, so no rank may bail out here alone
             src = self.slots[sslot][so[0]: so[-1] + sb[-1]]
             dst = self.slots[rslot][ro[0]: ro[-1] + rb[-1]]
-            if W == 1:
+            if self.local:
                 dst.copy_(src)
                 self._sync()  # (the library reads it on its own stream)
                 return 0
@@ -113,7 +118,7 @@ class TorchExchange:
         def go():
             W, r = self.world, self.rank
             full = self.slots[slot][: W * nbytes]
-            if W == 1:
+            if self.local:
                 return 0
             mine = full[r * nbytes: (r + 1) * nbytes]
             if self.gloo:
@@ -147,7 +152,63 @@ def join_partitioned(R, S, nR_total: int, args=None, exchange: TorchExchange | N
     return Stats(**{n: getattr(st, n) for n, _ in _Stats._fields_})
 
 
+def comm_init(group=None) -> tuple[int, int]:
+    """The library's own RCCL communicator on the current device (hwbrj_comm_init): rank 0 of the
+    torch.distributed group draws the unique id (hwbrj_comm_unique_id), the group broadcasts it,
+    every rank joins. Without a process group: a world-1 communicator. Returns (world, rank)."""
+    import torch
+    import torch.distributed as dist
+    L = lib()
+    on = dist.is_available() and dist.is_initialized()
+    world = dist.get_world_size(group) if on else 1
+    rank = dist.get_rank(group) if on else 0
+    uid = (ctypes.c_uint8 * 128)()
+    if rank == 0:
+        _err(L.hwbrj_comm_unique_id(uid), "hwbrj_comm_unique_id")
+    if on:
+        t = torch.tensor(list(bytes(uid)), dtype=torch.uint8)
+        if dist.get_backend(group) != "gloo":
+            t = t.cuda()
+        dist.broadcast(t, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+        uid = (ctypes.c_uint8 * 128)(*t.cpu().tolist())
+    _err(L.hwbrj_comm_init(uid, world, rank), "hwbrj_comm_init")
+    return world, rank
+
+
+def comm_destroy() -> None:
+    _err(lib().hwbrj_comm_destroy(), "hwbrj_comm_destroy")
+
+
+def set_filter_broadcast(on: bool) -> None:
+    """The replicated design with the north_star's bitmap broadcast (hwbrj_set_filter_broadcast):
+    rank 0 builds the filter slices, ncclBroadcast delivers them to every rank. Needs comm_init."""
+    _err(lib().hwbrj_set_filter_broadcast(1 if on else 0), "hwbrj_set_filter_broadcast")
+
+
+def join_partitioned_rccl(R, S, nR_total: int, args=None) -> Stats:
+    """join_partitioned over the library's own RCCL communicator (comm_init first): the all-to-alls
+    and the slice all-gather are RCCL calls on the join stream, no Python in between."""
+    _check_rel(R, S)
+    a = args._c() if args is not None else None
+    st = _Stats()
+    rc = lib().hwbrj_join_partitioned_rccl(_ptr(R), R.shape[0], int(nR_total), _ptr(S), S.shape[0],
+                                           ctypes.byref(a) if a is not None else None, ctypes.byref(st))
+    _err(rc, "hwbrj_join_partitioned_rccl")
+    return Stats(**{n: getattr(st, n) for n, _ in _Stats._fields_})
+
+
 def _bind(L):
+    L.hwbrj_comm_unique_id.restype = ctypes.c_int
+    L.hwbrj_comm_unique_id.argtypes = [ctypes.c_void_p]
+    L.hwbrj_comm_init.restype = ctypes.c_int
+    L.hwbrj_comm_init.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+    L.hwbrj_comm_destroy.restype = ctypes.c_int
+    L.hwbrj_set_filter_broadcast.restype = ctypes.c_int
+    L.hwbrj_set_filter_broadcast.argtypes = [ctypes.c_int]
+    L.hwbrj_join_partitioned_rccl.restype = ctypes.c_int
+    L.hwbrj_join_partitioned_rccl.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
+                                              ctypes.c_void_p, ctypes.c_uint64,
+                                              ctypes.POINTER(_BloomArgs), ctypes.POINTER(_Stats)]
     L.hwbrj_join_partitioned.restype = ctypes.c_int
     L.hwbrj_join_partitioned.argtypes = [ctypes.POINTER(_Exchange), ctypes.c_int, ctypes.c_int,
                                          ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,

@@ -193,6 +193,32 @@ int hwbrj_join_partitioned(const hwbrj_exchange_t * x, int rank, int world, cons
                            uint64_t nR, uint64_t nR_total, const tuple_t * d_S, uint64_t nS,
                            const bloom_filter_args_t * args, hwbrj_stats_t * stats);
 
+/* ---- native RCCL transport (this build) ----
+ * One communicator per device (one rank per GPU). hwbrj_comm_unique_id fills the 128-byte
+ * ncclUniqueId on one rank; the caller hands the bytes to every rank (torch.distributed, MPI, a
+ * file), and each calls hwbrj_comm_init on its device. librccl.so.1 is loaded at the first call
+ * (HWBRJ_RCCL_LIB overrides the path); 31 = it could not be loaded, 30 = an RCCL error, 32 = no
+ * communicator.
+ *   hwbrj_join_partitioned_rccl  hwbrj_join_partitioned over the communicator: the R-chunk and
+ *                                survivor all-to-alls (grouped ncclSend / ncclRecv) and the slice
+ *                                all-gather (in-place ncclAllGather) run on the join's stream;
+ *                                only the per-rank counts that size the all-to-alls reach the host.
+ *   hwbrj_set_filter_broadcast   the replicated design (hwbrj_join_device*, S sharded, R on every
+ *                                rank) with the north_star's bitmap broadcast: rank 0 builds the
+ *                                filter slices, ncclBroadcast sends them to every rank on the join
+ *                                stream; the other ranks only sub-partition R for the join. Off by
+ *                                default (every rank rebuilds the slices from its R).
+ *                                Slice modes only (blocked/sectorized, basic k = 1); a collective:
+ *                                every rank must enqueue the same joins. */
+int hwbrj_comm_unique_id(uint8_t * unique_id_out /* 128 bytes */);
+int hwbrj_comm_init(const uint8_t * unique_id /* 128 bytes */, int world, int rank);
+int hwbrj_comm_destroy(void);
+int hwbrj_comm_info(int * world, int * rank);
+int hwbrj_set_filter_broadcast(int on);
+int hwbrj_join_partitioned_rccl(const tuple_t * d_R, uint64_t nR, uint64_t nR_total,
+                                const tuple_t * d_S, uint64_t nS, const bloom_filter_args_t * args,
+                                hwbrj_stats_t * stats);
+
 /* Fill d_out / out with the reference generator's key multiset (src/generator.c:304-415 with
  * `nthreads` generator threads) in a seeded permuted order; payload = row index. */
 int hwbrj_generate_device(tuple_t * d_out, uint64_t n, uint32_t nthreads, uint64_t maxid,
@@ -237,6 +263,10 @@ int      hwbrj_rand_stream(uint32_t seed, int32_t * out, uint64_t n);
 /* The filter built by the last join, in the reference's byte layout (src/bloom_filter.c:143-171:
  * m/8 bytes, bit h of a block at byte h>>3, bit h&7). nbytes must be m/8. */
 int hwbrj_export_filter(uint8_t * host_out, uint64_t nbytes);
+
+/* Cycles per second of the counter behind BPRO's "RUNTIME TOTAL, BUILD, PART (cycles)" line (the
+ * reference's rdtsc timers, src/rdtsc.h:35-68), calibrated once against the steady clock. */
+uint64_t hwbrj_tsc_hz(void);
 
 /* Scalar hashes on the host (test hooks): crc32c(seed,key) and CrapWow(seed,key). */
 uint32_t hwbrj_hash_crc(uint32_t seed, int32_t key);

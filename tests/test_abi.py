@@ -112,3 +112,13 @@ def test_package_refuses_without_library(tmp_path):
             "try:\n    hw.lib()\nexcept ImportError as e:\n    print('RAISED', e)\n") % (ROOT, str(tmp_path))
     out = subprocess.run(["python3", "-c", code], capture_output=True, text=True, timeout=120)
     assert "RAISED" in out.stdout
+
+
+def test_rccl_binding_draws_unique_id(hw):
+    """The native RCCL transport binds librccl.so.1 at first use (hwbrj_comm.cpp) and draws the
+    128-byte ncclUniqueId a multi-GPU job hands to every rank (no GPU needed for the id)."""
+    import ctypes
+    a, b = (ctypes.c_uint8 * 128)(), (ctypes.c_uint8 * 128)()
+    assert hw.lib().hwbrj_comm_unique_id(a) == 0, hw.lib().hwbrj_last_error()
+    assert hw.lib().hwbrj_comm_unique_id(b) == 0
+    assert any(bytes(a)) and bytes(a) != bytes(b)

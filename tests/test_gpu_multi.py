@@ -1,0 +1,176 @@
+"""GPU tests of the multi-GPU machinery on one MI355X: the library's native RCCL transport
+(hwbrj_comm.cpp) at world 1, the north_star's filter broadcast in the replicated design, bench.py's
+N > 1 paths over the RCCL process group at world 1, and the partitioned join's status agreement
+(a rank that fails alone makes every rank return instead of hanging in a collective).
+
+RCCL refuses two ranks on one GPU, so runs with several ranks share the GPU over gloo
+(HWBRJ_BENCH_SHARED_GPU=1) and the torch.distributed callback transport; the native transport and
+the broadcast run at world 1, where their RCCL calls (grouped send/recv to self, in-place
+all-gather, broadcast from rank 0) execute for real on the join stream.
+
+Bar: bit-exact counts against the goldens or the oracle on the same inputs.
+"""
+import json
+import os
+import signal
+import socket
+import subprocess
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+GOLD = json.load(open(os.path.join(HERE, "golden", "survey_counts.json")))
+INT_MAX = 2**31 - 1
+
+
+def to_dev(cuda, a):
+    return cuda.from_numpy(np.ascontiguousarray(a, dtype=np.int32)).cuda()
+
+
+def rel(keys):
+    keys = np.asarray(keys, dtype=np.int64).astype(np.int32)
+    return np.stack([keys, np.arange(keys.size, dtype=np.int32)], 1)
+
+
+def torchrun(world, args, env_extra, timeout=300):
+    """bench.py under torch.distributed.run in its own process group, killed as a group on timeout
+    (no rank outlives the test). Returns (returncode, stdout, stderr); returncode None = timeout."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, **env_extra)
+    for k in ("HWBRJ_BENCH_SHARED_GPU", "HWBRJ_BENCH_DIST", "HWBRJ_PJ_FORCE_COLL", "HWBRJ_DEV_PJ_FAIL_RANK"):
+        if k not in env_extra:
+            env.pop(k, None)
+    p = subprocess.Popen(["python", "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
+                          "--master-addr", "127.0.0.1", "--master-port", str(port),
+                          os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--steps", "2", "--warmup", "1",
+                          "--no-cpu-baseline", "--no-e2e"] + [str(x) for x in args],
+                         stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env, cwd=ROOT,
+                         start_new_session=True)
+    try:
+        out, err = p.communicate(timeout=timeout)
+        return p.returncode, out, err
+    except subprocess.TimeoutExpired:
+        os.killpg(p.pid, signal.SIGKILL)
+        out, err = p.communicate()
+        return None, out, err
+
+
+def last_json(out):
+    return json.loads([x for x in out.splitlines() if x.startswith("{")][-1])
+
+
+# ------------------------------------------------------------ the native transport at world 1
+@pytest.fixture
+def rccl1(hw):
+    from hwbloomradixjoin_amd import pjoin
+    assert pjoin.comm_init() == (1, 0)  # no process group: a world-1 communicator
+    yield pjoin
+    pjoin.set_filter_broadcast(False)
+    pjoin.comm_destroy()
+
+
+PJ_ARGS = [None, ("blocked", 1 << 24, 1, 1024), ("blocked", 1 << 22, 3, 512), ("basic", 1 << 20, 1, 0),
+           ("sectorized", 1 << 22, 4, 512), ("blocked", 1 << 31, 2, 512)]
+
+
+@pytest.mark.parametrize("a", PJ_ARGS, ids=str)
+def test_partitioned_rccl_world1_vs_oracle(hw, cuda, orc, rccl1, a):
+    """hwbrj_join_partitioned_rccl: the R-chunk and survivor all-to-alls as grouped
+    ncclSend/ncclRecv and the slice all-gather as ncclAllGather on the join stream (no host drain
+    before them); counts equal the oracle's, empty and odd-sized shards included."""
+    args = None if a is None else hw.BloomFilterArgs.from_flag(a[0], a[1], a[2], a[3] or 1024)
+    rng = np.random.default_rng(41)
+    for nR, nS in [(0, 1000), (1000, 0), (7, 33), (100003, 400009), (1000000, 4000000)]:
+        Rk = rng.permutation(nR).astype(np.int64) + 1
+        Sk = rng.integers(0, 2 * max(nR, 1) + 2, size=nS)
+        R, S = rel(Rk), rel(Sk)
+        st = rccl1.join_partitioned_rccl(to_dev(cuda, R), to_dev(cuda, S), nR, args)
+        if args is None:
+            res, filt, _ = orc.bpro(R, S, 8, 0, 0, 0, 0, use_bloom=False)
+        else:
+            res, filt, _ = orc.bpro(R, S, 8, args.variant, args.m, args.k, args.B)
+        assert (st.filtered, st.matches) == (filt, res), (a, nR, nS, st)
+
+
+def test_partitioned_rccl_northstar(hw, cuda, rccl1):
+    """The north-star golden through the native partitioned join."""
+    g = GOLD["F4_northstar"]
+    R = cuda.empty((g["r"], 2), dtype=cuda.int32, device="cuda")
+    S = cuda.empty((g["s"], 2), dtype=cuda.int32, device="cuda")
+    hw.generate_device(R, 2, g["r"], g["r"], 1.0, 12345)
+    hw.generate_device(S, 2, INT_MAX, g["r"], g["q"], 54321)
+    st = rccl1.join_partitioned_rccl(R, S, g["r"], hw.BloomFilterArgs(hw.BLOCKED, g["m"], 1, g["B"]))
+    del R, S
+    assert (st.filtered, st.matches) == (g["k1_filtered"], g["results"])
+
+
+@pytest.mark.parametrize("a", [("blocked", 1 << 24, 1, 1024), ("blocked", 1 << 24, 4, 512),
+                               ("sectorized", 1 << 24, 2, 1024), ("basic", 1 << 24, 1, 1024),
+                               ("blocked", 1 << 31, 2, 512)], ids=str)
+def test_filter_broadcast_world1(hw, cuda, orc, rccl1, a):
+    """hwbrj_set_filter_broadcast: the replicated join with the slices built on rank 0 and sent by
+    ncclBroadcast on the join stream (the north_star's bitmap broadcast). Counts equal the F3
+    goldens / the oracle, and the exported filter is the reference layout's, bit for bit, as
+    without the broadcast."""
+    g = GOLD["F3_grid"]
+    R = hw.generate_host(g["r"], 2, g["r"], g["r"], 1.0, 1)
+    S = hw.generate_host(g["s"], 2, INT_MAX, g["r"], g["q"], 2)
+    args = hw.BloomFilterArgs.from_flag(*a)
+    dR, dS = to_dev(cuda, R), to_dev(cuda, S)
+    plain = hw.join_device(dR, dS, args)
+    want = hw.export_filter(a[1]).copy()
+    rccl1.set_filter_broadcast(True)
+    st = hw.join_device(dR, dS, args)
+    assert (st.filtered, st.matches) == (plain.filtered, plain.matches)
+    assert np.array_equal(hw.export_filter(a[1]), want)
+    res, filt, _ = orc.bpro(R, S, 8, args.variant, args.m, args.k, args.B)
+    assert (st.filtered, st.matches) == (filt, res)
+
+
+# ------------------------------------------------- bench.py over the RCCL process group, world 1
+@pytest.mark.parametrize("case", ["partitioned-native", "partitioned-torch-nccl", "replicated-bcast"])
+def test_bench_rccl_world1(hw, case):
+    """bench.py's multi-GPU designs under torch.distributed.run with the RCCL ("nccl") group at
+    world 1 (HWBRJ_BENCH_DIST=1): the native partitioned transport, the torch callback transport
+    with its collectives forced (HWBRJ_PJ_FORCE_COLL=1: all_to_all_single / all_gather_into_tensor
+    on device uint8 over RCCL), and the replicated design with the filter broadcast."""
+    g = GOLD["F3_grid"]
+    base = ["-r", g["r"], "-s", g["s"], "-m", g["m"]]
+    env = {"HWBRJ_BENCH_DIST": "1"}
+    if case == "partitioned-native":
+        args = base + ["--design", "partitioned", "--transport", "native"]
+    elif case == "partitioned-torch-nccl":
+        args = base + ["--design", "partitioned", "--transport", "torch"]
+        env["HWBRJ_PJ_FORCE_COLL"] = "1"
+    else:
+        args = base + ["--filter-bcast"]
+    rc, out, err = torchrun(1, args, env)
+    assert rc == 0, out[-2000:] + err[-3000:]
+    line = last_json(out)
+    assert (line["parity"]["filtered"], line["parity"]["matches"]) == (g["rows"]["1024"][0], g["results"])
+    assert line["dist"]["backend"] == "nccl" and line["dist"]["world_size_seen"] == 1
+    assert line["scaling"] == "strong"
+
+
+# ------------------------------------------------- status agreement (no hang on one rank's error)
+@pytest.mark.parametrize("fail_rank", [0, 1])
+def test_partitioned_rank_failure_does_not_hang(hw, fail_rank):
+    """One rank of two fails the capacity check alone (HWBRJ_DEV_PJ_FAIL_RANK, as an oversized
+    shard would): the ranks agree on their statuses before the first collective, so both return an
+    error promptly (torch.distributed.run exits nonzero) instead of the other rank waiting in the
+    R all-to-all forever."""
+    g = GOLD["F3_grid"]
+    rc, out, err = torchrun(2, ["--design", "partitioned", "-r", g["r"], "-s", g["s"], "-m", g["m"]],
+                            {"HWBRJ_BENCH_SHARED_GPU": "1", "HWBRJ_DEV_PJ_FAIL_RANK": str(fail_rank)},
+                            timeout=240)
+    assert rc is not None, "ranks hung: " + err[-3000:]
+    assert rc != 0
+    assert "shard too large" in err
+    assert f"rank {fail_rank} failed" in err

@@ -92,6 +92,27 @@ def test_print_timing_contract(hw, capfd):
     assert "S-tuples after filter" not in out and "TOTAL-TIME-USECS" in out
 
 
+def test_timing_cycles_cover_the_device_join(hw, capfd):
+    """RUNTIME TOTAL (cycles) and TOTAL-TIME-USECS time the same region, as in the reference
+    (src/parallel_radix_join_bloom.c:1107-1131, :1477-1484): the H2D copies and allocations are
+    staged before the cycle counter starts, so cycles / TSC rate is the device join plus the launch
+    and completion latency (5 % + 0.25 ms), not the ~PCIe copy of S."""
+    nR, nS = 32000000, 256000000
+    R = hw.Relation(hw.generate_host(nR, 2, nR, nR, 1.0, 1))
+    S = hw.Relation(hw.generate_host(nS, 2, INT_MAX, nR, 0.01, 2))
+    a = hw.BloomFilterArgs(hw.BLOCKED, 1 << 28, 1, 1024)
+    hz = hw.lib().hwbrj_tsc_hz()
+    assert hz > 1e8
+    for _ in range(2):  # (the first call also loads the kernels)
+        capfd.readouterr()
+        hw.BPRO(R, S, 2, a)
+        lines = capfd.readouterr().out.splitlines()
+    tot = float(lines[lines.index("TOTAL-TIME-USECS, TOTAL-TUPLES, NSEC-PER-TUPLE: ") + 1].split()[0])
+    cyc = int(lines[lines.index("RUNTIME TOTAL, BUILD, PART (cycles): ") + 1].split()[0])
+    host_us = cyc / hz * 1e6
+    assert tot > 300 and abs(host_us - tot) <= 0.05 * tot + 250, (host_us, tot)
+
+
 def test_joins_on_two_streams_are_ordered(hw, cuda):
     """A join enqueued on one stream and the next on another share the device's scratch: the second
     waits for the first (hwbrj_engine.cpp enqueue). Both end with the golden counts."""
@@ -165,6 +186,46 @@ def test_full_size_rows_vs_oracle(hw, cuda, full_R, row):
     st = hw.join_device(full_R, S, hw.BloomFilterArgs.from_flag(row["variant"], row["m"], row["k"], row["B"]))
     del S
     assert (st.filtered, st.matches) == (row["filtered"], row["results"])
+
+
+# BASELINE config 5: Zipf theta = 0.75 S x q. The matching rows draw keys from the alphabet
+# 1..|R| (src/genzipf.c:98-158); this build's q < 1 extension gives floor(|S| (1 - q)) rows the
+# unique keys |R| + 1 .. |R| + floor(|S| (1 - q)), the same non-matching keys as the uniform
+# generator at that q (src/generator.c:341-351). Every alphabet key passes the filter (no false
+# negatives), so `filtered` is the oracle-pinned uniform count at the same q (q = 1: the reference's
+# own -z relation, filtered = Results = |S|).
+ZIPF_Q = [(0.001, 116057774), (0.01, 124236515), (0.1, 206036818), (1.0, 1024000000)]
+
+
+@pytest.mark.parametrize("q,filtered", ZIPF_Q, ids=lambda v: str(v))
+def test_zipf_q_rows_full_size(hw, cuda, full_R, q, filtered):
+    nS = 1024000000
+    S = cuda.empty((nS, 2), dtype=cuda.int32, device="cuda")
+    hw.create_relation_zipf_device(S, 128000000, 0.75, 54321, q, 16)
+    st = hw.join_device(full_R, S, hw.BloomFilterArgs(hw.BLOCKED, 1 << 30, 1, 1024))
+    del S
+    assert st.matches == nS - int(nS * (1 - q))
+    assert st.filtered == filtered
+
+
+@pytest.mark.parametrize("q", [0.001, 0.01, 0.1, 1.0])
+def test_zipf_q_small_vs_oracle(hw, cuda, orc, q):
+    """The Zipf + q relation at |R| = 1M, |S| = 16M, generated on the GPU: its non-matching keys
+    are exactly |R| + 1 .. |R| + floor(|S| (1 - q)), and the join of the same tuples equals the
+    oracle's (blocked k = 1 and 3, basic k = 2)."""
+    nR, nS = 1000000, 16000000
+    R = hw.generate_host(nR, 2, nR, nR, 1.0, 12345)
+    dS = cuda.empty((nS, 2), dtype=cuda.int32, device="cuda")
+    hw.create_relation_zipf_device(dS, nR, 0.75, 54321, q, 8)
+    S = dS.cpu().numpy()
+    n_above = int(nS * (1 - q))
+    above = np.sort(S[S[:, 0] > nR, 0])
+    assert np.array_equal(above, np.arange(nR + 1, nR + 1 + n_above))
+    assert S[:, 0].min() >= 1 and np.array_equal(np.sort(S[:, 1]), np.arange(nS))
+    for a in [(hw.BLOCKED, 1 << 24, 1, 1024), (hw.BLOCKED, 1 << 24, 3, 512), (hw.BASIC, 1 << 24, 2, 1024)]:
+        st = hw.join_device(to_dev(cuda, R), dS, hw.BloomFilterArgs(*a))
+        res, filt, _ = orc.bpro(R, S, 8, *a)
+        assert (st.filtered, st.matches) == (filt, res) and res == nS - n_above, (a, st)
 
 
 def oracle_check(hw, cuda, orc, R, S, args):
@@ -334,7 +395,7 @@ def test_histogram_joins_northstar(hw, full_R, cuda, algo):
 
 
 def test_weak_scaling_ranks_reach_the_golden(hw, cuda):
-    """bench.py's default N > 1 run (weak scaling): rank r joins the whole |S| generated with seed
+    """bench.py --scaling weak (an A/B option): rank r joins the whole |S| generated with seed
     54321 + r. The seed orders the tuples only (the key multiset is the reference generator's), so
     every rank's counts are the north-star golden."""
     import torch

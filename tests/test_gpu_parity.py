@@ -376,8 +376,10 @@ def test_bench_two_ranks(hw):
                          capture_output=True, text=True, timeout=300, env=env, cwd=root)
     assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-2000:]
     line = json.loads([x for x in out.stdout.splitlines() if x.startswith("{")][-1])
-    assert line["n_gpus"] == 2
+    assert line["n_gpus"] == 2 and line["scaling"] == "strong" and line["dist"]["world_size_seen"] == 2
     assert (line["parity"]["filtered"], line["parity"]["matches"]) == (g["rows"]["1024"][0], g["results"])
+    per = line["parity"]["per_rank"]  # two S shards: their counts sum to the golden
+    assert len(per) == 2 and [sum(c) for c in zip(*per)] == [g["rows"]["1024"][0], g["results"]]
 
 
 def test_bench_rccl_process_group(hw):
@@ -400,6 +402,8 @@ def test_bench_rccl_process_group(hw):
     assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-2000:]
     line = json.loads([x for x in out.stdout.splitlines() if x.startswith("{")][-1])
     assert (line["parity"]["filtered"], line["parity"]["matches"]) == (g["rows"]["1024"][0], g["results"])
+    assert line["scaling"] == "strong" and line["dist"] == {"world_size_seen": 1, "backend": "nccl",
+                                                            "shared_gpu_rehearsal": False}
 
 
 def _sorted_pairs(p):

@@ -85,8 +85,8 @@ def main():
     json.dump(res, open(out, "w"), indent=1)
     for lab, p in res["phases"].items():
         gbs = p["hbm_bytes"] / (p["ms"] * 1e-3) / 1e9 if p["ms"] else 0
-        print(f"{lab:10s} {p['ms']:8.4f} ms  fetch {p['fetch_kib']/1e6:7.3f} GiB*  write "
-              f"{p['write_kib']/1e6:7.3f} GiB  -> {p['hbm_bytes']/1e9:7.3f} GB  {gbs:8.1f} GB/s")
+        print(f"{lab:10s} {p['ms']:8.4f} ms  fetch(raw, x2 in total) {p['fetch_kib']*1024/1e9:7.3f} GB  write "
+              f"{p['write_kib']*1024/1e9:7.3f} GB  -> {p['hbm_bytes']/1e9:7.3f} GB  {gbs:8.1f} GB/s")
 
 
 if __name__ == "__main__":
