@@ -435,7 +435,8 @@ def host_cpu() -> dict:
 
 
 # Calibration (BASELINE.md "Calibration of the CPU port"): on the same 8-core host the reference
-# binary needs 6.0 s where this port needs 13.5 s (C2, -n 8), i.e. the port runs at 0.45x it.
+# binary needs 6.0 s where this port needs 13.0-13.6 s (C2, -n 8, re-measured in round 3), i.e. the
+# port runs at 0.45x it.
 PORT_VS_REFERENCE = 6.0 / 13.5
 
 
@@ -463,6 +464,8 @@ def cpu_baseline(a, hw):
         v, secs, filt, res = runs[threads]
         return {"value": round(v, 1), "unit": "probe-tuples/s", "cores": threads, "kind": "port",
                 "host": info, "value_n8": round(runs[8][0], 1),
+                "cores_cap": (f"OMP_NUM_THREADS={cap}: the GPU pool's CPU share for one GPU's job "
+                              "(BASELINE.md, round-3 re-measurement)"),
                 "calibration_port_vs_reference": round(PORT_VS_REFERENCE, 3),
                 "reference_estimate": round(v / PORT_VS_REFERENCE, 1),
                 "sample": (f"|R|={a.r_size}, |S|={sample} tuples of the same generator "

@@ -106,10 +106,21 @@ void* nx_buffer(void* ctx, int slot, uint64_t bytes) {
     return b->ensure(bytes) ? b->p : nullptr;
 }
 
+// The block a rank sends to itself is a copy on the join stream: RCCL's send/recv to self runs
+// through its point-to-point protocol at a small fraction of HBM rate (measured at world 1: the
+// R and survivor blocks, 0.1-0.5 GB, cost ~1 ms more than a device copy). HWBRJ_RCCL_SELF=1
+// (tests) sends it through RCCL like the others, so a one-GPU run exercises ncclSend / ncclRecv.
+bool rccl_self() { return getenv("HWBRJ_RCCL_SELF") != nullptr; }
+
 int nx_alltoall_u64(void* ctx, const uint64_t* send, uint64_t* recv, uint64_t n) {
     Engine*        e  = (Engine*) ctx;
     const Rccl&    R  = rccl();
     const int      W  = e->comm_world();
+    const int      me = e->comm_rank();
+    if (!rccl_self()) {
+        memcpy(recv + (uint64_t) me * n, send + (uint64_t) me * n, n * 8);
+        if (W == 1) return 0;
+    }
     hipStream_t    st = e->stream();
     ncclComm_t     c  = (ncclComm_t) e->comm();
     const uint64_t nb = (uint64_t) W * n * 8;
@@ -122,12 +133,17 @@ int nx_alltoall_u64(void* ctx, const uint64_t* send, uint64_t* recv, uint64_t n)
     if (hipMemcpyAsync(ds, send, nb, hipMemcpyHostToDevice, st) != hipSuccess) return 1;
     RC_CALL(R.GroupStart(), "ncclGroupStart");
     for (int j = 0; j < W; j++) {
+        if (j == me && !rccl_self()) continue;
         RC_CALL(R.Send(ds + (uint64_t) j * n, n, ncclUint64, j, c, st), "ncclSend (counts)");
         RC_CALL(R.Recv(dr + (uint64_t) j * n, n, ncclUint64, j, c, st), "ncclRecv (counts)");
     }
     RC_CALL(R.GroupEnd(), "ncclGroupEnd");
+    std::vector<uint64_t> own(n);
+    memcpy(own.data(), recv + (uint64_t) me * n, n * 8);
     if (hipMemcpyAsync(recv, dr, nb, hipMemcpyDeviceToHost, st) != hipSuccess) return 1;
-    return hipStreamSynchronize(st) == hipSuccess ? 0 : 1;
+    if (hipStreamSynchronize(st) != hipSuccess) return 1;
+    if (!rccl_self()) memcpy(recv + (uint64_t) me * n, own.data(), n * 8);
+    return 0;
 }
 
 int nx_alltoallv(void* ctx, int sslot, const uint64_t* soff, const uint64_t* sbytes, int rslot,
@@ -138,9 +154,18 @@ int nx_alltoallv(void* ctx, int sslot, const uint64_t* soff, const uint64_t* sby
     ncclComm_t    c  = (ncclComm_t) e->comm();
     const uint8_t* s = (const uint8_t*) e->xslot(sslot)->p;
     uint8_t*      d  = (uint8_t*) e->xslot(rslot)->p;
+    const int     me = e->comm_rank();
+    if (!rccl_self() && sbytes[me]) {  // (rbytes[me] == sbytes[me]: the counts this rank sent itself)
+        if (hipMemcpyAsync(d + roff[me], s + soff[me], sbytes[me], hipMemcpyDeviceToDevice, e->stream()) != hipSuccess) {
+            set_last_error("device copy of the rank's own block failed");
+            return 1;
+        }
+    }
+    if (W == 1 && !rccl_self()) return 0;
     // a block of 0 bytes is neither sent nor received (its peer sees the same 0 in its counts)
     RC_CALL(R.GroupStart(), "ncclGroupStart");
     for (int j = 0; j < W; j++) {
+        if (j == me && !rccl_self()) continue;
         if (sbytes[j]) RC_CALL(R.Send(s + soff[j], sbytes[j], ncclUint8, j, c, e->stream()), "ncclSend");
         if (rbytes[j]) RC_CALL(R.Recv(d + roff[j], rbytes[j], ncclUint8, j, c, e->stream()), "ncclRecv");
     }

@@ -260,7 +260,7 @@ void Engine::release() {
                       &istartS, &listS, &slices, &bitmap, &rjoin, &rrun, &surv, &survcnt, &survoff,
                       &dense, &small, &bpos, &colR, &colS, &mtab, &mcount, &jtask, &jparts, &pjList,
                       &pjLstart, &pjSweep, &pjTab, &pjRegion, &pjTot, &pjSoff, &pjIbase, &pjCnt, &pjOff,
-                      &pjIstart, &pjJobs, &ppoolR, &ppoolS, &rpay, &survpos, &dense2, &kkcnt, &xcnt_})
+                      &pjIstart, &pjJobs, &ppoolR, &ppoolS, &rpay, &survpos, &dense2, &kkcnt, &xcnt_, &pjBsum, &pjBound, &pjWtot, &pjWscan, &pjTab2})
         b->release();
     for (DevBuf& b : xslot_) b.release();
     have_filter_ = false;

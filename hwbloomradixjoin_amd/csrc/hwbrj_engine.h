@@ -130,6 +130,7 @@ class Engine {
     DevBuf jtask, jparts;  // join task table; parts per job (+ the task count)
     // partitioned join: owned partitions' lists, tables and received survivor descriptors
     DevBuf pjList, pjLstart, pjSweep, pjTab, pjRegion, pjTot, pjSoff, pjIbase, pjCnt, pjOff, pjIstart, pjJobs;
+    DevBuf pjBsum, pjBound, pjWtot, pjWscan, pjTab2;  // device-side item tables (scans, bounds)
 };
 
 Engine* engine_for_current_device();

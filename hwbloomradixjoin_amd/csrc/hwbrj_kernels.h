@@ -177,6 +177,19 @@ void   launch_mat_probe(const uint2* S, uint64_t n, const uint2* R, const unsign
                         const CrcTables* tabs, hipStream_t st);
 // partitioned multi-GPU join (K13): chunks in list order + rebased entries; receiver lists;
 // survivor runs of items packed per destination
+// partitioned join, device-side item tables: probe items -> region, survivor totals, their
+// exclusive scan sofs [I + 1] and sofs at every partition's first item (bound [F + 1]); received
+// items -> exclusive scan of their totals (wscan [n + 1]); the owner's join tables per
+// (owned partition, source) pair (tab: first received item, items, first output item)
+void   launch_pj_items(const uint32_t* item_start, const uint32_t* list_start, const uint32_t* cnt,
+                       uint32_t items_max, uint32_t F, uint32_t nseg, uint32_t CH, uint64_t seg_words, uint32_t NSUB,
+                       uint64_t* region, uint32_t* tot, uint64_t* bsum, uint64_t* sofs, uint64_t* bound,
+                       hipStream_t st);
+void   launch_pj_recv_scan(const uint32_t* cnt, uint32_t n, uint32_t NSUB, uint32_t* tot, uint64_t* bsum,
+                           uint64_t* wscan, hipStream_t st);
+void   launch_pj_item_tables(const uint32_t* tab, uint32_t pairs, uint32_t W, const uint32_t* rcnt,
+                             const uint64_t* wscan, uint32_t NSUB, uint64_t* ibase, uint32_t* icnt, uint32_t* ioff,
+                             uint32_t* jobs, hipStream_t st);
 void   launch_pj_gather(const uint32_t* pool, const uint32_t* list, uint32_t n, void* out, uint32_t* ent,
                         hipStream_t st);
 void   launch_pj_relist(const uint32_t* rent, const int64_t* tab, uint32_t pairs, uint32_t* list,

@@ -3327,6 +3327,157 @@ __global__ __launch_bounds__(256) void k_pj_surv_pack(const uint32_t* __restrict
     }
 }
 
+// ---- device-side item tables (no host round trip for per-item counts)
+constexpr uint32_t kPjScanBlock = 1024;  // items per scan block
+
+// Block-wide exclusive scan of one u32 per thread (1024 threads): returns this thread's exclusive
+// prefix and the block total.
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wsum, uint32_t& total) {
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t incl = wave_incl_scan(v);
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    uint32_t base = 0;
+    total         = 0;
+    for (uint32_t w = 0; w < 16; w++) {
+        const uint32_t x = wsum[w];
+        if (w < wave) base += x;
+        total += x;
+    }
+    __syncthreads();
+    return base + incl - v;
+}
+
+// Probe items of this rank (it < I): the survivor region of the item (seg * LS * 32 + first list
+// position * 32, as k_probe wrote it), its survivor total over the NSUB sub runs, and the total of
+// each block of kPjScanBlock items.
+// (I = item_start[F], read on the device: the grid covers the items' upper bound, so no host round
+// trip is needed before the launch)
+__global__ __launch_bounds__(1024) void k_pj_items(const uint32_t* __restrict__ item_start,
+                                                   const uint32_t* __restrict__ list_start,
+                                                   const uint32_t* __restrict__ cnt, uint32_t F,
+                                                   uint32_t nseg, uint32_t CH, uint64_t seg_words,
+                                                   uint32_t NSUB, uint64_t* __restrict__ region,
+                                                   uint32_t* __restrict__ tot, uint64_t* __restrict__ bsum) {
+    __shared__ uint32_t wsum[16];
+    const uint32_t I  = item_start[F];
+    const uint32_t it = blockIdx.x * kPjScanBlock + threadIdx.x;
+    uint32_t       t  = 0;
+    if (it < I) {
+        const uint32_t q     = find_q(item_start, F, it);
+        const uint32_t i0    = item_start[q];
+        const uint32_t npc   = (item_start[q + 1] - i0) / nseg;
+        const uint32_t local = it - i0, seg = local / npc, piece = local - seg * npc;
+        region[it] = (uint64_t) seg * seg_words + (uint64_t) (list_start[q] + piece * CH) * 32;
+        for (uint32_t s = 0; s < NSUB; s++) t += cnt[(uint64_t) it * NSUB + s];
+        tot[it] = t;
+    }
+    uint32_t total;
+    (void) block_excl_scan(t, wsum, total);
+    if (threadIdx.x == 0) bsum[blockIdx.x] = total;
+}
+
+// Received items (it < n, in received order): survivor total over the NSUB counts, block totals.
+__global__ __launch_bounds__(1024) void k_pj_recv_tot(const uint32_t* __restrict__ cnt, uint32_t n,
+                                                      uint32_t NSUB, uint32_t* __restrict__ tot,
+                                                      uint64_t* __restrict__ bsum) {
+    __shared__ uint32_t wsum[16];
+    const uint32_t it = blockIdx.x * kPjScanBlock + threadIdx.x;
+    uint32_t       t  = 0;
+    if (it < n) {
+        for (uint32_t s = 0; s < NSUB; s++) t += cnt[(uint64_t) it * NSUB + s];
+        tot[it] = t;
+    }
+    uint32_t total;
+    (void) block_excl_scan(t, wsum, total);
+    if (threadIdx.x == 0) bsum[blockIdx.x] = total;
+}
+
+// out[it] = exclusive prefix of tot over [0, it) for it <= n (block b adds the totals of blocks < b;
+// the grid has n / kPjScanBlock + 1 blocks).
+__global__ __launch_bounds__(1024) void k_pj_scan(const uint32_t* __restrict__ tot, uint32_t n_host,
+                                                  const uint32_t* __restrict__ n_dev,
+                                                  const uint64_t* __restrict__ bsum,
+                                                  uint64_t* __restrict__ out) {
+    __shared__ uint32_t wsum[16];
+    __shared__ uint64_t red[16];
+    const uint32_t n = n_dev ? *n_dev : n_host;  // (n_dev: blocks past n / kPjScanBlock idle)
+    if (blockIdx.x > n / kPjScanBlock) return;
+    uint64_t p = 0;
+    for (uint32_t b = threadIdx.x; b < blockIdx.x; b += 1024) p += bsum[b];
+    p = wave_sum_u64(p);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = p;
+    __syncthreads();
+    uint64_t base = 0;
+    for (int w = 0; w < 16; w++) base += red[w];
+    const uint32_t it = blockIdx.x * kPjScanBlock + threadIdx.x;
+    uint32_t       total;
+    const uint32_t ex = block_excl_scan(it < n ? tot[it] : 0u, wsum, total);
+    if (it <= n) out[it] = base + ex;  // (the grid covers it = n: out[n] is the grand total)
+}
+
+// sofs at the first item of every partition (q <= F): the host's per-destination word counts.
+__global__ void k_pj_bound(const uint32_t* __restrict__ item_start, uint32_t F,
+                           const uint64_t* __restrict__ sofs, uint64_t* __restrict__ out) {
+    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q <= F) out[q] = sofs[item_start[q]];
+}
+
+// The owner's join tables from the received per-item counts. One block per (owned partition i,
+// source j) pair: tab[3 pair + {0, 1, 2}] = first received item, items, first output item. Output
+// item out of received item src: ibase = its first word in the received survivors (wscan[src]),
+// icnt / ioff its NSUB run counts and offsets; jobs[i][s] += the counts (every output order: items
+// of partition i from source 0, 1, ...).
+__global__ __launch_bounds__(256) void k_pj_item_tables(const uint32_t* __restrict__ tab, uint32_t W,
+                                                        const uint32_t* __restrict__ rcnt,
+                                                        const uint64_t* __restrict__ wscan, uint32_t NSUB,
+                                                        uint64_t* __restrict__ ibase, uint32_t* __restrict__ icnt,
+                                                        uint32_t* __restrict__ ioff, uint32_t* __restrict__ jobs) {
+    __shared__ uint32_t js[64];
+    const uint32_t* t  = tab + 3 * (uint64_t) blockIdx.x;
+    const uint32_t  i  = blockIdx.x / W;
+    const uint32_t  s0 = t[0], n = t[1], o0 = t[2];
+    if (threadIdx.x < 64) js[threadIdx.x] = 0;
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < n; k += blockDim.x) {
+        const uint32_t src = s0 + k, out = o0 + k;
+        ibase[out] = wscan[src];
+        uint32_t o = 0;
+        for (uint32_t s = 0; s < NSUB; s++) {
+            const uint32_t c = rcnt[(uint64_t) src * NSUB + s];
+            icnt[(uint64_t) out * NSUB + s] = c;
+            ioff[(uint64_t) out * NSUB + s] = o;
+            o += c;
+            if (c) atomicAdd(&js[s], c);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < NSUB && js[threadIdx.x]) atomicAdd(&jobs[(uint64_t) i * NSUB + threadIdx.x], js[threadIdx.x]);
+}
+
+void launch_pj_items(const uint32_t* item_start, const uint32_t* list_start, const uint32_t* cnt,
+                     uint32_t items_max, uint32_t F, uint32_t nseg, uint32_t CH, uint64_t seg_words, uint32_t NSUB,
+                     uint64_t* region, uint32_t* tot, uint64_t* bsum, uint64_t* sofs, uint64_t* bound,
+                     hipStream_t st) {
+    const uint32_t nb = (items_max + kPjScanBlock) / kPjScanBlock;  // (covers it == I for sofs[I])
+    k_pj_items<<<nb, 1024, 0, st>>>(item_start, list_start, cnt, F, nseg, CH, seg_words, NSUB, region, tot, bsum);
+    k_pj_scan<<<nb, 1024, 0, st>>>(tot, 0, item_start + F, bsum, sofs);
+    k_pj_bound<<<(F + 256) / 256, 256, 0, st>>>(item_start, F, sofs, bound);
+}
+
+void launch_pj_recv_scan(const uint32_t* cnt, uint32_t n, uint32_t NSUB, uint32_t* tot, uint64_t* bsum,
+                         uint64_t* wscan, hipStream_t st) {
+    const uint32_t nb = (n + kPjScanBlock) / kPjScanBlock;
+    k_pj_recv_tot<<<nb, 1024, 0, st>>>(cnt, n, NSUB, tot, bsum);
+    k_pj_scan<<<nb, 1024, 0, st>>>(tot, n, nullptr, bsum, wscan);
+}
+
+void launch_pj_item_tables(const uint32_t* tab, uint32_t pairs, uint32_t W, const uint32_t* rcnt,
+                           const uint64_t* wscan, uint32_t NSUB, uint64_t* ibase, uint32_t* icnt, uint32_t* ioff,
+                           uint32_t* jobs, hipStream_t st) {
+    if (pairs) k_pj_item_tables<<<pairs, 256, 0, st>>>(tab, W, rcnt, wscan, NSUB, ibase, icnt, ioff, jobs);
+}
+
 void launch_pj_gather(const uint32_t* pool, const uint32_t* list, uint32_t n, void* out, uint32_t* ent,
                       hipStream_t st) {
     if (n) k_pj_gather<<<4096, 256, 0, st>>>(pool, list, n, (uint4*) out, ent);

@@ -158,7 +158,7 @@ int Engine::join_partitioned(const hwbrj_exchange_t* x, int rank, int world, con
              *recvM = nullptr;
     uint64_t* d_result   = nullptr;
     uint64_t* d_filtered = nullptr;
-    std::vector<uint32_t> ls(F + 1, 0), lsS(F + 1, 0), isS(F + 1, 0);
+    std::vector<uint32_t> ls(F + 1, 0), isS(F + 1, 0);
     std::vector<uint64_t> scnt((size_t) W * NC, 0), rcnt((size_t) W * NC, 0);
     std::vector<uint64_t> soff(W), sbytes(W), roff(W), rbytes(W);
     uint64_t              RC = 0, sweeps = 0, RI = 0, RW = 0;
@@ -353,7 +353,6 @@ int Engine::join_partitioned(const hwbrj_exchange_t* x, int rank, int world, con
         PJ_XCHG(x->allgather(x->ctx, HWBRJ_PJ_SLICES, (uint64_t) QL * nseg * g.seg_words * 4), "filter slices");
     lap(3);
     // ------------------------------------------------------------- 5. S shard: partition, probe
-    std::vector<uint32_t> scntS;
     uint32_t I = 0;
     const int rc5 = [&]() -> int {
         sp.src        = dS;
@@ -388,41 +387,46 @@ int Engine::join_partitioned(const hwbrj_exchange_t* x, int rank, int world, con
         const uint32_t PG     = (uint32_t) cus_ * (uint32_t) std::max<size_t>(1, std::min<size_t>(2, 163840 / pl_lds));
         launch_probe(pp, PG, stream);
         PJ_STAGE("S scatter + probe");
-        PJ_CHECK(hipMemcpyAsync(lsS.data(), lstartS.p, (F + 1) * 4, hipMemcpyDeviceToHost, stream));
+        // ------------------------------------------------------------- 6. survivor exchange
+        // item tables on the device (k_pj_items: regions, survivor totals, their scan); the host
+        // reads only the item starts and the scan at every partition's first item
+        const uint32_t items_max = (uint32_t) ((LS / CH + F + 1) * nseg);
+        const uint32_t nbk       = items_max / 1024 + 1;
+        if (!pjRegion.ensure((uint64_t) items_max * 8 + 8) || !pjTot.ensure((uint64_t) items_max * 4 + 4) ||
+            !pjSoff.ensure((uint64_t) items_max * 8 + 8) || !pjBsum.ensure((uint64_t) nbk * 8) ||
+            !pjBound.ensure((uint64_t) (F + 1) * 8)) {
+            set_last_error("hipMalloc failed (device memory)");
+            return 4;
+        }
+        launch_pj_items(istartS.as<uint32_t>(), lstartS.as<uint32_t>(), survcnt.as<uint32_t>(), items_max, F, nseg,
+                        CH, LS * 32, NSUB, pjRegion.as<uint64_t>(), pjTot.as<uint32_t>(), pjBsum.as<uint64_t>(),
+                        pjSoff.as<uint64_t>(), pjBound.as<uint64_t>(), stream);
+        std::vector<uint64_t> bnd(F + 1);
         PJ_CHECK(hipMemcpyAsync(isS.data(), istartS.p, (F + 1) * 4, hipMemcpyDeviceToHost, stream));
+        PJ_CHECK(hipMemcpyAsync(bnd.data(), pjBound.p, (F + 1) * 8, hipMemcpyDeviceToHost, stream));
         PJ_CHECK(hipStreamSynchronize(stream));
         I = isS[F];
-        scntS.resize((size_t) I * NSUB);
-        if (I) PJ_CHECK(hipMemcpy(scntS.data(), survcnt.p, (size_t) I * NSUB * 4, hipMemcpyDeviceToHost));
         lap(4);
-        // ------------------------------------------------------------- 6. survivor exchange
-        std::vector<uint64_t> region(I);
-        std::vector<uint32_t> tot(I);
-        sofs.assign(I + 1, 0);
-        for (uint32_t q = 0; q < F; q++) {
-            const uint32_t npc = (isS[q + 1] - isS[q]) / nseg;
-            for (uint32_t it = isS[q]; it < isS[q + 1]; it++) {
-                const uint32_t local = it - isS[q], seg = local / npc, piece = local - seg * npc;
-                region[it] = (uint64_t) seg * (LS * 32) + (uint64_t) (lsS[q] + piece * CH) * 32;
-                uint32_t t = 0;
-                for (uint32_t s = 0; s < NSUB; s++) t += scntS[(size_t) it * NSUB + s];
-                tot[it]      = t;
-                sofs[it + 1] = sofs[it] + t;
-            }
-        }
-        sendS = (uint32_t*) x->buffer(x->ctx, HWBRJ_PJ_S_SEND, std::max<uint64_t>(16, sofs[I] * 4));
+        sofs = bnd;  // (sofs at partition starts: all the host needs)
+        sendS = (uint32_t*) x->buffer(x->ctx, HWBRJ_PJ_S_SEND, std::max<uint64_t>(16, bnd[F] * 4));
         sendM = (uint32_t*) x->buffer(x->ctx, HWBRJ_PJ_M_SEND, std::max<uint64_t>(16, (uint64_t) I * NSUB * 4));
         if (!sendS || !sendM) {
             set_last_error("exchange buffer (survivor send) unavailable");
             return 20;
         }
-        if (to_dev(pjRegion, region, stream) || to_dev(pjTot, tot, stream) || to_dev(pjSoff, sofs, stream)) {
-            set_last_error("host tables to the device failed");
-            return 4;
-        }
-        if (pj_check_on())
+        if (pj_check_on()) {
+            std::vector<uint64_t> region(I), so(I + 1);
+            std::vector<uint32_t> tot(I);
+            if (I) {
+                PJ_CHECK(hipMemcpy(region.data(), pjRegion.p, (size_t) I * 8, hipMemcpyDeviceToHost));
+                PJ_CHECK(hipMemcpy(tot.data(), pjTot.p, (size_t) I * 4, hipMemcpyDeviceToHost));
+            }
+            PJ_CHECK(hipMemcpy(so.data(), pjSoff.p, (size_t) (I + 1) * 8, hipMemcpyDeviceToHost));
             for (uint32_t it = 0; it < I; it++)
-                if (region[it] + tot[it] > nseg * LS * 32) PJ_FAIL("item region outside the survivor buffer");
+                if (region[it] + tot[it] > nseg * LS * 32 || so[it + 1] != so[it] + tot[it])
+                    PJ_FAIL("item " + std::to_string(it) + " region or survivor scan inconsistent");
+            if (so[I] != bnd[F]) PJ_FAIL("survivor scan total");
+        }
         launch_pj_surv_pack(surv.as<uint32_t>(), pjRegion.as<uint64_t>(), pjTot.as<uint32_t>(), pjSoff.as<uint64_t>(),
                             I, sendS, stream);
         PJ_STAGE("k_pj_surv_pack");
@@ -430,7 +434,7 @@ int Engine::join_partitioned(const hwbrj_exchange_t* x, int rank, int world, con
         // per destination j: items of each of its partitions, then its survivor words
         for (uint32_t j = 0; j < W; j++) {
             for (uint32_t i = 0; i < QL; i++) scnt[j * NC + i] = isS[j * QL + i + 1] - isS[j * QL + i];
-            scnt[j * NC + QL] = sofs[isS[(j + 1) * QL]] - sofs[isS[j * QL]];
+            scnt[j * NC + QL] = bnd[(j + 1) * QL] - bnd[j * QL];
         }
         return drain();
     }();
@@ -459,8 +463,8 @@ int Engine::join_partitioned(const hwbrj_exchange_t* x, int rank, int world, con
     {
         uint64_t ro = 0;
         for (uint32_t j = 0; j < W; j++) {
-            soff[j]   = sofs[isS[j * QL]] * 4;
-            sbytes[j] = (sofs[isS[(j + 1) * QL]] - sofs[isS[j * QL]]) * 4;
+            soff[j]   = sofs[j * QL] * 4;  // (sofs: the survivor scan at every partition's first item)
+            sbytes[j] = (sofs[(j + 1) * QL] - sofs[j * QL]) * 4;
             roff[j]   = ro * 4;
             rbytes[j] = rwords[j] * 4;
             ro += rwords[j];
@@ -483,50 +487,61 @@ int Engine::join_partitioned(const hwbrj_exchange_t* x, int rank, int world, con
     lap(5);
     // ------------------------------------------------------------- 7. join of the owned partitions
     // (no collective follows: a failure here is this rank's alone)
-    // items of owned partition i: those of source 0, 1, ... (each source's block is in partition order)
-    std::vector<uint32_t> rm((size_t) RI * NSUB);
-    if (RI) {  // (on the join stream: a native transport's receive is still in flight)
-        PJ_CHECK(hipMemcpyAsync(rm.data(), recvM, (size_t) RI * NSUB * 4, hipMemcpyDeviceToHost, stream));
-        PJ_CHECK(hipStreamSynchronize(stream));
-    }
-    std::vector<uint64_t> ibase(RI);
-    std::vector<uint32_t> icnt((size_t) RI * NSUB), ioff((size_t) RI * NSUB), istart(QL + 1, 0), jobs((size_t) QL * NSUB, 0);
+    // The owner's item tables on the device (k_pj_item_tables) from the received per-item counts;
+    // the host lays out only the (owned partition, source) pairs: items of owned partition i are
+    // those of source 0, 1, ... (each source's block is in partition order).
+    const uint32_t NJ = QL * NSUB;
+    std::vector<uint32_t> tab2((size_t) 3 * QL * W), istart(QL + 1, 0);
     {
-        std::vector<uint64_t> jitem(W), jword(W), jpos(W, 0), wpos(W, 0);  // per source: block starts, cursors
-        uint64_t              ai = 0, aw = 0;
+        std::vector<uint64_t> jitem(W), jpos(W, 0);  // per source: first received item, cursor
+        uint64_t              ai = 0;
         for (uint32_t j = 0; j < W; j++) {
-            jitem[j] = ai, jword[j] = aw;
-            ai += ritems[j], aw += rwords[j];
+            jitem[j] = ai;
+            ai += ritems[j];
         }
         uint32_t out = 0;
         for (uint32_t i = 0; i < QL; i++) {
             istart[i] = out;
             for (uint32_t j = 0; j < W; j++) {
-                for (uint64_t k = 0; k < rcnt[j * NC + i]; k++) {
-                    const uint64_t src = jitem[j] + jpos[j]++;
-                    ibase[out]         = jword[j] + wpos[j];
-                    uint32_t o = 0;
-                    for (uint32_t s = 0; s < NSUB; s++) {
-                        const uint32_t c               = rm[src * NSUB + s];
-                        icnt[(size_t) out * NSUB + s] = c;
-                        ioff[(size_t) out * NSUB + s] = o;
-                        jobs[(size_t) i * NSUB + s] += c;
-                        o += c;
-                    }
-                    wpos[j] += o;
-                    out++;
-                }
+                const uint32_t c = (uint32_t) rcnt[j * NC + i];
+                uint32_t*      t = &tab2[3 * ((size_t) i * W + j)];
+                t[0]             = (uint32_t) (jitem[j] + jpos[j]);
+                t[1]             = c;
+                t[2]             = out;
+                jpos[j] += c;
+                out += c;
             }
         }
         istart[QL] = out;
     }
-    if (to_dev(pjIbase, ibase, stream) || to_dev(pjCnt, icnt, stream) || to_dev(pjOff, ioff, stream) ||
-        to_dev(pjIstart, istart, stream) || to_dev(pjJobs, jobs, stream)) {
+    const uint32_t nbr = (uint32_t) (RI / 1024 + 1);
+    if (!pjIbase.ensure(std::max<uint64_t>(16, RI * 8)) || !pjCnt.ensure(std::max<uint64_t>(16, RI * NSUB * 4)) ||
+        !pjOff.ensure(std::max<uint64_t>(16, RI * NSUB * 4)) || !pjJobs.ensure((uint64_t) NJ * 4) ||
+        !pjWtot.ensure(std::max<uint64_t>(16, RI * 4)) || !pjWscan.ensure((RI + 1) * 8) ||
+        !pjBsum.ensure((uint64_t) nbr * 8)) {
+        set_last_error("hipMalloc failed (device memory)");
+        return 4;
+    }
+    if (to_dev(pjTab2, tab2, stream) || to_dev(pjIstart, istart, stream)) {
         set_last_error("host tables to the device failed");
         return 4;
     }
-    const uint32_t NJ = QL * NSUB;
+    PJ_CHECK(hipMemsetAsync(pjJobs.p, 0, (size_t) NJ * 4, stream));
+    launch_pj_recv_scan(recvM, (uint32_t) RI, NSUB, pjWtot.as<uint32_t>(), pjBsum.as<uint64_t>(),
+                        pjWscan.as<uint64_t>(), stream);
+    launch_pj_item_tables(pjTab2.as<uint32_t>(), QL * W, W, recvM, pjWscan.as<uint64_t>(), NSUB,
+                          pjIbase.as<uint64_t>(), pjCnt.as<uint32_t>(), pjOff.as<uint32_t>(), pjJobs.as<uint32_t>(),
+                          stream);
     if (pj_check_on()) {
+        PJ_CHECK(hipStreamSynchronize(stream));
+        std::vector<uint64_t> ibase(RI), ws(RI + 1);
+        std::vector<uint32_t> icnt((size_t) RI * NSUB);
+        if (RI) {
+            PJ_CHECK(hipMemcpy(ibase.data(), pjIbase.p, RI * 8, hipMemcpyDeviceToHost));
+            PJ_CHECK(hipMemcpy(icnt.data(), pjCnt.p, RI * NSUB * 4, hipMemcpyDeviceToHost));
+        }
+        PJ_CHECK(hipMemcpy(ws.data(), pjWscan.p, (RI + 1) * 8, hipMemcpyDeviceToHost));
+        if (ws[RI] != RW) PJ_FAIL("received survivor scan total " + std::to_string(ws[RI]) + " != " + std::to_string(RW));
         for (uint64_t it = 0; it < RI; it++) {
             uint64_t t = 0;
             for (uint32_t s2 = 0; s2 < NSUB; s2++) t += icnt[it * NSUB + s2];

@@ -44,7 +44,8 @@ def torchrun(world, args, env_extra, timeout=300):
     port = s.getsockname()[1]
     s.close()
     env = dict(os.environ, **env_extra)
-    for k in ("HWBRJ_BENCH_SHARED_GPU", "HWBRJ_BENCH_DIST", "HWBRJ_PJ_FORCE_COLL", "HWBRJ_DEV_PJ_FAIL_RANK"):
+    for k in ("HWBRJ_BENCH_SHARED_GPU", "HWBRJ_BENCH_DIST", "HWBRJ_PJ_FORCE_COLL", "HWBRJ_DEV_PJ_FAIL_RANK",
+              "HWBRJ_RCCL_SELF"):
         if k not in env_extra:
             env.pop(k, None)
     p = subprocess.Popen(["python", "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
@@ -80,11 +81,16 @@ PJ_ARGS = [None, ("blocked", 1 << 24, 1, 1024), ("blocked", 1 << 22, 3, 512), ("
            ("sectorized", 1 << 22, 4, 512), ("blocked", 1 << 31, 2, 512)]
 
 
+@pytest.mark.parametrize("self_rccl", [False, True], ids=["self-copy", "self-rccl"])
 @pytest.mark.parametrize("a", PJ_ARGS, ids=str)
-def test_partitioned_rccl_world1_vs_oracle(hw, cuda, orc, rccl1, a):
+def test_partitioned_rccl_world1_vs_oracle(hw, cuda, orc, rccl1, a, self_rccl, monkeypatch):
     """hwbrj_join_partitioned_rccl: the R-chunk and survivor all-to-alls as grouped
     ncclSend/ncclRecv and the slice all-gather as ncclAllGather on the join stream (no host drain
-    before them); counts equal the oracle's, empty and odd-sized shards included."""
+    before them); counts equal the oracle's, empty and odd-sized shards included. A rank's own
+    block is a device copy; HWBRJ_RCCL_SELF=1 sends it through ncclSend/ncclRecv instead, so the
+    RCCL calls run at world 1."""
+    if self_rccl:
+        monkeypatch.setenv("HWBRJ_RCCL_SELF", "1")
     args = None if a is None else hw.BloomFilterArgs.from_flag(a[0], a[1], a[2], a[3] or 1024)
     rng = np.random.default_rng(41)
     for nR, nS in [(0, 1000), (1000, 0), (7, 33), (100003, 400009), (1000000, 4000000)]:
@@ -144,8 +150,9 @@ def test_bench_rccl_world1(hw, case):
     g = GOLD["F3_grid"]
     base = ["-r", g["r"], "-s", g["s"], "-m", g["m"]]
     env = {"HWBRJ_BENCH_DIST": "1"}
-    if case == "partitioned-native":
+    if case == "partitioned-native":  # (the rank's own blocks through ncclSend / ncclRecv too)
         args = base + ["--design", "partitioned", "--transport", "native"]
+        env["HWBRJ_RCCL_SELF"] = "1"
     elif case == "partitioned-torch-nccl":
         args = base + ["--design", "partitioned", "--transport", "torch"]
         env["HWBRJ_PJ_FORCE_COLL"] = "1"

@@ -37,6 +37,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, uint32_
 
 // tuples [t0, t0 + nt) of S -> words into the ring: workgroup g's region is [g * reg, (g + 1) * reg)
 // uint4s; each thread turns 4 tuples (two 16-byte loads) into one 16-byte store
+template <int SAUX>  // cache policy of the word stores: 2 = nt (k_scatter_s), 0 = default
 __global__ __launch_bounds__(1024) void k_writer(const uint4* __restrict__ S, uint64_t t0, uint64_t nt,
                                                  uint4* __restrict__ ring, uint64_t reg) {
     const uint64_t per = (nt / 4 + gridDim.x - 1) / gridDim.x;  // quads of tuples per workgroup
@@ -50,7 +51,7 @@ __global__ __launch_bounds__(1024) void k_writer(const uint4* __restrict__ S, ui
         const v4u      x = __builtin_amdgcn_raw_buffer_load_b128(rin, o * 32, 0, 2);
         const v4u      y = __builtin_amdgcn_raw_buffer_load_b128(rin, o * 32 + 16, 0, 2);
         const v4u      w = {x.x * 0x9E3779B1u, x.z ^ 0x5bd1e995u, y.x + 7u, y.z};
-        __builtin_amdgcn_raw_buffer_store_b128(w, rout, o * 16, 0, 2);
+        __builtin_amdgcn_raw_buffer_store_b128(w, rout, o * 16, 0, SAUX);
     }
 }
 
@@ -105,6 +106,8 @@ int main() {
     std::mt19937_64 rng(11);
     printf("S = %llu tuples (8.19 GB) streamed once; words 4.096 GB written then gathered, in windows of W\n",
            (unsigned long long) nS);
+    for (int saux : {2, 0}) {
+    printf("word stores %s\n", saux ? "nt (as k_scatter_s)" : "default policy");
     printf("%10s %5s %11s %11s %13s %11s %11s\n", "W", "wins", "writer ms", "reader ms", "reader+slice", "total ms",
            "total+slice");
     for (uint64_t W : {64ull << 20, 128ull << 20, 192ull << 20, 256ull << 20, 512ull << 20, 1ull << 30, 4ull << 30}) {
@@ -133,7 +136,8 @@ int main() {
                     const uint64_t t0 = (uint64_t) w * win_t, nt = std::min(win_t, nS - t0);
                     float          a, b;
                     CK(hipEventRecord(ev[0]));
-                    k_writer<<<G, 1024>>>(S, t0, nt, ring, reg);
+                    if (saux) k_writer<2><<<G, 1024>>>(S, t0, nt, ring, reg);
+                    else k_writer<0><<<G, 1024>>>(S, t0, nt, ring, reg);
                     CK(hipEventRecord(ev[1]));
                     k_reader<<<G, 1024>>>(ring, list, (uint32_t) std::min<uint64_t>(nch, nt / 32), withs ? slices : nullptr,
                                           slice_b / 16, sink);
@@ -151,6 +155,7 @@ int main() {
         printf("%7llu MiB %5u %11.3f %11.3f %13.3f %11.3f %11.3f\n", (unsigned long long) (W >> 20), nwin, best[0],
                best[1], best[2], best[0] + best[1], best[0] + best[2]);
         fflush(stdout);
+    }
     }
     return 0;
 }

@@ -33,7 +33,22 @@ for G in [int(x) for x in sys.argv[1:]] or [1, 8]:
         if best is None or wall < best[0]:
             best = (wall, st)
     w, st = best
-    print(f"G={G} partitioned rank (world 1): wall {w:.3f} ms: R pass {st.ms_r_scatter:.3f} R xchg {st.ms_r_index:.3f} "
+    print(f"G={G} partitioned rank (world 1, torch callbacks): wall {w:.3f} ms: R pass {st.ms_r_scatter:.3f} R xchg {st.ms_r_index:.3f} "
+          f"build {st.ms_build:.3f} S pass {st.ms_s_scatter:.3f} xchg(slices+surv) {st.ms_surv:.3f} join {st.ms_join:.3f} "
+          f"counts {st.filtered} {st.matches}", flush=True)
+    # the same rank over the library's own RCCL communicator (world 1: send/recv to self)
+    pjoin.comm_init()
+    best = None
+    for i in range(4):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        st = pjoin.join_partitioned_rccl(dRs, dS, nR, args)
+        wall = (time.perf_counter() - t0) * 1e3
+        if best is None or wall < best[0]:
+            best = (wall, st)
+    pjoin.comm_destroy()
+    w, st = best
+    print(f"G={G} partitioned rank (world 1, native RCCL): wall {w:.3f} ms: R pass {st.ms_r_scatter:.3f} R xchg {st.ms_r_index:.3f} "
           f"build {st.ms_build:.3f} S pass {st.ms_s_scatter:.3f} xchg(slices+surv) {st.ms_surv:.3f} join {st.ms_join:.3f} "
           f"counts {st.filtered} {st.matches}", flush=True)
     del dRs, dS, x
