@@ -21,7 +21,7 @@ __all__ = [
     "generate_host", "nonunique_threshold", "create_relation_nonunique",
     "create_relation_nonunique_from_pk", "create_relation_fk_from_pk", "create_relation_zipf",
     "rand_stream", "reference_relations", "create_relation_zipf_device",
-    "export_filter", "hash_crc", "hash_crapwow", "lib", "LIB_PATH", "shard_range",
+    "export_filter", "hash_crc", "hash_crapwow", "lib", "LIB_PATH", "shard_range", "write_relation",
 ]
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
@@ -145,6 +145,10 @@ def lib() -> ctypes.CDLL:
             ctypes.c_double, ctypes.c_int, ctypes.c_void_p]
         L.hwbrj_rand_stream.restype = ctypes.c_int
         L.hwbrj_rand_stream.argtypes = [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint64]
+        L.hwbrj_write_relation.restype = ctypes.c_int
+        L.hwbrj_write_relation.argtypes = [ctypes.POINTER(_Relation), ctypes.c_char_p]
+        L.hwbrj_write_result_relation.restype = ctypes.c_int
+        L.hwbrj_write_result_relation.argtypes = [ctypes.c_void_p, ctypes.c_char_p]
         L.hwbrj_export_filter.restype = ctypes.c_int
         L.hwbrj_export_filter.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
         L.hwbrj_hash_crc.restype = ctypes.c_uint32
@@ -297,6 +301,13 @@ class Relation:
     @property
     def num_tuples(self) -> int:
         return self.tuples.shape[0]
+
+
+def write_relation(rel: "Relation | np.ndarray", filename: str) -> None:
+    """src/generator.c:250-263 write_relation (hwbrj_write_relation): a "#KEY, VAL" header, then
+    "key payload" lines; the CLI's -R / -S read it back."""
+    r = rel if isinstance(rel, Relation) else Relation(rel)
+    _err(lib().hwbrj_write_relation(ctypes.byref(r._c), os.fsencode(filename)), "hwbrj_write_relation")
 
 
 def assert_args(args: BloomFilterArgs) -> bool:

@@ -15,6 +15,7 @@
 // Host code, compiled without floating-point contraction: RAND_RANGE's a*b+c must round like the
 // reference's x86-64 build (no FMA).
 #include <math.h>
+#include <stdio.h>
 #include <stdint.h>
 #include <string.h>
 
@@ -298,6 +299,88 @@ int hwbrj_create_relation_zipf_device(tuple_t* d_out, uint64_t n, uint64_t alpha
     (void) hipFree(d_lut);
     (void) hipFree(d_rnd);
     return 0;
+}
+
+// ---- relation files (the reference's PERSIST_RELATIONS output, the only on-disk format) ----
+// "%d %d\n" lines through a large buffer (fprintf per tuple is slow for 10^9 tuples).
+static int write_pairs(FILE* fp, const tuple_t* t, uint64_t n) {
+    std::vector<char> buf(1 << 20);
+    size_t            used = 0;
+    auto put_int = [&](int32_t v, char end) {
+        char     tmp[16];
+        int      len = 0;
+        uint32_t u   = v < 0 ? 0u - (uint32_t) v : (uint32_t) v;
+        do {
+            tmp[len++] = (char) ('0' + u % 10);
+            u /= 10;
+        } while (u);
+        if (v < 0) buf[used++] = '-';
+        while (len) buf[used++] = tmp[--len];
+        buf[used++] = end;
+    };
+    for (uint64_t i = 0; i < n; i++) {
+        if (used + 32 > buf.size()) {
+            if (fwrite(buf.data(), 1, used, fp) != used) return 1;
+            used = 0;
+        }
+        put_int(t[i].key, ' ');
+        put_int(t[i].payload, '\n');
+    }
+    return used && fwrite(buf.data(), 1, used, fp) != used ? 1 : 0;
+}
+
+// src/generator.c:250-263 write_relation: a "#KEY, VAL" header, then "key payload" lines.
+int hwbrj_write_relation(const relation_t* rel, const char* filename) {
+    FILE* fp = fopen(filename, "w");
+    if (!fp) {
+        set_last_error(std::string("cannot open ") + filename);
+        return 2;
+    }
+    int rc = fputs("#KEY, VAL\n", fp) < 0 ? 1 : write_pairs(fp, rel->tuples, rel->num_tuples);
+    if (fclose(fp) != 0) rc = 1;
+    if (rc) set_last_error(std::string("write failed: ") + filename);
+    return rc;
+}
+
+// src/tuple_buffer.h:155-236 write_result_relation (SORTED_MATERIALIZE_TO_FILE 0, its default):
+// every worker's chained result buffers, "R.payload S.payload" lines, no header. The buffers are
+// this library's (result_t.resultlist of a materializing BPRO / PRO, hwbrj_api.cpp).
+int hwbrj_write_result_relation(const result_t* res, const char* filename) {
+    struct Buf {
+        tuple_t* tuples;
+        Buf*     next;
+    };
+    struct Chain {
+        Buf*     buf;
+        Buf*     readcursor;
+        Buf*     writecursor;
+        uint32_t writepos, readpos, readlen, numbufs;
+    };
+    constexpr uint64_t kPer = 1024 * 1024;  // CHAINEDBUFF_NUMTUPLESPERBUF (tuple_buffer.h)
+    if (!res || !res->resultlist) {
+        set_last_error("the result holds no materialized pairs (hwbrj_set_materialize)");
+        return 2;
+    }
+    FILE* fp = fopen(filename, "w");
+    if (!fp) {
+        set_last_error(std::string("cannot open ") + filename);
+        return 2;
+    }
+    int rc = 0;
+    for (int t = 0; t < res->nthreads && rc == 0; t++) {
+        const Chain* cb = (const Chain*) res->resultlist[t].results;
+        if (!cb) continue;
+        uint64_t left = (uint64_t) res->resultlist[t].nresults;
+        bool     head = true;  // the newest buffer holds writepos pairs, the older ones are full
+        for (const Buf* b = cb->buf; b && left && rc == 0; b = b->next, head = false) {
+            const uint64_t n = std::min<uint64_t>(left, head ? cb->writepos : kPer);
+            rc = write_pairs(fp, b->tuples, n);
+            left -= n;
+        }
+    }
+    if (fclose(fp) != 0) rc = 1;
+    if (rc) set_last_error(std::string("write failed: ") + filename);
+    return rc;
 }
 
 }  // extern "C"

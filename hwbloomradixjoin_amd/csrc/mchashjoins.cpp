@@ -54,6 +54,8 @@ static void print_help(const char* prog) {
         "       -z --skew=<z>      Zipf skew parameter for probe relation S <z> [0.0]   \n"
         "       --non-unique       Use non-unique (duplicated) keys in input relations  \n"
         "       --full-range       Spread keys in relns. in full 32-bit integer range   \n"
+        "       --persist          Write R.tbl / S.tbl (and Out.tbl when materializing) \n"
+        "                          as a -DPERSIST_RELATIONS reference build does        \n"
         "       -R --r-file=<Rf>   The file to load build relation R from <Rf> [R.tbl]  \n"
         "       -S --s-file=<Sf>   The file to load probe relation S from <Sf> [S.tbl]  \n"
         "                                                                               \n"
@@ -104,11 +106,12 @@ static int load_relation(relation_t* rel, const char* path, uint64_t n) {
 
 int main(int argc, char** argv) {
     Params         P;
-    static int     nonunique = 0, fullrange = 0, basic_numa = 0, verbose = 0;
+    static int     nonunique = 0, fullrange = 0, basic_numa = 0, verbose = 0, persist = 0;
     static option  opts[] = {{"verbose", no_argument, &verbose, 1},
                             {"brief", no_argument, &verbose, 0},
                             {"non-unique", no_argument, &nonunique, 1},
                             {"full-range", no_argument, &fullrange, 1},
+                            {"persist", no_argument, &persist, 1},
                             {"basic-numa", no_argument, &basic_numa, 1},
                             {"help", no_argument, 0, 'h'},
                             {"version", no_argument, 0, 'v'},
@@ -211,6 +214,14 @@ int main(int argc, char** argv) {
                                   P.r_seed, hthreads), "R");
     }
     printf("OK \n");
+    // src/generator.c:408-412 (PERSIST_RELATIONS): every generated relation, R then S
+    auto persist_rel = [&](const relation_t* rel, const char* name) {
+        if (persist && hwbrj_write_relation(rel, name) != 0) {
+            printf("[ERROR] %s\n", hwbrj_last_error());
+            exit(EXIT_FAILURE);
+        }
+    };
+    if (!P.loadR) persist_rel(&relR, "R.tbl");
     fprintf(stdout, "[INFO ] %s relation S with size = %.3lf MiB, #tuples = %lld : ",
             P.loadS ? "Loading" : "Creating", 8.0 * P.s_size / 1024.0 / 1024.0,
             (long long) P.s_size);
@@ -235,6 +246,7 @@ int main(int argc, char** argv) {
                                   P.s_seed, hthreads), "S");
     }
     printf("OK \n");
+    if (!P.loadS) persist_rel(&relS, "S.tbl");
     printf("[INFO ] Running join algorithm %s ...\n", P.algo.c_str());
     // src/main.c:331-339 algos[] and :473-478 (joinAlgoBloom when -b is not "no")
     struct Algo {
@@ -249,6 +261,13 @@ int main(int argc, char** argv) {
     result_t* res = P.bloom ? algo->bloom(&relR, &relS, (int) P.nthreads, &P.bf)
                             : algo->join(&relR, &relS, (int) P.nthreads);
     printf("[INFO ] Results = %llu. DONE.\n", (unsigned long long) res->totalresults);
+    if (persist && res->resultlist) {  // src/main.c:482-485 (PERSIST_RELATIONS + JOIN_RESULT_MATERIALIZE)
+        printf("[INFO ] Persisting the join result to \"Out.tbl\" ...\n");
+        if (hwbrj_write_result_relation(res, "Out.tbl") != 0) {
+            printf("[ERROR] %s\n", hwbrj_last_error());
+            exit(EXIT_FAILURE);
+        }
+    }
     free(relR.tuples);
     free(relS.tuples);
     free(res);

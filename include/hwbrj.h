@@ -260,6 +260,15 @@ int      hwbrj_create_relation_zipf_device(tuple_t * d_out, uint64_t n, uint64_t
 /* The first n values rand() returns after srand(seed) (test hook for the restatement). */
 int      hwbrj_rand_stream(uint32_t seed, int32_t * out, uint64_t n);
 
+/* Relation files, the reference's PERSIST_RELATIONS output (the only on-disk format; the CLI's
+ * --persist writes R.tbl / S.tbl / Out.tbl like a -DPERSIST_RELATIONS reference build):
+ *   hwbrj_write_relation         src/generator.c:250-263 write_relation ("#KEY, VAL" header,
+ *                                "key payload" lines); -R / -S read it back
+ *   hwbrj_write_result_relation  src/tuple_buffer.h:155-236 write_result_relation: the pairs of a
+ *                                materializing BPRO / PRO result ("R.payload S.payload", no header) */
+int hwbrj_write_relation(const relation_t * rel, const char * filename);
+int hwbrj_write_result_relation(const result_t * res, const char * filename);
+
 /* The filter built by the last join, in the reference's byte layout (src/bloom_filter.c:143-171:
  * m/8 bytes, bit h of a block at byte h>>3, bit h&7). nbytes must be m/8. */
 int hwbrj_export_filter(uint8_t * host_out, uint64_t nbytes);

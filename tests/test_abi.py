@@ -122,3 +122,18 @@ def test_rccl_binding_draws_unique_id(hw):
     assert hw.lib().hwbrj_comm_unique_id(a) == 0, hw.lib().hwbrj_last_error()
     assert hw.lib().hwbrj_comm_unique_id(b) == 0
     assert any(bytes(a)) and bytes(a) != bytes(b)
+
+
+def test_write_relation_format(hw, tmp_path):
+    """hwbrj_write_relation: src/generator.c:250-263's file, byte for byte as its fprintf writes it
+    ("#KEY, VAL" header, "%d %d" lines), negative and extreme values included."""
+    import numpy as np
+    rng = np.random.default_rng(5)
+    t = np.stack([rng.integers(-2**31, 2**31, size=5000), rng.integers(-2**31, 2**31, size=5000)], 1)
+    t[:4] = [[0, 0], [-1, 2**31 - 1], [-2**31, -2**31], [2**31 - 1, -7]]
+    f = tmp_path / "R.tbl"
+    hw.write_relation(t.astype(np.int32), str(f))
+    want = "#KEY, VAL\n" + "".join(f"{k} {p}\n" for k, p in t.tolist())
+    assert f.read_text() == want
+    hw.write_relation(np.zeros((0, 2), dtype=np.int32), str(f))
+    assert f.read_text() == "#KEY, VAL\n"

@@ -158,6 +158,31 @@ def test_tbl_loader(hw, orc, tmp_path):
         assert counts(out) == (filt, res)
 
 
+def test_cli_persist_round_trip(hw, orc, tmp_path):
+    """--persist (a -DPERSIST_RELATIONS reference build, src/generator.c:408-412 and
+    src/main.c:482-485): the CLI writes R.tbl and S.tbl as it generates them and, materializing,
+    the pairs to Out.tbl (src/tuple_buffer.h:155-236). Out.tbl is the oracle's pair multiset on the
+    written relations, and -R R.tbl -S S.tbl reproduces the counts."""
+    def run(*args):
+        out = subprocess.run([hw.CLI_PATH, *map(str, args)], capture_output=True, text=True, timeout=600,
+                             cwd=tmp_path, env=dict(os.environ, HWBRJ_MATERIALIZE="1"))
+        assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-3000:]
+        return out.stdout
+    flags = ["-a", "PRO", "-r", 200000, "-s", 1000000, "-q", 0.05, "-b", "blocked", "-m", 1 << 22, "-k", 2]
+    out = run(*flags, "--persist")
+    assert '[INFO ] Persisting the join result to "Out.tbl" ...' in out
+    load = lambda f: np.loadtxt(tmp_path / f, dtype=np.int64, comments="#", ndmin=2).astype(np.int32)  # noqa: E731
+    R, S, pairs = load("R.tbl"), load("S.tbl"), load("Out.tbl")
+    assert (tmp_path / "R.tbl").read_text().startswith("#KEY, VAL\n") and R.shape == (200000, 2)
+    res, filt, _ = orc.bpro(R, S, 8, hw.BLOCKED, 1 << 22, 2, 1024)
+    assert counts(out) == (filt, res) == (filt, 50000)
+    want = orc.join_pairs(R, S)
+    key = lambda x: x[np.lexsort((x[:, 1], x[:, 0]))]  # noqa: E731
+    assert np.array_equal(key(pairs), key(want))
+    out2 = run(*flags, "-R", tmp_path / "R.tbl", "-S", tmp_path / "S.tbl")
+    assert counts(out2) == (filt, res)
+
+
 def test_device_zipf_equals_host_zipf(hw, cuda):
     """hwbrj_create_relation_zipf_device at q = 1 is the -z relation (src/genzipf.c:98-158) of
     hwbrj_create_relation_zipf, key for key and row for row."""
