@@ -365,6 +365,9 @@ constexpr int      kScThreads = 1024;
 #ifndef HWBRJ_SC_PRE
 #define HWBRJ_SC_PRE 1
 #endif
+#ifndef HWBRJ_SC_KEEPY
+#define HWBRJ_SC_KEEPY 1
+#endif
 #ifndef HWBRJ_SC_LAUX
 #define HWBRJ_SC_LAUX 2  // cache policy of the tuple loads: nt (read once; 0 measured 2 % slower)
 #endif
@@ -536,6 +539,10 @@ struct ScRaw {  // one round's raw loads of this thread (tuples: keys only; code
     uint32_t k[SRC == SRC_TUPLES ? kScE : 1];
     uint4    v[SRC == SRC_TUPLES ? 1 : kScE / 4];
     uint32_t jb[SRC == SRC_TUPLES ? kScE : 1];  // MODE_BASIC_POS: which bit of the key
+    // the payloads of a 16-byte tuple-pair load, unused but held until the keys are consumed: a
+    // load's destination registers must not be reused while it is in flight, so a dead payload
+    // register taken for a temporary costs an s_waitcnt vmcnt(0) right after the loads are issued
+    uint32_t y[SRC == SRC_TUPLES && HWBRJ_SC_KEEPY ? kScE : 1];
 };
 
 // LDS: static CRC nibble table (512 B, at 0, so its row offsets are immediates); dynamic (words):
@@ -613,12 +620,17 @@ __device__ __forceinline__ void scatter_body(const ScatterParams& P) {
                 const v4u x = __builtin_amdgcn_raw_buffer_load_b128(rsrc, 2 * tid * EB, (base + h * 2 * kScThreads) * EB, HWBRJ_SC_LAUX);
                 R.k[2 * h]     = x.x;
                 R.k[2 * h + 1] = x.z;
+                if (HWBRJ_SC_KEEPY) {
+                    R.y[2 * h]     = x.y;
+                    R.y[2 * h + 1] = x.w;
+                }
             }
         } else if (SRC == SRC_TUPLES) {
 #pragma unroll
             for (int j = 0; j < kScE; j++) {
                 const uint32_t i = base + (j >> 1) * 2 * kScThreads + 2 * tid + (j & 1);
                 R.k[j] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, i < len ? i * EB : kOob, 0, 0);
+                if (HWBRJ_SC_KEEPY) R.y[j] = 0;
             }
 #else
         } else if (SRC == SRC_TUPLES && base + kScRound <= len) {
@@ -741,10 +753,14 @@ __device__ __forceinline__ void scatter_body(const ScatterParams& P) {
         }
     };
 
-    auto round = [&](uint32_t base, ScRaw<SRC>& R) {
+    // The round's words: hash (consumes R) of the round at `base`; q = F marks elements past len.
+    uint32_t q[kScE], w[kScE];
+    auto hash = [&](uint32_t base, const ScRaw<SRC>& R) {
         const bool full = base + kScRound <= len;  // uniform
-        // ---- A: hash (consumes R), refill R, copy out the last plan, rank
-        uint32_t q[kScE], w[kScE];
+        if (SRC == SRC_TUPLES && MODE != MODE_BASIC_POS && HWBRJ_SC_KEEPY) {
+#pragma unroll
+            for (int j = 0; j < kScE; j++) asm volatile("" ::"v"(R.y[j]));  // (ScRaw::y)
+        }
 #pragma unroll
         for (int j = 0; j < kScE; j++) {
             uint32_t x, idx;
@@ -773,6 +789,11 @@ __device__ __forceinline__ void scatter_body(const ScatterParams& P) {
                 if (idx >= len) q[j] = F;  // invalid: ranked on the dummy counter
             }
         }
+    };
+    auto round = [&](uint32_t base, ScRaw<SRC>& R) {
+        const bool full = base + kScRound <= len;  // uniform
+        // ---- A: hash (consumes R), refill R, copy out the last plan, rank
+        hash(base, R);
         stamp(0);
         load_round(base + kScPre * kScRound, R);
 #ifndef HWBRJ_SC_NOORD
