@@ -267,6 +267,12 @@ def main():
                     "frac": round(dom_alg / (dom_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if dom_alg else None,
                     "traffic": pm["phases"].get(dom, {}).get("hbm_bytes") if pm else None}}
 
+    if world == 1:  # the measured copy rate beside the spec peak (not the frac's denominator)
+        cbw = round(hw.copy_bandwidth(4 << 30, 5), 1)
+        roofline["copy_measured"] = {"GBps": cbw, "frac_of_copy": round(achieved / cbw, 4),
+                                     "what": "hwbrj_copy_bandwidth: streaming 16-byte nt copy of 4 GiB, "
+                                             "(read + write) bytes / median time of 5; the spec peak "
+                                             "stays the denominator"}
     cpu = None
     if world == 1 and not a.no_cpu_baseline:
         cpu = cpu_baseline(a, hw)

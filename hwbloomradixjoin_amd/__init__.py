@@ -161,6 +161,8 @@ def lib() -> ctypes.CDLL:
         L.hwbrj_last_error.restype = ctypes.c_char_p
         L.hwbrj_version.restype = ctypes.c_char_p
         L.hwbrj_tsc_hz.restype = ctypes.c_uint64
+        L.hwbrj_copy_bandwidth.restype = ctypes.c_int
+        L.hwbrj_copy_bandwidth.argtypes = [ctypes.c_uint64, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
         L.hwbrj_release.restype = None
         _LIB = L
     return _LIB
@@ -447,6 +449,14 @@ def join_materialize_device(R, S, args: Optional[BloomFilterArgs] = None, stream
     _err(rc, "hwbrj_join_materialize_device")
     stats = Stats(**{f: getattr(st2, f) for f, _ in _Stats._fields_})
     return stats, out[: n.value], ms.value
+
+
+def copy_bandwidth(nbytes: int = 4 << 30, reps: int = 5) -> float:
+    """GB/s of a streaming device copy ((read + write) bytes / median time; hwbrj_copy_bandwidth):
+    the measured copy rate the roofline reports beside the 8 TB/s spec peak."""
+    g = ctypes.c_double()
+    _err(lib().hwbrj_copy_bandwidth(int(nbytes), int(reps), ctypes.byref(g)), "hwbrj_copy_bandwidth")
+    return g.value
 
 
 def generate_device(out, nthreads: int, maxid: int, threshold: int, selectivity: float,

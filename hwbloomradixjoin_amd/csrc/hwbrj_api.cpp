@@ -61,6 +61,52 @@ uint64_t hwbrj_tsc_hz(void) {
     return hz;
 }
 
+int hwbrj_copy_bandwidth(uint64_t bytes, int reps, double* gbps) {
+    if (!gbps || reps < 1 || bytes < 16 || bytes % 16) {
+        set_last_error("hwbrj_copy_bandwidth: bytes must be a positive multiple of 16, reps >= 1");
+        return 1;
+    }
+    void *a = nullptr, *b = nullptr;
+    if (hipMalloc(&a, bytes) != hipSuccess || hipMalloc(&b, bytes) != hipSuccess) {
+        if (a) (void) hipFree(a);
+        set_last_error("hwbrj_copy_bandwidth: hipMalloc failed");
+        return 6;
+    }
+    hipStream_t st = nullptr;
+    hipEvent_t  e0 = nullptr, e1 = nullptr;
+    int         rc = 0;
+    std::vector<float> ms;
+    if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess || hipEventCreate(&e0) != hipSuccess ||
+        hipEventCreate(&e1) != hipSuccess || hipMemsetAsync(a, 1, bytes, st) != hipSuccess) {
+        rc = 3;
+    } else {
+        int dev = 0, cus = 256;
+        (void) hipGetDevice(&dev);
+        (void) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        launch_copy_bw(a, b, bytes, cus, st);  // warm-up (page mapping, clocks)
+        for (int r = 0; r < reps && rc == 0; r++) {
+            float t = 0;
+            (void) hipEventRecord(e0, st);
+            launch_copy_bw(a, b, bytes, cus, st);
+            (void) hipEventRecord(e1, st);
+            if (hipEventSynchronize(e1) != hipSuccess || hipEventElapsedTime(&t, e0, e1) != hipSuccess) rc = 3;
+            ms.push_back(t);
+        }
+    }
+    if (rc == 0) {
+        std::sort(ms.begin(), ms.end());
+        *gbps = 2.0 * (double) bytes / (ms[ms.size() / 2] * 1e-3) / 1e9;
+    } else {
+        set_last_error(std::string("hwbrj_copy_bandwidth: ") + hipGetErrorString(hipGetLastError()));
+    }
+    if (e0) (void) hipEventDestroy(e0);
+    if (e1) (void) hipEventDestroy(e1);
+    if (st) (void) hipStreamDestroy(st);
+    (void) hipFree(a);
+    (void) hipFree(b);
+    return rc;
+}
+
 uint32_t hwbrj_hash_crc(uint32_t seed, int32_t key) { return crc_f_bitwise(seed ^ (uint32_t) key); }
 uint32_t hwbrj_hash_crapwow(uint32_t seed, int32_t key) { return crapwow(seed, (uint32_t) key); }
 

@@ -198,5 +198,8 @@ void   launch_pj_surv_pack(const uint32_t* surv, const uint64_t* region, const u
                            const uint64_t* soff, uint32_t n, uint32_t* out, hipStream_t st);
 void   launch_export(const uint32_t* slices, const Geometry& g, uint32_t* out, uint64_t nwords,
                      hipStream_t st);
+// a streaming copy of bytes (multiple of 16) from src to dst, grid workgroups of contiguous ranges
+// (hwbrj_copy_bandwidth)
+void   launch_copy_bw(const void* src, void* dst, uint64_t bytes, int grid, hipStream_t st);
 
 }  // namespace hwbrj

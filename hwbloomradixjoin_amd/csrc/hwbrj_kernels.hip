@@ -3537,6 +3537,30 @@ size_t scatter_lds_bytes(uint32_t log2F) {
 
 // The R and S scatters are one body under two kernel names, so per-kernel profiles (rocprofv3
 // --kernel-trace --stats) report the two phases separately.
+// ---------------------------------------------------------- measured copy rate (hwbrj_copy_bandwidth)
+// The roofline's "measured copy-kernel bandwidth" beside the spec peak: every
+// workgroup streams its own contiguous range (the shape of the scatter's reads), 16-byte loads,
+// four in flight per thread.
+__global__ __launch_bounds__(1024) void k_copy_bw(const uint4* __restrict__ src, uint4* __restrict__ dst, uint64_t n) {
+    const uint64_t per = (n + gridDim.x - 1) / gridDim.x;
+    const uint64_t b = (uint64_t) blockIdx.x * per, e = min(n, b + per);
+    for (uint64_t i = b + threadIdx.x; i < e; i += 4u * 1024u) {
+        uint4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const uint64_t k = i + u * 1024u;
+            v[u] = k < e ? src[k] : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+            if (i + u * 1024u < e) dst[i + u * 1024u] = v[u];
+    }
+}
+
+void launch_copy_bw(const void* src, void* dst, uint64_t bytes, int grid, hipStream_t st) {
+    k_copy_bw<<<grid, 1024, 0, st>>>((const uint4*) src, (uint4*) dst, bytes / 16);
+}
+
 template <int SRC, int MODE, int FMT>
 __global__ __launch_bounds__(kScThreads) void k_scatter_r(ScatterParams P) { scatter_body<SRC, MODE, FMT>(P); }
 template <int SRC, int MODE, int FMT>

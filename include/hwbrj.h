@@ -277,6 +277,12 @@ int hwbrj_export_filter(uint8_t * host_out, uint64_t nbytes);
  * reference's rdtsc timers, src/rdtsc.h:35-68), calibrated once against the steady clock. */
 uint64_t hwbrj_tsc_hz(void);
 
+/* Measurement utility (no reference counterpart): the device's streaming copy rate, for the
+ * roofline's measured-copy figure beside the spec peak. Copies `bytes` (a
+ * multiple of 16) between two fresh device buffers `reps` times; *gbps = (read + write bytes) /
+ * the median copy time. Returns 0, or an error code (device memory). */
+int hwbrj_copy_bandwidth(uint64_t bytes, int reps, double * gbps);
+
 /* Scalar hashes on the host (test hooks): crc32c(seed,key) and CrapWow(seed,key). */
 uint32_t hwbrj_hash_crc(uint32_t seed, int32_t key);
 uint32_t hwbrj_hash_crapwow(uint32_t seed, int32_t key);

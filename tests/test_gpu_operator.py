@@ -433,3 +433,12 @@ def test_weak_scaling_ranks_reach_the_golden(hw, cuda):
         hw.generate_device(dS, 2, INT_MAX, nR, g["q"], 54321 + rank)
         st = hw.join_device(dR, dS, hw.BloomFilterArgs(hw.BLOCKED, g["m"], 1, g["B"]))
         assert (st.filtered, st.matches) == (g["k1_filtered"], g["results"])
+
+
+def test_copy_bandwidth_is_plausible(hw, cuda):
+    """hwbrj_copy_bandwidth (the roofline's measured copy rate): a streaming copy on one MI355X runs
+    between 1 TB/s and the 8 TB/s spec peak (read + write bytes per second)."""
+    g = hw.copy_bandwidth(1 << 30, 3)
+    assert 1000.0 < g < 8000.0, g
+    with pytest.raises(RuntimeError):
+        hw.copy_bandwidth(15, 1)
