@@ -387,7 +387,8 @@ def _check_rel(R, S):
 
 def join_device_async(R, S, args: Optional[BloomFilterArgs] = None, stream=None) -> None:
     """Enqueue the join of device tensors R, S without waiting (hwbrj_join_device_async);
-    join_wait() returns the Stats of the last join enqueued on this device."""
+    join_wait() returns the Stats of the last join enqueued on this device (counts; an async join
+    records no phase events, so its ms_* fields are 0)."""
     _check_rel(R, S)
     a = args._c() if args is not None else None
     sp = ctypes.c_void_p(stream.cuda_stream) if stream is not None else None

@@ -244,7 +244,13 @@ Engine::Engine(int device) : device_(device) {
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess) cus_ = prop.multiProcessorCount;
     (void) hipStreamCreateWithFlags(&own_stream_, hipStreamNonBlocking);
-    for (auto& e : ev_) (void) hipEventCreate(&e);
+    // ev_[0..7] only time phases (elapsed-time reads after ev_[8] has completed): no system-scope
+    // fence on record, whose cache writeback idled the GPU ~6 us per marker. ev_[8] (waited on,
+    // and ordering later joins) and ev_[9] keep the default release.
+    unsigned evf = hipEventDisableSystemFence;
+    if (const char* e = getenv("HWBRJ_DEV_EVFLAGS")) evf = (unsigned) strtoul(e, nullptr, 0);  // dev A/B
+    for (int i = 0; i < 10; i++)
+        (void) (i < 8 ? hipEventCreateWithFlags(&ev_[i], evf) : hipEventCreate(&ev_[i]));
     CrcTables t;
     if (!build_crc_tables(&t)) set_last_error("CRC table inversion failed");
     (void) hipMalloc((void**) &d_tabs_, sizeof(CrcTables));
@@ -280,7 +286,19 @@ int Engine::run(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
 
 int Engine::run_async(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
                       const bloom_filter_args_t* args, hipStream_t stream, int jkind) {
-    return enqueue(dR, nR, dS, nS, args, stream, false, jkind);
+    // back-to-back joins: no phase events (each marker idles the GPU ~6 us between the kernels
+    // around it, profiles/r03/gaps_*), so hwbrj_join_wait reports counts only
+    phase_ev_    = false;
+    const int rc = enqueue(dR, nR, dS, nS, args, stream, false, jkind);
+    phase_ev_    = true;
+    return rc;
+}
+
+// Phase boundary i (synchronous joins only). A marker idles the GPU ~6 us between the kernels
+// around it; attaching the boundary to the next kernel's dispatch instead (hipExtLaunchKernel's
+// start event) measured slower still (~10 us gaps, profiles/r03/async_no_events_ab.log).
+hipError_t Engine::mark(int i, hipStream_t stream) {
+    return phase_ev_ ? hipEventRecord(ev_[i], stream) : hipSuccess;
 }
 
 int Engine::reserve(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
@@ -321,13 +339,14 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     if (!mat && g.mode == MODE_SLICE_BASIC && (g.k > 1 || kk1) && (uint64_t) g.k * nR <= (1ull << 31) &&
         !getenv("HWBRJ_DEV_KK_GATHER")) {
         if (!stream) stream = own_stream_;
-        if (pending_) HWBRJ_CHECK(hipStreamWaitEvent(stream, ev_[8], 0));
+        if (pending_ && stream != pending_stream_) HWBRJ_CHECK(hipStreamWaitEvent(stream, ev_[8], 0));
         return enqueue_basic_kk(dR, nR, dS, nS, g, stream, jkind);
     }
     if (!stream) stream = own_stream_;
     // Every join on this device shares this Engine's scratch (pools, lists, slices, counters):
-    // a join enqueued on another stream than a still-pending one must run after it.
-    if (pending_) HWBRJ_CHECK(hipStreamWaitEvent(stream, ev_[8], 0));
+    // a join enqueued on another stream than a still-pending one must run after it (on the same
+    // stream, stream order does it: no wait packet between back-to-back joins).
+    if (pending_ && stream != pending_stream_) HWBRJ_CHECK(hipStreamWaitEvent(stream, ev_[8], 0));
     const uint32_t F = 1u << g.log2F, NSUB = 1u << g.log2NSUB, NJ = F * NSUB;
     const bool     slice_mode = g.mode == MODE_SLICE_BLOCK || g.mode == MODE_SLICE_BASIC;
     const uint32_t nseg       = slice_mode ? g.nseg : 1;
@@ -392,18 +411,19 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     uint64_t* d_dcount   = small.as<uint64_t>() + 1;  // [1] dense survivor count (global mode)
     uint64_t* d_filtered = small.as<uint64_t>() + 2;  // [2] S-tuples after filter
 
-    // zeroing outside the timed region (the reference callocs before its timer, :1583, :1601);
-    // job_surv is left zero by every join's k_join_split, so it is cleared only when new
-    HWBRJ_CHECK(hipMemsetAsync(small.p, 0, 64, stream));
+    // zeroing (the reference callocs before its timer, :1583, :1601): the counts and the join's
+    // extra-task count are zeroed by the R scatter's workgroup 0 (two memset dispatches less per
+    // join); job_surv is left zero by every join's k_join_split, so it is cleared only when new
     if (jnew) HWBRJ_CHECK(hipMemsetAsync(jparts.p, 0, jparts.bytes, stream));
-    HWBRJ_CHECK(hipMemsetAsync(jparts.as<uint32_t>() + 2 * NJ, 0, 4, stream));
     if (g.mode == MODE_GLOBAL) HWBRJ_CHECK(hipMemsetAsync(bitmap.p, 0, bitmap.bytes, stream));
 
     ScatterParams sp{};
     sp.tabs = d_tabs_;
     sp.g    = g;
+    sp.zero_small = small.as<uint32_t>();  // (the R scatter only: cleared below)
+    sp.zero_word  = jparts.as<uint32_t>() + 2 * NJ;
 
-    HWBRJ_CHECK(hipEventRecord(ev_[0], stream));
+    HWBRJ_CHECK(mark(0, stream));
     // ---------------------------------------------------------------- R: pass-1 (+ filter)
     if (g.mode == MODE_GLOBAL)
         launch_build_global(dR, nR, g, d_tabs_, bitmap.as<uint32_t>(), stream);
@@ -419,13 +439,15 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     sp.cap        = capR;
     launch_scatter(sp, SRC_TUPLES, SIDE_R, G, stream);
     sp.ppool      = nullptr;
-    HWBRJ_CHECK(hipEventRecord(ev_[1], stream));
+    sp.zero_small = nullptr;
+    sp.zero_word  = nullptr;
+    HWBRJ_CHECK(mark(1, stream));
     launch_plan(wgqcR.as<uint32_t>(), wgqeR.as<uint32_t>(), G, g.log2F, wgqoR.as<uint32_t>(),
                 colR.as<uint32_t>() + 2 * F, colR.as<uint64_t>(), stream);
     launch_list_fill(metaR.as<uint32_t>(), usedR.as<uint32_t>(), capR, g.log2F, wgqoR.as<uint32_t>(),
                      colR.as<uint32_t>() + 2 * F, colR.as<uint64_t>(), (uint32_t) BSW, 1, lstartR.as<uint32_t>(),
                      estartR.as<uint64_t>(), istartR.as<uint32_t>(), listR.as<uint32_t>(), G, stream);
-    HWBRJ_CHECK(hipEventRecord(ev_[2], stream));
+    HWBRJ_CHECK(mark(2, stream));
     BuildParams bp{};
     bp.g          = g;
     bp.tabs       = d_tabs_;
@@ -472,7 +494,7 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
         launch_slice_fill(poolS.as<uint32_t>(), listS.as<uint32_t>(), lstartS.as<uint32_t>(), g,
                           slices.as<uint32_t>(), stream);
     }
-    HWBRJ_CHECK(hipEventRecord(ev_[3], stream));
+    HWBRJ_CHECK(mark(3, stream));
     // ---------------------------------------------------------------- S: pass-1 (+ probe)
     if (g.mode == MODE_GLOBAL) {
         launch_probe_global(dS, nS, g, d_tabs_, bitmap.as<uint32_t>(), dense.as<uint32_t>(),
@@ -500,13 +522,13 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     sp.ppool = mat ? ppoolS.as<uint32_t>() : nullptr;
     launch_scatter(sp, g.mode == MODE_GLOBAL ? SRC_CODES : SRC_TUPLES, SIDE_S, G, stream);
     sp.dbg = nullptr;
-    HWBRJ_CHECK(hipEventRecord(ev_[4], stream));
+    HWBRJ_CHECK(mark(4, stream));
     launch_plan(wgqcS.as<uint32_t>(), wgqeS.as<uint32_t>(), G, g.log2F, wgqoS.as<uint32_t>(),
                 colS.as<uint32_t>() + 2 * F, colS.as<uint64_t>(), stream);
     launch_list_fill(metaS.as<uint32_t>(), usedS.as<uint32_t>(), capS, g.log2F, wgqoS.as<uint32_t>(),
                      colS.as<uint32_t>() + 2 * F, colS.as<uint64_t>(), CH, nseg, lstartS.as<uint32_t>(),
                      estartS.as<uint64_t>(), istartS.as<uint32_t>(), listS.as<uint32_t>(), G, stream);
-    HWBRJ_CHECK(hipEventRecord(ev_[5], stream));
+    HWBRJ_CHECK(mark(5, stream));
     ProbeParams pp{};
     pp.g               = g;
     pp.tabs            = d_tabs_;
@@ -532,8 +554,8 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
         pp.dbg = dbgP.as<uint64_t>();
     }
     launch_probe(pp, PG, stream);
-    HWBRJ_CHECK(hipEventRecord(ev_[6], stream));
-    HWBRJ_CHECK(hipEventRecord(ev_[7], stream));  // (survivor sub-partitioning is fused into k_probe)
+    HWBRJ_CHECK(mark(6, stream));  // (survivor sub-partitioning is fused into k_probe: no ev_[7])
+    surv_fused_ = true;
     // -------------------------------------------------------------------------- join
     JoinParams jp{};
     jp.r_codes         = rjoin.as<uint32_t>();
@@ -596,6 +618,8 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     pending_      = true;
     pending_args_ = args != nullptr;
     pending_nS_   = nS;
+    pending_ev_   = phase_ev_;
+    pending_stream_ = stream;
     have_filter_  = args != nullptr;
     last_g_       = g;
 
@@ -721,16 +745,16 @@ int Engine::enqueue_basic_kk(const uint2* dR, uint64_t nR, const uint2* dS, uint
                          (r ? istartR : istartS).as<uint32_t>(), (r ? listR : listS).as<uint32_t>(), G, stream);
     };
 
-    HWBRJ_CHECK(hipEventRecord(ev_[0], stream));
+    HWBRJ_CHECK(mark(0, stream));
     // ---------------------------------------------------------------- R: the join layout
     ScatterParams sp = side(true);
     sp.g   = gj;
     sp.src = dR;
     sp.n   = nR;
     launch_scatter(sp, SRC_TUPLES, SIDE_R, G, stream);
-    HWBRJ_CHECK(hipEventRecord(ev_[1], stream));
+    HWBRJ_CHECK(mark(1, stream));
     index(true, gj.log2F, (uint32_t) BSW, 1);
-    HWBRJ_CHECK(hipEventRecord(ev_[2], stream));
+    HWBRJ_CHECK(mark(2, stream));
     BuildParams bp{};
     bp.g           = gj;
     bp.tabs        = d_tabs_;
@@ -763,16 +787,16 @@ int Engine::enqueue_basic_kk(const uint2* dR, uint64_t nR, const uint2* dS, uint
     index(false, g.log2F, (uint32_t) BSW, 1);
     launch_slice_fill(poolS.as<uint32_t>(), listS.as<uint32_t>(), lstartS.as<uint32_t>(), g,
                       slices.as<uint32_t>(), stream);
-    HWBRJ_CHECK(hipEventRecord(ev_[3], stream));
+    HWBRJ_CHECK(mark(3, stream));
     // ---------------------------------------------------------------- S: by the slice of bit 0
     sp     = side(false);
     sp.g   = g;
     sp.src = dS;
     sp.n   = nS;
     launch_scatter(sp, SRC_TUPLES, SIDE_S, G, stream);
-    HWBRJ_CHECK(hipEventRecord(ev_[4], stream));
+    HWBRJ_CHECK(mark(4, stream));
     index(false, g.log2F, CH, nseg);
-    HWBRJ_CHECK(hipEventRecord(ev_[5], stream));
+    HWBRJ_CHECK(mark(5, stream));
     // ---------------------------------------------------------------- one bit per pass
     const uint32_t PG = G;
     ProbeParams    pb{};
@@ -802,7 +826,7 @@ int Engine::enqueue_basic_kk(const uint2* dR, uint64_t nR, const uint2* dS, uint
         pb.filtered        = j + 1 < g.k ? cnt + j : d_filtered;
         launch_probe_bitj(pb, PG, stream);
     }
-    HWBRJ_CHECK(hipEventRecord(ev_[6], stream));
+    HWBRJ_CHECK(mark(6, stream));
     // ---------------------------------------------------------------- survivors: the join layout
     {
         Geometry gc = gj;
@@ -830,7 +854,8 @@ int Engine::enqueue_basic_kk(const uint2* dR, uint64_t nR, const uint2* dS, uint
     pp.job_surv        = jparts.as<uint32_t>() + NJ;
     const size_t   pl_lds = probe_lds_bytes(gj, nullptr);
     launch_probe(pp, (uint32_t) cus_ * (uint32_t) std::max<size_t>(1, std::min<size_t>(2, 163840 / pl_lds)), stream);
-    HWBRJ_CHECK(hipEventRecord(ev_[7], stream));
+    HWBRJ_CHECK(mark(7, stream));
+    surv_fused_ = false;
     // -------------------------------------------------------------------------- join
     JoinParams jp{};
     jp.r_codes         = rjoin.as<uint32_t>();
@@ -863,6 +888,8 @@ int Engine::enqueue_basic_kk(const uint2* dR, uint64_t nR, const uint2* dS, uint
     pending_      = true;
     pending_args_ = true;
     pending_nS_   = nS;
+    pending_ev_   = phase_ev_;
+    pending_stream_ = stream;
     have_filter_  = true;
     last_g_       = g;
     return 0;
@@ -893,9 +920,14 @@ int Engine::wait(hwbrj_stats_t* st) {
         st->partitions     = F;
         st->subparts       = NSUB;
         st->slice_segments = nseg;
-        float ms[9];
-        for (int i = 1; i <= 8; i++) HWBRJ_CHECK(hipEventElapsedTime(&ms[i], ev_[i - 1], ev_[i]));
-        HWBRJ_CHECK(hipEventElapsedTime(&ms[0], ev_[0], ev_[8]));
+        float ms[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+        if (pending_ev_) {  // (async joins: counts only)
+            hipEvent_t e[9];
+            for (int i = 0; i <= 8; i++) e[i] = ev_[i];
+            if (surv_fused_) e[7] = ev_[6];
+            for (int i = 1; i <= 8; i++) HWBRJ_CHECK(hipEventElapsedTime(&ms[i], e[i - 1], e[i]));
+            HWBRJ_CHECK(hipEventElapsedTime(&ms[0], e[0], e[8]));
+        }
         st->ms_total     = ms[0];
         st->ms_r_scatter = ms[1];
         st->ms_r_index   = ms[2];
@@ -960,13 +992,13 @@ int Engine::materialize(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t 
                          mcount.as<unsigned long long>(), g, slices.as<uint32_t>(),
                          bitmap.as<uint32_t>(), d_tabs_, stream);
     }
-    HWBRJ_CHECK(hipEventRecord(ev_[1], stream));
+    HWBRJ_CHECK(hipEventRecord(ev_[8], stream));
     HWBRJ_CHECK(hipGetLastError());
-    HWBRJ_CHECK(hipEventSynchronize(ev_[1]));
+    HWBRJ_CHECK(hipEventSynchronize(ev_[8]));
     HWBRJ_CHECK(hipMemcpy(n, mcount.p, 8, hipMemcpyDeviceToHost));
     if (ms) {
         float f = 0;
-        HWBRJ_CHECK(hipEventElapsedTime(&f, ev_[0], ev_[1]));
+        HWBRJ_CHECK(hipEventElapsedTime(&f, ev_[0], ev_[8]));
         *ms = f;
     }
     return 0;

@@ -106,6 +106,13 @@ class Engine {
     bool         pending_args_ = false;
     uint64_t     pending_nS_   = 0;
     uint32_t     last_nj_      = 0;  // join jobs of the last enqueue (job_surv layout)
+    // phase events: recorded by synchronous joins only (run_async clears phase_ev_); surv_fused_:
+    // the pending join's survivor phase is fused into its probe (no ev_[7] of its own)
+    bool         phase_ev_     = true;
+    bool         pending_ev_   = true;
+    hipStream_t  pending_stream_ = nullptr;  // the stream the pending join was enqueued on
+    bool         surv_fused_   = false;
+    hipError_t   mark(int i, hipStream_t stream);  // ev_[i] when phase_ev_
     bool         alloc_only_   = false;  // reserve(): enqueue returns after its allocations
     int          enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
                          const bloom_filter_args_t* args, hipStream_t stream, bool dbg, int jkind,

@@ -27,6 +27,10 @@ struct ScatterParams {
     const uint32_t*  seg_cnt;      // SRC_CODES from per-workgroup segments: workgroup w partitions
     uint64_t         seg_stride;   // src + w * seg_stride (elements), seg_cnt[w] of them; or nullptr
     uint64_t         vn;           // MODE_BASIC_POS: tuples of src (n = k * vn elements, k <= grid)
+    // the join's per-call zeroing, done by workgroup 0 instead of memset dispatches: zero_small[0, 16)
+    // (counts) and *zero_word (the join's extra-task count), each when not nullptr
+    uint32_t*        zero_small;
+    uint32_t*        zero_word;
     Geometry         g;
     const CrcTables* tabs;
 };

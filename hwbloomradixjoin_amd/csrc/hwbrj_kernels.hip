@@ -572,6 +572,8 @@ __device__ __forceinline__ void scatter_body(const ScatterParams& P) {
         crc_tab[tid] = v;
     }
     if (tid < 8) misc[tid] = 0;
+    if (blockIdx.x == 0 && P.zero_small && tid < 16) P.zero_small[tid] = 0;
+    if (blockIdx.x == 0 && P.zero_word && tid == 0) *P.zero_word = 0;
 
     if (P.dbg && tid == 0) P.dbg[blockIdx.x * 8 + 6] = __builtin_amdgcn_s_memrealtime();  // dev-only: start
     const uint64_t n     = P.n_dev ? *P.n_dev : P.n;
@@ -986,6 +988,8 @@ __device__ __forceinline__ void scatter_body_pay(const ScatterParams& P) {
         crc_tab[tid] = v;
     }
     if (tid < 8) misc[tid] = 0;
+    if (blockIdx.x == 0 && P.zero_small && tid < 16) P.zero_small[tid] = 0;  // (as scatter_body)
+    if (blockIdx.x == 0 && P.zero_word && tid == 0) *P.zero_word = 0;
 
     const uint64_t n     = P.n;
     const uint64_t units = (n + 3) >> 2;

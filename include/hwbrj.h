@@ -130,7 +130,9 @@ int hwbrj_join_device_algo(const tuple_t * d_R, uint64_t nR, const tuple_t * d_S
                            hwbrj_stats_t * stats);
 /* The same join, enqueued on `stream` without waiting (back-to-back joins then run without host
  * gaps); the inputs must stay valid until it completes. hwbrj_join_wait() waits for the last join
- * enqueued on this device and fills stats (counts and phase times of that join). */
+ * enqueued on this device and fills stats with its counts. An async join records no phase events
+ * (each would idle the GPU between the kernels around it), so its ms_* fields are 0; the
+ * synchronous entry points measure the phases. */
 int hwbrj_join_device_async(const tuple_t * d_R, uint64_t nR, const tuple_t * d_S, uint64_t nS,
                             const bloom_filter_args_t * args, void * stream);
 int hwbrj_join_wait(hwbrj_stats_t * stats);

@@ -255,7 +255,9 @@ def test_repeatable_and_buffer_reuse(hw, cuda, f3):
 
 
 def test_async_joins_back_to_back(hw, cuda, f3):
-    """hwbrj_join_device_async x3 then hwbrj_join_wait: the last join's counts are the golden's."""
+    """hwbrj_join_device_async x3 then hwbrj_join_wait: the last join's counts are the golden's.
+    Async joins record no phase events (counts only); a synchronous join after them measures its
+    phases again."""
     g = GOLD["F3_grid"]
     R, S = f3
     args = hw.BloomFilterArgs(hw.BLOCKED, g["m"], 1, 1024)
@@ -263,7 +265,13 @@ def test_async_joins_back_to_back(hw, cuda, f3):
         hw.join_device_async(R, S, args)
     st = hw.join_wait()
     assert (st.filtered, st.matches) == (g["rows"]["1024"][0], g["results"])
-    assert st.ms_total > 0
+    assert st.ms_total == 0 and st.ms_probe == 0
+    st = hw.join_device(R, S, args)
+    assert (st.filtered, st.matches) == (g["rows"]["1024"][0], g["results"])
+    assert st.ms_total > 0 and st.ms_probe > 0 and st.ms_s_scatter > 0
+    assert st.ms_surv == 0  # (fused into the probe: no boundary of its own)
+    parts = st.ms_r_scatter + st.ms_r_index + st.ms_build + st.ms_s_scatter + st.ms_s_index + st.ms_probe + st.ms_join
+    assert abs(parts - st.ms_total) <= 1e-3 * st.ms_total + 1e-3
 
 
 def test_generate_device_matches_host(hw, cuda):
