@@ -1209,12 +1209,34 @@ __device__ __forceinline__ void scatter_body_pay(const ScatterParams& P) {
 
 // ====================================================== K4: planning scan and chunk lists
 // List entries carry the chunk's element count, so consumers never read `meta`:
-//   entry = chunk_id | (count & 31) << kListIdBits   (count 32 is stored as 0)
+//   entry = chunk_id | (count - 1) << kListIdBits   (count 1..32)
 constexpr uint32_t kListIdBits = 27;
 constexpr uint32_t kListIdMask = (1u << kListIdBits) - 1u;
 constexpr uint32_t kNoEntry    = 0xFFFFFFFFu;
 
-__device__ __forceinline__ uint32_t list_count(uint32_t e) { return (((e >> kListIdBits) - 1u) & 31u) + 1u; }
+__device__ __forceinline__ uint32_t list_count(uint32_t e) { return (e >> kListIdBits) + 1u; }
+
+// LDS byte addresses as integers (address arithmetic the compiler cannot fold into a select)
+typedef __attribute__((address_space(3))) uint32_t lds_u32_t;
+__device__ __forceinline__ uint32_t lds_byte_addr(const uint32_t* p) {
+    return (uint32_t) (uintptr_t) (const lds_u32_t*) p;
+}
+__device__ __forceinline__ void lds_store_u32(uint32_t byte_addr, uint32_t v) {
+    *(lds_u32_t*) (uintptr_t) byte_addr = v;
+}
+// a * b + c for a, b < 2^24 (v_mad_u32_u24): the caller guarantees the ranges, which the compiler
+// cannot see (it would mask the operands or fall back to v_mul_lo_u32)
+__device__ __forceinline__ uint32_t mad_u24(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t r;
+    asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+// (a << s) + b as one v_lshl_add_u32 (keeps a running sum the compiler would re-derive per use)
+__device__ __forceinline__ uint32_t shl_add(uint32_t a, uint32_t s, uint32_t b) {
+    uint32_t r;
+    asm("v_lshl_add_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "i"(s), "v"(b));
+    return r;
+}
 
 // Column-wise exclusive scan of the scatter's (workgroup x partition) matrices: every (wg, q) gets
 // its offset inside q's chunk list, and every partition its chunk / element totals. A block takes
@@ -1372,7 +1394,7 @@ __global__ __launch_bounds__(kLfThreads) void k_list_fill(const uint32_t* __rest
             if (m[j] == kNoEntry) continue;
             const uint32_t q   = m[j] & 0xFFFFu;
             const uint32_t pos = off[q] + rk[j];
-            ids[pos] = (uint32_t) (region + b0 + tid + j * kLfThreads) | (((m[j] >> 16) & 31u) << kListIdBits);
+            ids[pos] = (uint32_t) (region + b0 + tid + j * kLfThreads) | ((((m[j] >> 16) - 1u) & 31u) << kListIdBits);
             qs[pos]  = (uint16_t) q;
         }
         __syncthreads();
@@ -1450,9 +1472,9 @@ __device__ __forceinline__ void load_chunks_u(const uint32_t* __restrict__ pool,
             __builtin_memcpy(&S.v[j], &pool[(uint64_t) (ent[j] & kListIdMask) * 22 + c22_load_dword(l8)], 16);
         else
             S.v[j] = *(const uint4*) &pool[(uint64_t) (ent[j] & kListIdMask) * 32 + l8 * 4];
-        const uint32_t cnt   = lb + cslot + (uint32_t) j * 128u < le ? list_count(ent[j]) : 0u;
-        const uint32_t first = l8 * 4;
-        S.n[j]  = cnt > first ? min(cnt - first, 4u) : 0u;
+        // valid words of this thread's quad: clamp(count - 4 * l8, 0, 4), 0 past le
+        const int32_t  d     = (int32_t) (ent[j] >> kListIdBits) + 1 - (int32_t) (l8 * 4);
+        S.n[j]  = lb + cslot + (uint32_t) j * 128u < le ? (uint32_t) min(max(d, 0), 4) : 0u;
         S.id[j] = ent[j] & kListIdMask;
     }
 }
@@ -1665,9 +1687,11 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
     uint32_t*       subow  = subc + 3 * 128;  // 16 waves x NSUB: each wave's copy of the offsets
     constexpr uint32_t kScrCap = scr_cap<KIND>();
     constexpr int      kDense  = kScrCap / 64 > 0 ? kScrCap / 64 : 1;
-    uint32_t*       scratch = subow + 16 * NSUB;  // 16 waves x kScrCap: compacted survivors (not PAY)
-    uint32_t*       scrdum = scratch + (PAY ? 0u : 16 * kScrCap);  // 64 dummy slots shared by all waves
-    uint32_t*       stage  = scrdum + 64;             // 2 x sstr, double-buffered by item
+    // 64 garbage slots shared by all waves, below the scratch (the compaction's address arithmetic
+    // needs scratch slots above them)
+    uint32_t*       scrdum  = subow + 16 * NSUB;
+    uint32_t*       scratch = scrdum + 64;            // 16 waves x kScrCap: compacted survivors (not PAY)
+    uint32_t*       stage  = scratch + (PAY ? 0u : 16 * kScrCap);  // 2 x sstr, double-buffered by item
     const uint32_t  hp     = scap / 2;                // PAY: codes at [0, hp), positions at [hp, scap)
     const int       tid    = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     load_tab(inv, &P.tabs->inv[0][0]);
@@ -1811,9 +1835,9 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
                 if (pk) {  // bit = one bfe at the word's low 5 bits; the chunk quads' fill as one mask each
 #pragma unroll
                     for (int i = 0; i < NW; i++) pass |= __builtin_amdgcn_ubfe(wv[i], bb[i], 1u) << i;
-                    uint32_t vm = 0;
+                    uint32_t vm = 0;  // valid words: (1 << n) - 1 per quad, by one bfe each
 #pragma unroll
-                    for (int j = 0; j < kPC; j++) vm |= ((1u << Sc.n[j]) - 1u) << (4 * j);
+                    for (int j = 0; j < kPC; j++) vm |= __builtin_amdgcn_ubfe(0xFu, 0u, Sc.n[j]) << (4 * j);
                     pass &= vm;
                 } else {
 #pragma unroll
@@ -1843,14 +1867,17 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
                         at0 += (uint32_t) __builtin_popcountll(m);
                     }
 #else
-                    // lane-major: this lane's survivors at its exclusive prefix (the scan above) plus
-                    // their rank among its own (one v_bcnt with the base as addend)
-                    const uint32_t pbase = pinc - pcnt;
+                    // lane-major: this lane's survivors from its exclusive prefix (the scan above) on.
+                    // Word i goes to byte address dmy + t_i * x (t_i its pass bit, x = the next
+                    // survivor slot - dmy, dmy the lane's garbage slot below the scratch): one bfe,
+                    // one mad_u24 and one shift-add per word
+                    const uint32_t dmy = lds_byte_addr(&scrdum[lane]);
+                    uint32_t       x   = lds_byte_addr(&scr[pinc - pcnt]) - dmy;
 #pragma unroll
                     for (int i = 0; i < NW; i++) {
-                        const bool     ok = (pass >> i) & 1u;
-                        const uint32_t r  = pbase + (uint32_t) __builtin_popcount(pass & ((1u << i) - 1u));
-                        *(ok ? &scr[r] : &scrdum[lane]) = sweep_word(Sc, i >> 2, i & 3);  // others: garbage slot
+                        const uint32_t t = __builtin_amdgcn_ubfe(pass, (uint32_t) i, 1u);
+                        lds_store_u32(mad_u24(t, x, dmy), sweep_word(Sc, i >> 2, i & 3));
+                        x = shl_add(t, 2, x);
                     }
 #endif
                 }
