@@ -374,6 +374,9 @@ constexpr int      kScThreads = 1024;
 #ifndef HWBRJ_SC_SAUX
 #define HWBRJ_SC_SAUX 2  // cache policy of the chunk stores: nt (16 = sc1 measured slower)
 #endif
+#ifndef HWBRJ_SC_SAUX_R
+#define HWBRJ_SC_SAUX_R HWBRJ_SC_SAUX  // (the R scatter's, A/B)
+#endif
 constexpr int      kScPre     = HWBRJ_SC_PRE;             // rounds of loads in flight (1 or 2)
 constexpr int      kScE       = HWBRJ_SC_E;                        // elements per thread per round
 constexpr uint32_t kScRound   = kScThreads * kScE;        // elements per workgroup round
@@ -547,7 +550,7 @@ struct ScRaw {  // one round's raw loads of this thread (tuples: keys only; code
 
 // LDS: static CRC nibble table (512 B, at 0, so its row offsets are immediates); dynamic (words):
 // stage F x 32 | 64 dummy slots | fill F + 4 | ncb 2F | flq F | misc 8 (per-partition totals: registers of the plan thread)
-template <int SRC, int MODE, int FMT>
+template <int SRC, int MODE, int FMT, int SAUX = HWBRJ_SC_SAUX>
 __device__ __forceinline__ void scatter_body(const ScatterParams& P) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     __shared__ uint32_t crc_tab[128];
@@ -693,7 +696,7 @@ __device__ __forceinline__ void scatter_body(const ScatterParams& P) {
 #ifdef HWBRJ_ABL_NOSTORE
             if (v.x == 0x12345678u && v.y == 0x9abcdef0u)  // dev ablation: practically never stores
 #endif
-            __builtin_amdgcn_raw_buffer_store_b128(v, rpool, ok ? (cb * 32 + l8 * 4) * 4 : kOob, 0, HWBRJ_SC_SAUX);
+            __builtin_amdgcn_raw_buffer_store_b128(v, rpool, ok ? (cb * 32 + l8 * 4) * 4 : kOob, 0, SAUX);
             }
             __builtin_amdgcn_raw_buffer_store_b32(qq | (32u << 16), rmeta, ok && l8 == 0 ? cb * 4 : kOob, 0, 0);
         };
@@ -3593,7 +3596,7 @@ void launch_copy_bw(const void* src, void* dst, uint64_t bytes, int grid, hipStr
 }
 
 template <int SRC, int MODE, int FMT>
-__global__ __launch_bounds__(kScThreads) void k_scatter_r(ScatterParams P) { scatter_body<SRC, MODE, FMT>(P); }
+__global__ __launch_bounds__(kScThreads) void k_scatter_r(ScatterParams P) { scatter_body<SRC, MODE, FMT, HWBRJ_SC_SAUX_R>(P); }
 template <int SRC, int MODE, int FMT>
 __global__ __launch_bounds__(kScThreads) void k_scatter_s(ScatterParams P) { scatter_body<SRC, MODE, FMT>(P); }
 
