@@ -3,7 +3,7 @@
     python tools/prof_summary.py <trace_dir> <pmc_fetch_dir> <pmc_write_dir> <out.json> [config...]
 
 Kernel-trace: per-dispatch durations of the last join of the run. PMC: FETCH_SIZE and WRITE_SIZE
-(KiB per dispatch) from two separate --pmc passes; on gfx950 FETCH_SIZE reports half the bytes of
+(KiB per dispatch; printed below as KiB x 1024 / 1e9 = GB) from two separate --pmc passes; on gfx950 FETCH_SIZE reports half the bytes of
 wide coalesced reads (MI355X_MICROARCH.md, HBM), so hbm_bytes = (2*FETCH_SIZE + WRITE_SIZE)*1024.
 Infinity-Cache hits are included in these counters.
 """
@@ -15,7 +15,7 @@ from collections import defaultdict
 
 # dispatch order of one join (hwbrj_engine.cpp Engine::run) -> phase
 PHASE_OF = {"k_build_global": "build", "k_build": "build", "k_probe_global": "probe",
-            "k_probe": "probe", "k_join_split": "join", "k_join": "join", "k_plan": "index",
+            "k_probe": "probe", "k_join_split": "join", "k_join": "join", "k_join_sum": "join", "k_plan": "index",
             "k_list_fill": "index", "k_mat_build": "materialize", "k_mat_probe": "materialize"}
 
 
@@ -27,9 +27,13 @@ def one(path_glob):
 
 
 def last_join(names):
-    """Indices of the dispatches of the last join (from the last R scatter on)."""
+    """Indices of the dispatches of the last join: from the last R scatter to the join's final
+    count reduction (k_join_sum), so kernels the bench runs after the joins (its copy-rate
+    measurement) are not counted."""
     sc = [i for i, n in enumerate(names) if n == "k_scatter_r"]
-    return list(range(sc[-1] if sc else 0, len(names)))
+    b = sc[-1] if sc else 0
+    end = next((i for i in range(b, len(names)) if names[i] == "k_join_sum"), len(names) - 1)
+    return list(range(b, end + 1))
 
 
 def label(names, idx):
