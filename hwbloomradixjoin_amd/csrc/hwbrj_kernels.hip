@@ -357,7 +357,12 @@ __global__ __launch_bounds__(1024) void k_probe_global(const uint2* S, uint64_t 
 // line, further ones (only when a round overfills a partition by > 32, i.e. skew) are written
 // directly by the threads holding those overflow words. Chunk metadata = partition | count << 16.
 // (Reference pass-1: src/parallel_radix_join_bloom.c:758-852, SWWC variant :611-700.)
-constexpr int      kScThreads = 1024;
+#ifndef HWBRJ_SC_T
+#define HWBRJ_SC_T 1024  // threads per scatter workgroup (A/B: 512)
+#endif
+constexpr int      kScThreads = HWBRJ_SC_T;
+constexpr int      kScPlanPer = (1024 + kScThreads - 1) / kScThreads;  // partitions per plan thread (F <= 1024)
+constexpr int      kScPayThreads = 1024;  // the materializing scatter (scatter_body_pay)
 #ifndef HWBRJ_SC_E
 #define HWBRJ_SC_E 8
 #define HWBRJ_SC_K 2
@@ -564,7 +569,10 @@ __device__ __forceinline__ void scatter_body(const ScatterParams& P) {
     const int      tid   = threadIdx.x, lane = tid & 63;
     const uint32_t dummy = F * 32 + lane;        // stage index of this lane's dummy slot
     for (uint32_t i = tid; i < F + 1; i += kScThreads) fill[i] = 0;
-    uint32_t my_tch = 0, my_tel = 0;  // chunks / elements of partition tid (its plan thread) here
+    // chunks / elements of partitions tid + i * kScThreads (their plan thread) here
+    uint32_t my_tch[kScPlanPer], my_tel[kScPlanPer];
+#pragma unroll
+    for (int i = 0; i < kScPlanPer; i++) my_tch[i] = my_tel[i] = 0;
     if (tid < 128) {  // nibble table; f(kSeed) folded into row 0
         const uint32_t* src = &P.tabs->fwd[0][0];
         uint32_t        v   = src[tid];
@@ -840,9 +848,10 @@ __device__ __forceinline__ void scatter_body(const ScatterParams& P) {
             pw[j] = w[j];
         }
         pskew = skew;
-        {
+#pragma unroll
+        for (int pp = 0; pp < kScPlanPer; pp++) {
             // one thread per partition (F <= 1024): flush plan
-            const uint32_t qq  = tid;
+            const uint32_t qq  = tid + pp * kScThreads;
             const uint32_t f   = qq < F ? fill[qq] : 0u;
             const uint32_t nch = f >> 5;
             // wave prefix of (chunks, flushes); one LDS atomic per wave for the bases
@@ -861,8 +870,8 @@ __device__ __forceinline__ void scatter_body(const ScatterParams& P) {
                 ncb[par * F + qq] = cb | (nch << kCbBits);
                 flq[wbf + (incl >> 16) - 1] = qq;
                 fill[qq]          = f & 31u;
-                my_tch += nch;
-                my_tel += nch * 32;
+                my_tch[pp] += nch;
+                my_tel[pp] += nch * 32;
                 for (uint32_t c = 1; c < nch; c++) {  // direct chunks
                     meta[cb + c] = qq | (32u << 16);
                     if (FMT == FMT_C22)  // filled by atomic adds after the next barriers
@@ -891,8 +900,9 @@ __device__ __forceinline__ void scatter_body(const ScatterParams& P) {
         __syncthreads();
         write_pending();
         __syncthreads();
-        {  // one thread per partition (F <= 1024): chunk ids of the partial stages (wave scan)
-            const uint32_t qq   = tid;
+#pragma unroll
+        for (int pp = 0; pp < kScPlanPer; pp++) {  // one thread per partition (F <= 1024): chunk ids of the partial stages (wave scan)
+            const uint32_t qq   = tid + pp * kScThreads;
             const uint32_t f    = qq < F ? fill[qq] : 0u;
             const uint32_t has  = f > 0 ? 1u : 0u;
             const uint32_t incl = wave_incl_scan_dpp(has);
@@ -904,8 +914,8 @@ __device__ __forceinline__ void scatter_body(const ScatterParams& P) {
                 const uint32_t cb = wb + incl - 1u;
                 ncb[qq]  = cb;
                 meta[cb] = qq | (f << 16);
-                my_tch += 1;
-                my_tel += f;
+                my_tch[pp] += 1;
+                my_tel[pp] += f;
             }
         }
         __syncthreads();
@@ -932,9 +942,13 @@ __device__ __forceinline__ void scatter_body(const ScatterParams& P) {
         }
         // this workgroup's row of the (workgroup x partition) chunk / element matrices (k_plan
         // scans them column-wise: no global atomics)
-        if ((uint32_t) tid < F) {
-            P.wgq_chunks[wg * F + tid] = my_tch;
-            P.wgq_elems[wg * F + tid]  = my_tel;
+#pragma unroll
+        for (int pp = 0; pp < kScPlanPer; pp++) {
+            const uint32_t qq = tid + pp * kScThreads;
+            if (qq < F) {
+                P.wgq_chunks[wg * F + qq] = my_tch[pp];
+                P.wgq_elems[wg * F + qq]  = my_tel[pp];
+            }
         }
     }
 }
@@ -976,8 +990,8 @@ __device__ __forceinline__ void scatter_body_pay(const ScatterParams& P) {
     uint32_t*      misc  = flq + F;             // [0] chunks used, [1 + parity] flushes, [3 + parity] skew
     const int      tid   = threadIdx.x, lane = tid & 63;
     const uint32_t dummy = F * kPayDepth + lane;
-    for (uint32_t i = tid; i < F + 1; i += kScThreads) fill[i] = 0;
-    for (uint32_t i = tid; i < F; i += kScThreads) {
+    for (uint32_t i = tid; i < F + 1; i += kScPayThreads) fill[i] = 0;
+    for (uint32_t i = tid; i < F; i += kScPayThreads) {
         cst[i] = 0;
         tel[i] = 0;
     }
@@ -1017,11 +1031,11 @@ __device__ __forceinline__ void scatter_body_pay(const ScatterParams& P) {
         if (base + kScRound <= len) {
 #pragma unroll
             for (int j = 0; j < kScE; j++)
-                R[j] = __builtin_amdgcn_raw_buffer_load_b64(rsrc, tid * 8, (base + j * kScThreads) * 8, 0);
+                R[j] = __builtin_amdgcn_raw_buffer_load_b64(rsrc, tid * 8, (base + j * kScPayThreads) * 8, 0);
         } else {
 #pragma unroll
             for (int j = 0; j < kScE; j++) {
-                const uint32_t i = base + j * kScThreads + tid;
+                const uint32_t i = base + j * kScPayThreads + tid;
                 R[j] = __builtin_amdgcn_raw_buffer_load_b64(rsrc, i < len ? i * 8 : kOob, 0, 0);
             }
         }
@@ -1049,8 +1063,8 @@ __device__ __forceinline__ void scatter_body_pay(const ScatterParams& P) {
             __builtin_amdgcn_raw_buffer_store_b32(qq | (32u << 16), rmeta, ok && l4 == 0 && (H & 1u) ? (H >> 1) * 4 : kOob, 0, 0);
         };
 #pragma unroll
-        for (int i = 0; i < kScKP; i++) task(tid + i * kScThreads);
-        for (uint32_t k = kScKP * kScThreads + tid; k < nf * 4; k += kScThreads) task(k);  // rare
+        for (int i = 0; i < kScKP; i++) task(tid + i * kScPayThreads);
+        for (uint32_t k = kScKP * kScPayThreads + tid; k < nf * 4; k += kScPayThreads) task(k);  // rare
     };
     // previous round's pending words: q | slot << 11 (kNoPend: none); resolved into a stage index
     // (ps) or, in a skewed round, written directly into the plan's further halves
@@ -1099,7 +1113,7 @@ __device__ __forceinline__ void scatter_body_pay(const ScatterParams& P) {
         if (!full) {
 #pragma unroll
             for (int j = 0; j < kScE; j++)
-                if (base + j * kScThreads + tid >= len) q[j] = F;  // invalid: ranked on the dummy counter
+                if (base + j * kScPayThreads + tid >= len) q[j] = F;  // invalid: ranked on the dummy counter
         }
         load_round(base + kScRound, RA);
         flush_copy();
@@ -1190,7 +1204,7 @@ __device__ __forceinline__ void scatter_body_pay(const ScatterParams& P) {
             }
         }
         __syncthreads();
-        for (uint32_t k = tid; k < F * 4; k += kScThreads) {
+        for (uint32_t k = tid; k < F * 4; k += kScPayThreads) {
             const uint32_t qq = k >> 2, l4 = k & 3;
             const uint32_t o  = fill[qq] > 0 ? (hword(pl0[qq]) + l4 * 4) * 4 : kOob;
             const v4u      x0 = *(const v4u*) &stg[qq * kPayDepth + l4 * 4];
@@ -1203,7 +1217,7 @@ __device__ __forceinline__ void scatter_body_pay(const ScatterParams& P) {
         }
         __syncthreads();
         if (tid == 0) P.wg_used[wg] = misc[0];
-        for (uint32_t qq = tid; qq < F; qq += kScThreads) {
+        for (uint32_t qq = tid; qq < F; qq += kScPayThreads) {
             P.wgq_chunks[wg * F + qq] = (tel[qq] + 31u) >> 5;
             P.wgq_elems[wg * F + qq]  = tel[qq];
         }
@@ -3615,17 +3629,17 @@ size_t scatter_pay_lds_bytes(uint32_t log2F) {
 }
 
 template <int MODE, int FMT>
-__global__ __launch_bounds__(kScThreads) void k_scatter_rp(ScatterParams P) { scatter_body_pay<MODE, FMT>(P); }
+__global__ __launch_bounds__(kScPayThreads) void k_scatter_rp(ScatterParams P) { scatter_body_pay<MODE, FMT>(P); }
 template <int MODE, int FMT>
-__global__ __launch_bounds__(kScThreads) void k_scatter_sp(ScatterParams P) { scatter_body_pay<MODE, FMT>(P); }
+__global__ __launch_bounds__(kScPayThreads) void k_scatter_sp(ScatterParams P) { scatter_body_pay<MODE, FMT>(P); }
 
 template <int MODE, int FMT>
 static void scatter_pay_inst(const ScatterParams& p, int side, uint32_t grid, hipStream_t st) {
     const size_t lds = scatter_pay_lds_bytes(p.g.log2F);
     const void*  fn  = side == SIDE_R ? (const void*) &k_scatter_rp<MODE, FMT> : (const void*) &k_scatter_sp<MODE, FMT>;
     (void) hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds);
-    if (side == SIDE_R) k_scatter_rp<MODE, FMT><<<grid, kScThreads, lds, st>>>(p);
-    else k_scatter_sp<MODE, FMT><<<grid, kScThreads, lds, st>>>(p);
+    if (side == SIDE_R) k_scatter_rp<MODE, FMT><<<grid, kScPayThreads, lds, st>>>(p);
+    else k_scatter_sp<MODE, FMT><<<grid, kScPayThreads, lds, st>>>(p);
 }
 
 void launch_scatter(const ScatterParams& p, int src, int side, uint32_t grid, hipStream_t st) {

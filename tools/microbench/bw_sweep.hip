@@ -65,6 +65,37 @@ __global__ void k_bw(const v4u* __restrict__ in, void* __restrict__ out, uint64_
     if (KIND == 2 && acc == 0x12345678u) sink[0] = acc;
 }
 
+// rw21 software-pipelined: the next step's U loads are issued before this step's stores (the
+// scatter's shape: loads one round ahead), each workgroup its own contiguous range
+template <int U, bool NT>
+__global__ void k_rw_pipe(const v4u* __restrict__ in, v2u* __restrict__ out, uint64_t n) {
+    const uint64_t T = blockDim.x, per = (n + gridDim.x - 1) / gridDim.x;
+    const uint64_t b = (uint64_t) blockIdx.x * per, e = min(n, b + per);
+    v4u cur[U], nxt[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const uint64_t k = b + threadIdx.x + (uint64_t) u * T;
+        cur[u] = k < e ? ld<NT>(in + k) : v4u{0, 0, 0, 0};
+    }
+    for (uint64_t i = b + threadIdx.x; i < e; i += T * U) {
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const uint64_t k = i + T * U + (uint64_t) u * T;
+            nxt[u] = k < e ? ld<NT>(in + k) : v4u{0, 0, 0, 0};
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const uint64_t k = i + (uint64_t) u * T;
+            if (k < e) st<NT>(out + k, v2u{cur[u].x ^ 0x9e3779b9u, cur[u].z});
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) cur[u] = nxt[u];
+    }
+}
+
+template <int U, bool NT>
+static void run_pipe(const v4u* in, void* out, uint64_t n, int grid, int thr);
+
 template <class L>
 static float timeit(L launch, int reps = 5) {
     hipEvent_t a, b;
@@ -93,6 +124,14 @@ static void run(const v4u* in, void* out, uint64_t n, uint32_t* sink, int grid, 
     fflush(stdout);
 }
 
+template <int U, bool NT>
+static void run_pipe(const v4u* in, void* out, uint64_t n, int grid, int thr) {
+    const float ms = timeit([&] { k_rw_pipe<U, NT><<<grid, thr>>>(in, (v2u*) out, n); });
+    printf("rw21 P U=%d %-3s grid=%5d x %4d  %7.3f ms  %7.1f GB/s (pipelined: next loads before stores)\n", U,
+           NT ? "nt" : "def", grid, thr, ms, (n * 24.0) / ms / 1e6);
+    fflush(stdout);
+}
+
 template <int KIND>
 static void sweep(const v4u* in, void* out, uint64_t n, uint32_t* sink) {
     const int cfg[][2] = {{256, 1024}, {512, 1024}, {1024, 256}, {2048, 256}, {4096, 256}, {8192, 256}};
@@ -110,7 +149,8 @@ static void sweep(const v4u* in, void* out, uint64_t n, uint32_t* sink) {
     run<KIND, 1, true, true>(in, out, n, sink, 16384, 256);
 }
 
-int main() {
+int main(int argc, char** argv) {
+    (void) argv;
     const uint64_t bytes = 4ull << 30, n = bytes / 16;
     v4u*      in;
     void*     out;
@@ -120,6 +160,20 @@ int main() {
     CK(hipMalloc(&sink, 4));
     CK(hipMemset(in, 1, bytes));
     CK(hipMemset(out, 2, bytes));
+    if (argc > 1) {  // pipelined rw21 only
+        for (int r = 0; r < 2; r++) {
+            run<1, 4, true, false>(in, out, n, sink, 256, 1024);
+            run<1, 4, true, false>(in, out, n, sink, 512, 1024);
+            run_pipe<2, true>(in, out, n, 256, 1024);
+            run_pipe<4, true>(in, out, n, 256, 1024);
+            run_pipe<4, false>(in, out, n, 256, 1024);
+            run_pipe<8, true>(in, out, n, 256, 1024);
+            run_pipe<4, true>(in, out, n, 512, 1024);
+            run_pipe<2, true>(in, out, n, 256, 512);
+        }
+        printf("done\n");
+        return 0;
+    }
     sweep<0>(in, out, n, sink);
     sweep<1>(in, out, n, sink);
     sweep<2>(in, out, n, sink);
