@@ -1479,7 +1479,8 @@ __device__ __forceinline__ void load_list_u(const uint32_t* __restrict__ list, u
     for (int j = 0; j < NPQ; j++) ent[j] = list[min(lb + cslot + (uint32_t) j * 128u, le - 1u)];
 }
 
-template <int NPQ, bool C22 = false>
+// NT: non-temporal chunk loads (the chunks are read once)
+template <int NPQ, bool C22 = false, bool NT = false>
 __device__ __forceinline__ void load_chunks_u(const uint32_t* __restrict__ pool, const uint32_t (&ent)[NPQ],
                                               uint32_t lb, uint32_t le, Sweep<NPQ>& S) {
     const uint32_t l8 = threadIdx.x & 7, cslot = threadIdx.x >> 3;
@@ -1487,7 +1488,10 @@ __device__ __forceinline__ void load_chunks_u(const uint32_t* __restrict__ pool,
     for (int j = 0; j < NPQ; j++) {
         if (C22)  // 16 bytes at a dword-aligned offset of the 88-byte chunk (c22_unpack decodes them)
             __builtin_memcpy(&S.v[j], &pool[(uint64_t) (ent[j] & kListIdMask) * 22 + c22_load_dword(l8)], 16);
-        else
+        else if (NT) {
+            const v4u v = __builtin_nontemporal_load((const v4u*) &pool[(uint64_t) (ent[j] & kListIdMask) * 32 + l8 * 4]);
+            S.v[j]      = make_uint4(v.x, v.y, v.z, v.w);
+        } else
             S.v[j] = *(const uint4*) &pool[(uint64_t) (ent[j] & kListIdMask) * 32 + l8 * 4];
         // valid words of this thread's quad: clamp(count - 4 * l8, 0, 4), 0 past le
         const int32_t  d     = (int32_t) (ent[j] >> kListIdBits) + 1 - (int32_t) (l8 * 4);
@@ -1516,6 +1520,10 @@ __device__ __forceinline__ uint32_t sweep_word(const Sweep<NPQ>& S, int j, int t
 #define HWBRJ_BPQ 2
 #endif
 constexpr int      kBPQ    = HWBRJ_BPQ;       // sweeps per group (chunk quads per thread)
+#ifndef HWBRJ_BD_NT
+#define HWBRJ_BD_NT 0
+#endif
+constexpr bool     kBdNT   = HWBRJ_BD_NT != 0;  // non-temporal chunk loads in the build
 constexpr uint32_t kBSweep = 128u;            // chunks per sweep (8 threads per chunk)
 constexpr uint32_t kBSlot  = kBSweep * 32u;   // out_codes words per sweep (4096)
 
@@ -1551,14 +1559,14 @@ __global__ __launch_bounds__(1024) void k_build(BuildParams P) {
         Sweep<kBPQ> SA, SB, PA, PB;  // words; payloads (PAY)
         if (l0 < l1) {
             load_list_u<kBPQ>(P.list, l0, l1, eA);
-            load_chunks_u<kBPQ>(P.pool, eA, l0, l1, SA);
+            load_chunks_u<kBPQ, false, kBdNT>(P.pool, eA, l0, l1, SA);
             if (PAY) load_chunks_u<kBPQ>(P.ppool, eA, l0, l1, PA);
         }
         for (uint32_t lb = l0; lb < l1; lb += GRP) {
             const uint32_t nb = min(lb + GRP, l1 - 1u);  // next group (re-reads the last entry past the end)
             const uint32_t ne = min(nb + GRP, l1);
             load_list_u<kBPQ>(P.list, nb, ne, eB);
-            load_chunks_u<kBPQ>(P.pool, eB, nb, ne, SB);
+            load_chunks_u<kBPQ, false, kBdNT>(P.pool, eB, nb, ne, SB);
             if (PAY) load_chunks_u<kBPQ>(P.ppool, eB, nb, ne, PB);
 #pragma unroll
             for (int jj = 0; jj < kBPQ; jj++) {
@@ -1654,6 +1662,10 @@ __global__ __launch_bounds__(1024) void k_build(BuildParams P) {
 #define HWBRJ_SCR1 128
 #endif
 constexpr int      kPC      = HWBRJ_PC;       // chunk quads per thread per item
+#ifndef HWBRJ_PR_NT
+#define HWBRJ_PR_NT 0
+#endif
+constexpr bool     kPrNT    = HWBRJ_PR_NT != 0;  // non-temporal chunk loads in the probe
 constexpr uint32_t kProbeCH = 128u * kPC;     // chunks per probe item (1024 threads, 8 per chunk)
 // compacted survivors (first-bit candidates for KIND_BLOCK_PKK, whose rate is higher) per wave
 // and item in the LDS scratch, and the dense ranking rounds per wave
@@ -1797,8 +1809,8 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
             load_list_u<kPC>(P.list, lb_of(p0), le_of(p0), eA);
             load_list_u<kPC>(P.list, lb_of(pa), le_of(pa), eB);
             load_list_u<kPC>(P.list, lb_of(pb), le_of(pb), eC);
-            load_chunks_u<kPC, zfmt>(P.pool, eA, lb_of(p0), le_of(p0), SA);
-            load_chunks_u<kPC, zfmt>(P.pool, eB, lb_of(pa), le_of(pa), SB);
+            load_chunks_u<kPC, zfmt, kPrNT>(P.pool, eA, lb_of(p0), le_of(p0), SA);
+            load_chunks_u<kPC, zfmt, kPrNT>(P.pool, eB, lb_of(pa), le_of(pa), SB);
         }
         if (slices) {
             __syncthreads();  // every wave is done with the previous slice
@@ -1812,7 +1824,7 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
             const uint32_t p2  = min(p + 2, p1 - 1);
             const uint32_t p3  = min(p + 3, p1 - 1);
             const uint32_t cb3 = nstep % 3;  // counter buffer of this piece
-            load_chunks_u<kPC, zfmt>(P.pool, en, lb_of(p2), le_of(p2), Sl);
+            load_chunks_u<kPC, zfmt, kPrNT>(P.pool, en, lb_of(p2), le_of(p2), Sl);
             load_list_u<kPC>(P.list, lb_of(p3), le_of(p3), enn);
             if (zfmt) {  // the 22-bit words of this piece, in place
 #pragma unroll
