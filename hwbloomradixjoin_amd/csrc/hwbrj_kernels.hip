@@ -1319,6 +1319,7 @@ constexpr uint32_t kLfThreads = 1024;
 #endif
 constexpr uint32_t kLfPer     = HWBRJ_LFPER;
 constexpr uint32_t kLfBatch   = kLfThreads * kLfPer;
+static_assert(kLfBatch <= (1u << 17), "batch-local index in 17 bits of a packed entry");
 
 __global__ __launch_bounds__(kLfThreads) void k_list_fill(const uint32_t* __restrict__ meta,
                                                           const uint32_t* __restrict__ wg_used,
@@ -1333,12 +1334,14 @@ __global__ __launch_bounds__(kLfThreads) void k_list_fill(const uint32_t* __rest
                                                           uint32_t* __restrict__ list) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const uint32_t F    = 1u << log2F;
-    uint32_t*      ids  = lds;                // [kLfBatch] sorted entries
-    uint16_t*      qs   = (uint16_t*) (ids + kLfBatch);  // [kLfBatch] their partitions
-    uint32_t*      cnt  = ids + kLfBatch + kLfBatch / 2;  // [F]
+    // sorted batch entries, packed: partition | (count - 1) << 10 | batch-local index << 15
+    // (F <= 1024, kLfBatch <= 2^15)
+    uint32_t*      pk   = lds;                // [kLfBatch]
+    uint32_t*      cnt  = pk + kLfBatch;      // [F]
     uint32_t*      off  = cnt + F;            // [F] batch offsets
     uint32_t*      cur  = off + F;            // [F] next list slot
-    uint32_t*      wtot = cur + F;            // [16] wave totals of the scan
+    uint32_t*      dcur = cur + F;            // [F] cur - off: the entry sorted to pos goes to list[dcur[q] + pos]
+    uint32_t*      wtot = dcur + F;           // [16] wave totals of the scan
     const uint32_t tid  = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t wg   = blockIdx.x;
     {
@@ -1404,20 +1407,22 @@ __global__ __launch_bounds__(kLfThreads) void k_list_fill(const uint32_t* __rest
         __syncthreads();
         uint32_t wbase = 0;
         for (uint32_t w = 0; w < wave; w++) wbase += wtot[w];
-        if (tid < F) off[tid] = wbase + incl - c;
+        if (tid < F) {
+            const uint32_t o = wbase + incl - c;
+            off[tid]  = o;
+            dcur[tid] = cur[tid] - o;
+        }
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < (int) kLfPer; j++) {
             if (m[j] == kNoEntry) continue;
-            const uint32_t q   = m[j] & 0xFFFFu;
-            const uint32_t pos = off[q] + rk[j];
-            ids[pos] = (uint32_t) (region + b0 + tid + j * kLfThreads) | ((((m[j] >> 16) - 1u) & 31u) << kListIdBits);
-            qs[pos]  = (uint16_t) q;
+            const uint32_t q = m[j] & 0xFFFFu;
+            pk[off[q] + rk[j]] = q | ((((m[j] >> 16) - 1u) & 31u) << 10) | ((tid + j * kLfThreads) << 15);
         }
         __syncthreads();
         for (uint32_t pos = tid; pos < nb; pos += kLfThreads) {
-            const uint32_t q = qs[pos];
-            list[cur[q] + (pos - off[q])] = ids[pos];
+            const uint32_t v = pk[pos];
+            list[dcur[v & 1023u] + pos] = (uint32_t) (region + b0 + (v >> 15)) | (((v >> 10) & 31u) << kListIdBits);
         }
         __syncthreads();
         if (tid < F) {
@@ -3688,7 +3693,7 @@ void launch_list_fill(const uint32_t* meta, const uint32_t* wg_used, uint64_t ca
                       const uint32_t* wgq_off, const uint32_t* colc, const uint64_t* cole,
                       uint32_t CH, uint32_t nseg, uint32_t* list_start, uint64_t* elem_start,
                       uint32_t* item_start, uint32_t* list, uint32_t grid, hipStream_t st) {
-    const size_t lds = (kLfBatch + kLfBatch / 2 + 3 * (1u << log2F) + 16) * sizeof(uint32_t);
+    const size_t lds = (kLfBatch + 4 * (1u << log2F) + 16) * sizeof(uint32_t);
     (void) hipFuncSetAttribute((const void*) &k_list_fill, hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds);
     k_list_fill<<<grid, kLfThreads, lds, st>>>(meta, wg_used, cap, log2F, wgq_off, colc, cole, CH,
                                                nseg, list_start, elem_start, item_start, list);
