@@ -2008,7 +2008,9 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
                 }
             }
             stamp(1);
+#ifndef HWBRJ_ABL_PNOB1  // (dev ablation, results invalid: the probe without its per-piece barrier)
             __syncthreads();  // B1: every rank of this piece taken; the previous piece staged
+#endif
             stamp(2);
             // ---- every wave: run offsets of this piece (DPP scan over the NSUB counters)
             const uint32_t cs    = lane < (int) NSUB ? cnt[lane] : 0u;
