@@ -134,6 +134,30 @@ def test_joins_on_two_streams_are_ordered(hw, cuda):
         assert (st.filtered, st.matches) == (g["rows"]["1024"][0], g["results"])
 
 
+def test_back_to_back_joins_of_mixed_configs_on_one_stream(hw, cuda):
+    """Async joins of different filter configurations back to back on one stream: no wait packet
+    between them (stream order), the counts zeroed by each join's own first kernel (the R scatter's
+    workgroup 0; the basic k >= 2 pipeline zeroes by memset), the job table cleared when its layout
+    changes. The last join's counts are its golden's."""
+    g = GOLD["F3_grid"]
+    R = cuda.empty((g["r"], 2), dtype=cuda.int32, device="cuda")
+    S = cuda.empty((g["s"], 2), dtype=cuda.int32, device="cuda")
+    hw.generate_device(R, 2, g["r"], g["r"], 1.0, 11)
+    hw.generate_device(S, 2, INT_MAX, g["r"], g["q"], 22)
+    s1 = cuda.cuda.Stream()
+    blocked = hw.BloomFilterArgs(hw.BLOCKED, g["m"], 1, 1024)
+    basic2 = hw.BloomFilterArgs(hw.BASIC, g["m"], 2, 1024)
+    basic1 = hw.BloomFilterArgs(hw.BASIC, g["m"], 1, 1024)
+    want = {id(blocked): g["rows"]["1024"][0], id(basic2): g["rows"]["basic"][1], id(basic1): g["rows"]["basic"][0]}
+    for seq in ((basic2, blocked, basic1), (blocked, basic1, basic2), (basic1, basic2, blocked), (blocked, blocked)):
+        for a in seq:
+            hw.join_device_async(R, S, a, stream=s1)
+        st = hw.join_wait()
+        assert (st.filtered, st.matches) == (want[id(seq[-1])], g["results"]), seq
+    st = hw.join_device(R, S, basic1)
+    assert (st.filtered, st.matches) == (want[id(basic1)], g["results"])
+
+
 def test_tbl_loader(hw, orc, tmp_path):
     """-R / -S files (src/generator.c:685-741 read_relation): header line skipped, 'key payload',
     'key,payload' and bare-key formats, a [WARN ] line for the first negative key. Counts equal the
