@@ -1315,7 +1315,7 @@ __global__ __launch_bounds__(1024) void k_plan(const uint32_t* __restrict__ wgq_
 // partition, so the list stores are coalesced.
 constexpr uint32_t kLfThreads = 1024;
 #ifndef HWBRJ_LFPER
-#define HWBRJ_LFPER 24
+#define HWBRJ_LFPER 28
 #endif
 constexpr uint32_t kLfPer     = HWBRJ_LFPER;
 constexpr uint32_t kLfBatch   = kLfThreads * kLfPer;
