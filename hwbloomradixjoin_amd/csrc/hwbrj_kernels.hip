@@ -1257,23 +1257,26 @@ __device__ __forceinline__ uint32_t shl_add(uint32_t a, uint32_t s, uint32_t b) 
 
 // Column-wise exclusive scan of the scatter's (workgroup x partition) matrices: every (wg, q) gets
 // its offset inside q's chunk list, and every partition its chunk / element totals. A block takes
-// 64 partitions (lanes) x 16 row groups (waves): every row is loaded by an independent load, so the
-// scan costs one memory latency instead of one per workgroup row.
-constexpr uint32_t kPlanMaxRG = 32;  // rows per wave: G <= 16 * 32 scatter workgroups
+// kPlanCols partitions x 64 row groups (thread t: column t % kPlanCols, row group t / kPlanCols):
+// every row is loaded by an independent load, so the scan costs one memory latency instead of one
+// per workgroup row, and F / kPlanCols blocks share the 2 x G x F x 4 bytes (64 CUs at F = 1024).
+constexpr uint32_t kPlanCols  = 16;
+constexpr uint32_t kPlanMaxRG = 8;  // rows per row group: G <= 64 * 8 scatter workgroups
 
 __global__ __launch_bounds__(1024) void k_plan(const uint32_t* __restrict__ wgq_chunks,
                                                const uint32_t* __restrict__ wgq_elems, uint32_t G,
                                                uint32_t log2F, uint32_t* __restrict__ wgq_off,
                                                uint32_t* __restrict__ colc,
                                                uint64_t* __restrict__ cole) {
-    __shared__ uint32_t tc[16][64];
-    __shared__ uint64_t te[16][64];
+    __shared__ uint32_t tc[16][kPlanCols];  // per wave and column: chunk sum of its 4 row groups
+    __shared__ uint64_t te[16][kPlanCols];
     const uint32_t F = 1u << log2F;
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const uint32_t col = blockIdx.x * 64 + lane;
+    const uint32_t cl = threadIdx.x % kPlanCols, rg = threadIdx.x / kPlanCols;
+    const uint32_t col = blockIdx.x * kPlanCols + cl;
     const bool     okc = col < F;
-    const uint32_t RG  = (G + 15) / 16;
-    const uint32_t r0  = min(G, w * RG), r1 = min(G, r0 + RG);
+    const uint32_t RG  = (G + 63) / 64;
+    const uint32_t r0  = min(G, rg * RG), r1 = min(G, r0 + RG);
     uint32_t       pre[kPlanMaxRG];
     uint32_t       c = 0;
     uint64_t       e = 0;
@@ -1287,22 +1290,30 @@ __global__ __launch_bounds__(1024) void k_plan(const uint32_t* __restrict__ wgq_
         c += cc;
         e += ee;
     }
-    tc[w][lane] = c;
-    te[w][lane] = e;
+    // inclusive scan of c over the wave's 4 row groups (lanes 16 apart), sum of e
+    uint32_t inc = c;
+#pragma unroll
+    for (uint32_t d = kPlanCols; d < 64; d *= 2) {
+        const uint32_t y = __shfl_up(inc, d);
+        if (lane >= d) inc += y;
+        e += __shfl_xor(e, d);
+    }
+    if (lane >= 64 - kPlanCols) tc[w][cl] = inc;
+    if (lane < kPlanCols) te[w][cl] = e;
     __syncthreads();
-    uint32_t base = 0;
-    for (uint32_t v = 0; v < w; v++) base += tc[v][lane];
+    uint32_t base = inc - c;
+    for (uint32_t v = 0; v < w; v++) base += tc[v][cl];
 #pragma unroll
     for (uint32_t j = 0; j < kPlanMaxRG; j++) {
         const uint32_t r = r0 + j;
         if (okc && r < r1) wgq_off[(uint64_t) r * F + col] = base + pre[j];
     }
-    if (w == 0 && okc) {
+    if (w == 0 && lane < kPlanCols && okc) {
         uint32_t tcs = 0;
         uint64_t tes = 0;
         for (int v = 0; v < 16; v++) {
-            tcs += tc[v][lane];
-            tes += te[v][lane];
+            tcs += tc[v][cl];
+            tes += te[v][cl];
         }
         colc[col] = tcs;
         cole[col] = tes;
@@ -3703,9 +3714,9 @@ void launch_list_fill(const uint32_t* meta, const uint32_t* wg_used, uint64_t ca
 
 bool launch_plan(const uint32_t* wgq_chunks, const uint32_t* wgq_elems, uint32_t G, uint32_t log2F,
                  uint32_t* wgq_off, uint32_t* colc, uint64_t* cole, hipStream_t st) {
-    if (G > 16 * kPlanMaxRG) return false;
+    if (G > 64 * kPlanMaxRG) return false;
     const uint32_t F = 1u << log2F;
-    k_plan<<<(F + 63) / 64, 1024, 0, st>>>(wgq_chunks, wgq_elems, G, log2F, wgq_off, colc, cole);
+    k_plan<<<(F + kPlanCols - 1) / kPlanCols, 1024, 0, st>>>(wgq_chunks, wgq_elems, G, log2F, wgq_off, colc, cole);
     return true;
 }
 
