@@ -1260,22 +1260,26 @@ __device__ __forceinline__ uint32_t shl_add(uint32_t a, uint32_t s, uint32_t b) 
 // kPlanCols partitions x 64 row groups (thread t: column t % kPlanCols, row group t / kPlanCols):
 // every row is loaded by an independent load, so the scan costs one memory latency instead of one
 // per workgroup row, and F / kPlanCols blocks share the 2 x G x F x 4 bytes (64 CUs at F = 1024).
-constexpr uint32_t kPlanCols  = 16;
-constexpr uint32_t kPlanMaxRG = 8;  // rows per row group: G <= 64 * 8 scatter workgroups
+#ifndef HWBRJ_PLANCOLS
+#define HWBRJ_PLANCOLS 16
+#endif
+constexpr uint32_t kPlanCols  = HWBRJ_PLANCOLS;
+constexpr uint32_t kPlanRGs   = 1024 / kPlanCols;   // row groups per block
+constexpr uint32_t kPlanMaxRG = 512 / kPlanRGs;     // rows per row group: G <= 512 scatter workgroups
 
 __global__ __launch_bounds__(1024) void k_plan(const uint32_t* __restrict__ wgq_chunks,
                                                const uint32_t* __restrict__ wgq_elems, uint32_t G,
                                                uint32_t log2F, uint32_t* __restrict__ wgq_off,
                                                uint32_t* __restrict__ colc,
                                                uint64_t* __restrict__ cole) {
-    __shared__ uint32_t tc[16][kPlanCols];  // per wave and column: chunk sum of its 4 row groups
+    __shared__ uint32_t tc[16][kPlanCols];  // per wave and column: chunk sum of its row groups
     __shared__ uint64_t te[16][kPlanCols];
     const uint32_t F = 1u << log2F;
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const uint32_t cl = threadIdx.x % kPlanCols, rg = threadIdx.x / kPlanCols;
     const uint32_t col = blockIdx.x * kPlanCols + cl;
     const bool     okc = col < F;
-    const uint32_t RG  = (G + 63) / 64;
+    const uint32_t RG  = (G + kPlanRGs - 1) / kPlanRGs;
     const uint32_t r0  = min(G, rg * RG), r1 = min(G, r0 + RG);
     uint32_t       pre[kPlanMaxRG];
     uint32_t       c = 0;
@@ -3714,7 +3718,7 @@ void launch_list_fill(const uint32_t* meta, const uint32_t* wg_used, uint64_t ca
 
 bool launch_plan(const uint32_t* wgq_chunks, const uint32_t* wgq_elems, uint32_t G, uint32_t log2F,
                  uint32_t* wgq_off, uint32_t* colc, uint64_t* cole, hipStream_t st) {
-    if (G > 64 * kPlanMaxRG) return false;
+    if (G > kPlanRGs * kPlanMaxRG) return false;
     const uint32_t F = 1u << log2F;
     k_plan<<<(F + kPlanCols - 1) / kPlanCols, 1024, 0, st>>>(wgq_chunks, wgq_elems, G, log2F, wgq_off, colc, cole);
     return true;
