@@ -1403,17 +1403,34 @@ __global__ __launch_bounds__(kLfThreads) void k_list_fill(const uint32_t* __rest
     __syncthreads();
     const uint64_t region = (uint64_t) wg * cap;
     const uint32_t used   = wg_used[wg];
+    const uint32_t* __restrict__ rmeta = meta + region;
+    // the next batch's metas are loaded while the current one is sorted and written
+    uint32_t nx[kLfPer];
+#pragma unroll
+    for (int j = 0; j < (int) kLfPer; j++) {
+        const uint32_t i = tid + j * kLfThreads;
+        nx[j]            = i < used ? rmeta[i] : kNoEntry;
+    }
     for (uint32_t b0 = 0; b0 < used; b0 += kLfBatch) {
         const uint32_t nb = min(kLfBatch, used - b0);
-        uint32_t       m[kLfPer], rk[kLfPer];
+        // p: partition | (count - 1) << 10 | rank in the partition's batch run << 15
+        uint32_t p[kLfPer];
 #pragma unroll
         for (int j = 0; j < (int) kLfPer; j++) {
-            const uint32_t i = b0 + tid + j * kLfThreads;
-            m[j]             = i < used ? meta[region + i] : kNoEntry;
+            const uint32_t m = nx[j];
+            p[j]             = kNoEntry;
+            if (m != kNoEntry) {
+                const uint32_t q = m & 0xFFFFu;
+                p[j] = q | ((((m >> 16) - 1u) & 31u) << 10) | (atomicAdd(&cnt[q], 1u) << 15);
+            }
         }
+        if (b0 + kLfBatch < used) {
 #pragma unroll
-        for (int j = 0; j < (int) kLfPer; j++)
-            if (m[j] != kNoEntry) rk[j] = atomicAdd(&cnt[m[j] & 0xFFFFu], 1u);
+            for (int j = 0; j < (int) kLfPer; j++) {
+                const uint32_t i = b0 + kLfBatch + tid + j * kLfThreads;
+                nx[j]            = i < used ? rmeta[i] : kNoEntry;
+            }
+        }
         __syncthreads();
         // exclusive scan of cnt over F (<= 1024) partitions: one per thread, wave scans + totals
         const uint32_t c    = tid < F ? cnt[tid] : 0u;
@@ -1430,9 +1447,9 @@ __global__ __launch_bounds__(kLfThreads) void k_list_fill(const uint32_t* __rest
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < (int) kLfPer; j++) {
-            if (m[j] == kNoEntry) continue;
-            const uint32_t q = m[j] & 0xFFFFu;
-            pk[off[q] + rk[j]] = q | ((((m[j] >> 16) - 1u) & 31u) << 10) | ((tid + j * kLfThreads) << 15);
+            if (p[j] == kNoEntry) continue;
+            const uint32_t q = p[j] & 1023u;
+            pk[off[q] + (p[j] >> 15)] = (p[j] & 0x7FFFu) | ((tid + j * kLfThreads) << 15);
         }
         __syncthreads();
         for (uint32_t pos = tid; pos < nb; pos += kLfThreads) {
