@@ -8,6 +8,7 @@ library is missing this package raises instead of falling back to anything on th
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
 from dataclasses import dataclass
@@ -160,6 +161,8 @@ def lib() -> ctypes.CDLL:
         L.hwbrj_set_device.argtypes = [ctypes.c_int]
         L.hwbrj_last_error.restype = ctypes.c_char_p
         L.hwbrj_version.restype = ctypes.c_char_p
+        L.hwbrj_set_test_hook.restype = ctypes.c_int
+        L.hwbrj_set_test_hook.argtypes = [ctypes.c_int, ctypes.c_int64]
         L.hwbrj_tsc_hz.restype = ctypes.c_uint64
         L.hwbrj_copy_bandwidth.restype = ctypes.c_int
         L.hwbrj_copy_bandwidth.argtypes = [ctypes.c_uint64, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
@@ -256,6 +259,30 @@ def _take_result(r) -> Result:
     out = Result(res.totalresults, res.nthreads, pairs)
     libc.free(r)
     return out
+
+
+HOOK_JOIN_SPLIT, HOOK_PJ_FAIL_RANK, HOOK_BCAST_NONROOT = 1, 2, 3  # include/hwbrj.h hwbrj_set_test_hook
+_HOOK_OFF = {HOOK_JOIN_SPLIT: 0, HOOK_PJ_FAIL_RANK: -1, HOOK_BCAST_NONROOT: 0}
+
+
+def version() -> str:
+    """hwbrj_version(): name, version and every non-default compile-time knob ("knobs: ...")."""
+    return lib().hwbrj_version().decode()
+
+
+def set_test_hook(hook: int, value: int) -> None:
+    """hwbrj_set_test_hook: force a rarely taken path or inject a failure (tests only)."""
+    _err(lib().hwbrj_set_test_hook(hook, int(value)), "hwbrj_set_test_hook")
+
+
+@contextlib.contextmanager
+def hooked(hook: int, value: int):
+    """set_test_hook for the duration of a with-block (then off again)."""
+    set_test_hook(hook, value)
+    try:
+        yield
+    finally:
+        set_test_hook(hook, _HOOK_OFF[hook])
 
 
 def set_gpus(gpus: int) -> None:

@@ -25,7 +25,39 @@ using namespace hwbrj;
 extern "C" {
 
 const char* hwbrj_last_error(void) { return g_last_error.c_str(); }
-const char* hwbrj_version(void) { return "hwbloomradixjoin_amd 0.1 (gfx950)"; }
+// "<name> <version> (gfx950)", then " knobs: ..." naming every compile-time switch of the kernels
+// and every dev environment knob (dev builds only) that differs from the product default
+const char* hwbrj_version(void) {
+    static const std::string v = [] {
+        std::string k = kernel_build_knobs();
+        const std::string d = dev_knobs_string();
+        if (!d.empty()) k += (k.empty() ? "" : " ") + d;
+        return std::string("hwbloomradixjoin_amd 0.4 (gfx950)") + (k.empty() ? "" : " knobs: " + k);
+    }();
+    return v.c_str();
+}
+
+int hwbrj_set_test_hook(int hook, int64_t value) {
+    TestHooks& h = test_hooks();
+    switch (hook) {
+        case HWBRJ_HOOK_JOIN_SPLIT:
+            if (value < 0 || value > 0xFFFFFFFFll) break;
+            h.join_split = (uint32_t) value;
+            return 0;
+        case HWBRJ_HOOK_PJ_FAIL_RANK:
+            h.pj_fail_rank = (int) value;
+            return 0;
+        case HWBRJ_HOOK_BCAST_NONROOT:
+            if (value < 0 || value > 2) break;
+            h.bcast_nonroot = (int) value;
+            return 0;
+        default:
+            set_last_error("unknown test hook");
+            return 2;
+    }
+    set_last_error("test hook value out of range");
+    return 2;
+}
 
 int hwbrj_device_count(void) {
     int n = 0;

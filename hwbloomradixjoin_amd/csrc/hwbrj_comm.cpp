@@ -192,6 +192,34 @@ int rccl_broadcast(void* comm, void* buf, size_t bytes, int root, hipStream_t st
     return 0;
 }
 
+// Status agreement before a collective: every rank contributes its status word to an
+// in-place ncclAllGather and reads all of them back (host-synchronous), so a rank that failed
+// alone (an allocation, a size check) makes every rank return instead of leaving its peers in the
+// collective. Returns rc (this rank's own failure), 22 if another rank failed, 30/31 on RCCL errors.
+int rccl_agree_status(void* comm, int world, int rank, int rc, hipStream_t stream, DevBuf* tmp) {
+    if (int e = need_rccl()) return rc ? rc : e;
+    if (!tmp->ensure((size_t) world * 8)) {
+        set_last_error("hipMalloc failed (status agreement)");
+        rc = rc ? rc : 4;  // (still take part: the peers wait for this rank's word)
+    }
+    std::vector<uint64_t> st(world, 0);
+    st[rank] = (uint64_t) (uint32_t) rc;
+    if (tmp->p == nullptr) return rc;  // no buffer at all: nothing can be exchanged
+    uint64_t* d = tmp->as<uint64_t>();
+    if (hipMemcpyAsync(d + rank, &st[rank], 8, hipMemcpyHostToDevice, stream) != hipSuccess) return rc ? rc : 1;
+    RC_CALL(rccl().AllGather(d + rank, d, 1, ncclUint64, (ncclComm_t) comm, stream), "ncclAllGather (status)");
+    if (hipMemcpyAsync(st.data(), d, (size_t) world * 8, hipMemcpyDeviceToHost, stream) != hipSuccess ||
+        hipStreamSynchronize(stream) != hipSuccess)
+        return rc ? rc : 1;
+    if (rc) return rc;  // (this rank's own message stays)
+    for (int j = 0; j < world; j++)
+        if (st[j]) {
+            set_last_error("rank " + std::to_string(j) + " failed (code " + std::to_string(st[j]) + ")");
+            return 22;
+        }
+    return 0;
+}
+
 int Engine::comm_init(const uint8_t* unique_id, int world, int rank) {
     if (int rc = need_rccl()) return rc;
     if (world < 1 || rank < 0 || rank >= world) {

@@ -168,8 +168,7 @@ bool plan_geometry(const bloom_filter_args_t* a, uint64_t nR, Geometry* g, std::
             if (B >= 8 && m >= 32 && (m / B) <= 0xFFFFFFFFull) {
                 g->mode = MODE_SLICE_BLOCK;
                 F       = std::min<uint64_t>(std::min<uint64_t>(1024, m / B), m / 32);
-                if (const char* e = getenv("HWBRJ_DEV_MAXF"))  // dev-only experiments
-                    F = std::min<uint64_t>(F, strtoull(e, nullptr, 10));
+                if (dev_knobs().maxf) F = std::min<uint64_t>(F, dev_knobs().maxf);  // dev A/B
             } else {
                 g->mode = MODE_GLOBAL;
             }
@@ -182,11 +181,11 @@ bool plan_geometry(const bloom_filter_args_t* a, uint64_t nR, Geometry* g, std::
             g->seg_words  = std::max<uint32_t>(4, g->seg_bits / 32);
         }
         if (g->mode == MODE_SLICE_BLOCK && ilog2u(B) <= g->log2F) g->format = FMT_PACKED;
-        // S partitions: FMT_C22 (22-bit words in 88-byte chunks) is opt-in (HWBRJ_DEV_C22): it cuts
+        // S partitions: FMT_C22 (22-bit words in 88-byte chunks) is a dev A/B (HWBRJ_DEV_C22): it cuts
         // the S traffic by 2.6 GB per join, but the probe's per-word key recovery costs more than
         // that saves
         g->s_format = g->format;
-        if (!mat && g->mode == MODE_SLICE_BLOCK && g->log2F == 10 && getenv("HWBRJ_DEV_C22")) g->s_format = FMT_C22;
+        if (!mat && g->mode == MODE_SLICE_BLOCK && g->log2F == 10 && dev_knobs().c22) g->s_format = FMT_C22;
         if (g->mode == MODE_SLICE_BLOCK || g->mode == MODE_SLICE_BASIC) g->log2seg = ilog2u(g->seg_bits);
         if (a->variant != BASIC) {
             g->log2B    = ilog2u(B);
@@ -239,7 +238,51 @@ void DevBuf::release() {
     bytes = 0;
 }
 
+// ------------------------------------------------------------- dev knobs and test hooks
+const DevKnobs& dev_knobs() {
+    static const DevKnobs k = [] {
+        DevKnobs d;
+#ifdef HWBRJ_DEV_BUILD
+        auto u = [](const char* n) -> uint32_t {
+            const char* e = getenv(n);
+            return e ? (uint32_t) strtoul(e, nullptr, 0) : 0u;
+        };
+        d.kk1       = getenv("HWBRJ_DEV_KK1") != nullptr;
+        d.kk_gather = getenv("HWBRJ_DEV_KK_GATHER") != nullptr;
+        d.c22       = getenv("HWBRJ_DEV_C22") != nullptr;
+        d.noxcd     = getenv("HWBRJ_DEV_NOXCD") != nullptr;
+        d.dbg       = getenv("HWBRJ_DBG") != nullptr;
+        d.maxf      = u("HWBRJ_DEV_MAXF");
+        d.scwpc     = u("HWBRJ_DEV_SCWPC");
+        if (getenv("HWBRJ_DEV_EVFLAGS")) d.evflags = (int) u("HWBRJ_DEV_EVFLAGS");
+#endif
+        return d;
+    }();
+    return k;
+}
+
+std::string dev_knobs_string() {
+    const DevKnobs& d = dev_knobs();
+    std::string     r;
+    auto add = [&](const std::string& w) { r += (r.empty() ? "" : " ") + w; };
+    if (d.kk1) add("HWBRJ_DEV_KK1");
+    if (d.kk_gather) add("HWBRJ_DEV_KK_GATHER");
+    if (d.c22) add("HWBRJ_DEV_C22");
+    if (d.noxcd) add("HWBRJ_DEV_NOXCD");
+    if (d.dbg) add("HWBRJ_DBG");
+    if (d.maxf) add("HWBRJ_DEV_MAXF=" + std::to_string(d.maxf));
+    if (d.scwpc) add("HWBRJ_DEV_SCWPC=" + std::to_string(d.scwpc));
+    if (d.evflags >= 0) add("HWBRJ_DEV_EVFLAGS=" + std::to_string(d.evflags));
+    return r;
+}
+
+TestHooks& test_hooks() {
+    static TestHooks h;
+    return h;
+}
+
 Engine::Engine(int device) : device_(device) {
+    (void) dev_knobs();  // the dev environment is read once, here (dev builds only)
     (void) hipSetDevice(device);
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess) cus_ = prop.multiProcessorCount;
@@ -247,8 +290,7 @@ Engine::Engine(int device) : device_(device) {
     // ev_[0..7] only time phases (elapsed-time reads after ev_[8] has completed): no system-scope
     // fence on record, whose cache writeback idled the GPU ~6 us per marker. ev_[8] (waited on,
     // and ordering later joins) and ev_[9] keep the default release.
-    unsigned evf = hipEventDisableSystemFence;
-    if (const char* e = getenv("HWBRJ_DEV_EVFLAGS")) evf = (unsigned) strtoul(e, nullptr, 0);  // dev A/B
+    const unsigned evf = dev_knobs().evflags >= 0 ? (unsigned) dev_knobs().evflags : hipEventDisableSystemFence;
     for (int i = 0; i < 10; i++)
         (void) (i < 8 ? hipEventCreateWithFlags(&ev_[i], evf) : hipEventCreate(&ev_[i]));
     CrcTables t;
@@ -280,7 +322,7 @@ static uint64_t region_cap(uint64_t n, uint32_t G, uint32_t F) {
 
 int Engine::run(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
                 const bloom_filter_args_t* args, hipStream_t stream, hwbrj_stats_t* st, int jkind) {
-    const int rc = enqueue(dR, nR, dS, nS, args, stream, getenv("HWBRJ_DBG") != nullptr, jkind);
+    const int rc = enqueue(dR, nR, dS, nS, args, stream, dev_knobs().dbg, jkind);
     return rc ? rc : wait(st);
 }
 
@@ -335,9 +377,9 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
         set_last_error("global-bitmap mode: materialized by the side pass");
         return kRcMatGlobal;
     }
-    const bool kk1 = getenv("HWBRJ_DEV_KK1") != nullptr;  // A/B: basic k = 1 on the bit-pass path
+    const bool kk1 = dev_knobs().kk1;  // dev A/B: basic k = 1 on the bit-pass path
     if (!mat && g.mode == MODE_SLICE_BASIC && (g.k > 1 || kk1) && (uint64_t) g.k * nR <= (1ull << 31) &&
-        !getenv("HWBRJ_DEV_KK_GATHER")) {
+        !dev_knobs().kk_gather) {
         if (!stream) stream = own_stream_;
         if (pending_ && stream != pending_stream_) HWBRJ_CHECK(hipStreamWaitEvent(stream, ev_[8], 0));
         return enqueue_basic_kk(dR, nR, dS, nS, g, stream, jkind);
@@ -353,27 +395,36 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     const uint32_t CH         = probe_chunks_per_item();  // chunks per probe item
     const size_t   sc_lds     = mat ? scatter_pay_lds_bytes(g.log2F) : scatter_lds_bytes(g.log2F);
     uint32_t       sc_wpc     = (uint32_t) std::max<size_t>(1, std::min<size_t>(2, 163840 / sc_lds));
-    if (const char* e = getenv("HWBRJ_DEV_SCWPC"))  // dev-only: scatter workgroups per CU
-        sc_wpc = std::max(1u, std::min(sc_wpc, (uint32_t) atoi(e)));
+    if (dev_knobs().scwpc)  // dev A/B: scatter workgroups per CU
+        sc_wpc = std::max(1u, std::min(sc_wpc, dev_knobs().scwpc));
     const uint32_t G          = (uint32_t) cus_ * sc_wpc;
     // basic k >= 2: the S-side buffers first partition the R keys' k * |R| bit positions
     const bool     basic_kk = g.mode == MODE_SLICE_BASIC && g.k > 1;
     const uint64_t nRk      = basic_kk ? (uint64_t) g.k * nR : 0;
+    // the north_star's bitmap broadcast (opt-in, hwbrj_set_filter_broadcast) makes this join a
+    // collective: from here on a failure of this rank alone must not leave its peers waiting in
+    // ncclBroadcast, so every return before the first kernel goes through one status agreement
+    // (argument errors above fail alike on every rank)
+    const bool bcast = bcast_ && comm_ && slice_mode && !basic_kk;
+    auto pre = [&](int rc) -> int {
+        if (!bcast || alloc_only_) return rc;
+        return rccl_agree_status(comm_, comm_world_, comm_rank_, rc, stream, &agree_);
+    };
     const uint64_t capR = region_cap(nR, G, F), capS = region_cap(std::max(nS, nRk), G, F);
     const uint64_t LR = (uint64_t) G * capR, LS = (uint64_t) G * capS;  // max chunks
     const uint64_t items_max = (LS / CH + F + 1) * nseg;
     // list entries hold a 27-bit chunk id (hwbrj_kernels.hip, K4); metas a 22-bit region offset
     if (G > 512) {
         set_last_error("more than 512 scatter workgroups (k_plan row groups)");
-        return 3;
+        return pre(3);
     }
     if (LS > (1ull << 27) || LR > (1ull << 27) || capS >= (1u << 22) || capR >= (1u << 22)) {
         set_last_error("relation too large for 27-bit chunk ids (|S| or |R| > ~4.2e9 tuples per GPU)");
-        return 3;
+        return pre(3);
     }
     if (mat && (capS >= (1u << 21) || capR >= (1u << 21))) {  // half indices (scatter_body_pay) < 2^22
         set_last_error("relation too large for the materializing scatter's 22-bit half indices");
-        return 3;
+        return pre(3);
     }
     const uint64_t GF = (uint64_t) G * F;
     bool ok = true;
@@ -404,9 +455,10 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     }
     if (!ok) {
         set_last_error("hipMalloc failed (device memory)");
-        return 4;
+        return pre(4);
     }
     if (alloc_only_) return 0;
+    if (const int rc = pre(0)) return rc;
     uint64_t* d_result   = small.as<uint64_t>();      // [0] matches
     uint64_t* d_dcount   = small.as<uint64_t>() + 1;  // [1] dense survivor count (global mode)
     uint64_t* d_filtered = small.as<uint64_t>() + 2;  // [2] S-tuples after filter
@@ -462,14 +514,23 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     bp.run_off     = rrun.as<uint32_t>() + sweeps_max * NSUB;
     bp.ppool       = mat ? ppoolR.as<uint32_t>() : nullptr;
     bp.out_pay     = mat ? rpay.as<uint32_t>() : nullptr;
-    // the north_star's bitmap broadcast (opt-in, hwbrj_set_filter_broadcast): rank 0 builds the
-    // slices, the other ranks only sub-partition R for the join and receive them over RCCL
-    const bool bcast = bcast_ && comm_ && slice_mode && !basic_kk;
-    bp.no_slices     = bcast && comm_rank_ != 0 ? 1u : 0u;
+    // the broadcast: rank 0 builds the slices, the other ranks only sub-partition R for the join
+    // and receive them over RCCL (HWBRJ_HOOK_BCAST_NONROOT: this rank takes the non-root side, for
+    // tests at world 1; value 2 zeroes the slices first, so the counts show whether k_build wrote any)
+    const int nonroot_hook = bcast ? test_hooks().bcast_nonroot : 0;
+    bp.no_slices = bcast && (comm_rank_ != 0 || nonroot_hook) ? 1u : 0u;
+    if (nonroot_hook == 2) HWBRJ_CHECK(hipMemsetAsync(slices.p, 0, slices.bytes, stream));
     launch_build(bp, F, stream);
     if (bcast) {
         const int rc = rccl_broadcast(comm_, slices.p, (size_t) F * nseg * g.seg_words * 4, 0, stream);
-        if (rc) return rc;
+        if (rc) {  // kernels of this join are enqueued: later joins must still order after them
+            (void) hipEventRecord(ev_[8], stream);
+            pending_        = true;
+            pending_stream_ = stream;
+            pending_rc_     = rc;
+            pending_err_    = hwbrj_last_error();
+            return rc;
+        }
     }
     if (basic_kk) {
         // basic k >= 2: the k bit positions of every R key, partitioned by slice with the S-side
@@ -581,8 +642,7 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     jp.extra           = jtask.as<uint2>();
     jp.nextra          = jparts.as<uint32_t>() + 2 * NJ;
     jp.jkind           = (uint32_t) jkind;
-    if (const char* e = getenv("HWBRJ_DEV_JOIN_SPLIT"))  // tests: force the skew split
-        jp.split_surv = (uint32_t) strtoul(e, nullptr, 10);
+    jp.split_surv      = test_hooks().join_split;  // (tests: force the skew split)
     if (mat) {
         // (k_join_split, which leaves job_surv zero for the next join, does not run here)
         HWBRJ_CHECK(hipMemsetAsync(jparts.as<uint32_t>() + NJ, 0, (size_t) NJ * 4, stream));
@@ -616,6 +676,7 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     HWBRJ_CHECK(hipEventRecord(ev_[8], stream));
     HWBRJ_CHECK(hipGetLastError());
     pending_      = true;
+    pending_rc_   = 0;
     pending_args_ = args != nullptr;
     pending_nS_   = nS;
     pending_ev_   = phase_ev_;
@@ -880,12 +941,12 @@ int Engine::enqueue_basic_kk(const uint2* dR, uint64_t nR, const uint2* dS, uint
     jp.extra           = jtask.as<uint2>();
     jp.nextra          = jparts.as<uint32_t>() + 2 * NJ;
     jp.jkind           = (uint32_t) jkind;
-    if (const char* e = getenv("HWBRJ_DEV_JOIN_SPLIT"))
-        jp.split_surv = (uint32_t) strtoul(e, nullptr, 10);
+    jp.split_surv      = test_hooks().join_split;
     launch_join(jp, NJ, jparts.as<uint32_t>() + NJ, stream);
     HWBRJ_CHECK(hipEventRecord(ev_[8], stream));
     HWBRJ_CHECK(hipGetLastError());
     pending_      = true;
+    pending_rc_   = 0;
     pending_args_ = true;
     pending_nS_   = nS;
     pending_ev_   = phase_ev_;
@@ -902,6 +963,10 @@ int Engine::wait(hwbrj_stats_t* st) {
         return 6;
     }
     HWBRJ_CHECK(hipEventSynchronize(ev_[8]));
+    if (pending_rc_) {  // the last join stopped after some of its kernels (a failed broadcast)
+        set_last_error(pending_err_);
+        return pending_rc_;
+    }
     const Geometry& g = last_g_;
     const uint32_t  F = 1u << g.log2F, NSUB = 1u << g.log2NSUB;
     const uint32_t  nseg = (g.mode == MODE_SLICE_BLOCK || g.mode == MODE_SLICE_BASIC) ? g.nseg : 1;

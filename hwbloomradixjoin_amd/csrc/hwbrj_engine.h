@@ -95,6 +95,7 @@ class Engine {
     int          comm_world_ = 1, comm_rank_ = 0;
     bool         bcast_      = false;
     DevBuf       xslot_[HWBRJ_PJ_NSLOTS], xcnt_;  // the native exchange's buffers
+    DevBuf       agree_;                           // status words of the broadcast join's agreement
     int          device_;
     int          cus_ = 256;
     hipStream_t  own_stream_ = nullptr;
@@ -110,7 +111,12 @@ class Engine {
     // the pending join's survivor phase is fused into its probe (no ev_[7] of its own)
     bool         phase_ev_     = true;
     bool         pending_ev_   = true;
-    hipStream_t  pending_stream_ = nullptr;  // the stream the pending join was enqueued on
+    // the stream the pending join was enqueued on. Joins on the same stream are ordered by it; a
+    // join on another stream waits for ev_[8]. Compared by handle: a stream must outlive the
+    // joins enqueued on it (a destroyed stream's handle can be reused by a new one).
+    hipStream_t  pending_stream_ = nullptr;
+    int          pending_rc_     = 0;   // nonzero: the pending join failed after enqueuing kernels
+    std::string  pending_err_;
     bool         surv_fused_   = false;
     hipError_t   mark(int i, hipStream_t stream);  // ev_[i] when phase_ev_
     bool         alloc_only_   = false;  // reserve(): enqueue returns after its allocations
@@ -146,6 +152,7 @@ void    set_last_error(const std::string& s);
 // RCCL entry points used by the engine (hwbrj_comm.cpp; librccl is bound at first use). Return 0 or
 // an error code with the message in set_last_error.
 int rccl_broadcast(void* comm, void* buf, size_t bytes, int root, hipStream_t stream);
+int rccl_agree_status(void* comm, int world, int rank, int rc, hipStream_t stream, DevBuf* tmp);
 
 // glibc's rand() (stdlib/random_r.c TYPE_3) with private state (hwbrj_gen.cpp).
 struct GlibcRand {

@@ -3,6 +3,8 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+
+#include <string>
 #include <stddef.h>
 #include <stdint.h>
 
@@ -205,5 +207,35 @@ void   launch_export(const uint32_t* slices, const Geometry& g, uint32_t* out, u
 // a streaming copy of bytes (multiple of 16) from src to dst, grid workgroups of contiguous ranges
 // (hwbrj_copy_bandwidth)
 void   launch_copy_bw(const void* src, void* dst, uint64_t bytes, int grid, hipStream_t st);
+
+// every compile-time switch of hwbrj_kernels.hip that differs from the product default ("" for the
+// product build); hwbrj_version() appends it
+const char* kernel_build_knobs();
+
+// Dev-only runtime switches (A/B experiments of measured alternatives), read from the HWBRJ_DEV_*
+// environment once, at the first Engine's construction, and only in builds with -DHWBRJ_DEV_BUILD:
+// a product build ignores the environment, so no stray variable changes its path.
+struct DevKnobs {
+    bool     kk1 = false;        // HWBRJ_DEV_KK1: basic k = 1 on the bit-pass pipeline
+    bool     kk_gather = false;  // HWBRJ_DEV_KK_GATHER: basic k >= 2 by global-slice gathers
+    bool     c22 = false;        // HWBRJ_DEV_C22: 22-bit S words (FMT_C22)
+    bool     noxcd = false;      // HWBRJ_DEV_NOXCD: k_join_mat without XCD-aware job order
+    bool     dbg = false;        // HWBRJ_DBG: in-kernel phase stamps (a -DHWBRJ_STAMPS build)
+    uint32_t maxf = 0;           // HWBRJ_DEV_MAXF: cap on the partition count F
+    uint32_t scwpc = 0;          // HWBRJ_DEV_SCWPC: scatter workgroups per CU
+    int      evflags = -1;       // HWBRJ_DEV_EVFLAGS: phase-event creation flags
+};
+const DevKnobs& dev_knobs();
+// "name=value" of every dev knob that is set ("" in product builds); hwbrj_version() appends it
+std::string dev_knobs_string();
+
+// Test hooks (hwbrj_set_test_hook, include/hwbrj.h): explicit process-wide settings that force
+// rarely taken paths (no result changes) or inject a failure; all off by default.
+struct TestHooks {
+    uint32_t join_split    = 0;   // HWBRJ_HOOK_JOIN_SPLIT: survivors per join part (0: the default)
+    int      pj_fail_rank  = -1;  // HWBRJ_HOOK_PJ_FAIL_RANK: this rank fails the shard check
+    int      bcast_nonroot = 0;   // HWBRJ_HOOK_BCAST_NONROOT: the broadcast join as a non-root rank
+};
+TestHooks& test_hooks();
 
 }  // namespace hwbrj

@@ -22,10 +22,24 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <string>
 #include <type_traits>
 
 #include "hwbrj_common.h"
 #include "hwbrj_kernels.h"
+
+// Ablations ("results invalid": they skip work to time what is left) and cycle stamps exist for
+// measurements only. They build only with -DHWBRJ_DEV_BUILD (tools/build_abl.sh sets it), so no
+// product build can carry one by accident; hwbrj_version() names every non-default knob.
+#if !defined(HWBRJ_DEV_BUILD) &&                                                                   \
+    (defined(HWBRJ_ABL_NOCRC) || defined(HWBRJ_ABL_NOCRAP) || defined(HWBRJ_ABL_NOSTORE) ||        \
+     defined(HWBRJ_ABL_SPLITH) || defined(HWBRJ_ABL_PNOPST) || defined(HWBRJ_ABL_BNOBITS) ||       \
+     defined(HWBRJ_ABL_BNOSORT) || defined(HWBRJ_ABL_PNOB1) || defined(HWBRJ_ABL_JNOR) ||          \
+     defined(HWBRJ_ABL_JNOS) || defined(HWBRJ_ABL_MJ_EMPTY) || defined(HWBRJ_ABL_MJ_NOLOAD) ||     \
+     defined(HWBRJ_ABL_MJ_NOINS) || defined(HWBRJ_ABL_MJ_R) || defined(HWBRJ_ABL_PROBE) ||         \
+     defined(HWBRJ_STAMPS))
+#error "HWBRJ_ABL_* / HWBRJ_STAMPS give invalid results or perturb timing: dev builds only (-DHWBRJ_DEV_BUILD)"
+#endif
 
 namespace hwbrj {
 
@@ -1713,6 +1727,29 @@ template <int KIND> constexpr uint32_t scr_cap() {
     return KIND == KIND_BLOCK_PKK || KIND == KIND_BASIC_KK || KIND == KIND_BLOCK_ZK ? (uint32_t) HWBRJ_SCRK
                                                                                      : (uint32_t) HWBRJ_SCR1;
 }
+// Dev ablations of the probe's parts (dev builds only; results invalid except `filtered`):
+// 1 = loads + test + barrier only, 2 = + the compaction, 3 = everything but the copy-out.
+#ifndef HWBRJ_ABL_PROBE
+#define HWBRJ_ABL_PROBE 0
+#endif
+constexpr int kAblProbe = HWBRJ_ABL_PROBE;
+// The counting probe's copy-out: b128 stores per thread per piece (a fixed count: vmcnt), so its
+// stage holds at most kPco * 4096 words. Every store instruction costs its whole wave's issue and
+// data path even when its lanes are out of range (the copy-out of 3 per thread was 0.21 ms of the
+// north star's 1.08 ms probe while its stage held 648 quads: profiles/r04/probe_split.txt).
+#ifndef HWBRJ_PCO
+#define HWBRJ_PCO 1
+#endif
+#ifndef HWBRJ_PCO_AUX
+#define HWBRJ_PCO_AUX 0
+#endif
+#ifndef HWBRJ_PCO_SKIP  // (A/B) 1: a wave with no quad of the stage in range skips its store
+#define HWBRJ_PCO_SKIP 0
+#endif
+#ifndef HWBRJ_PRT_W0  // (A/B) 1: only wave 0 issues the run-table stores and the job-count atomic
+#define HWBRJ_PRT_W0 0
+#endif
+constexpr int kPco = HWBRJ_PCO < kPC ? HWBRJ_PCO : kPC;
 
 __device__ __forceinline__ uint32_t find_q(const uint32_t* item_start, uint32_t F, uint32_t it) {
     uint32_t lo = 0, hi = F - 1;
@@ -1790,7 +1827,8 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
         const uint32_t nbytes = ((prev_total + 3u) & ~3u) * 4u;  // item region holds round_up(total, 4)
         const auto     ro     = buf_rsrc(prev_out, nbytes);
         const v4u*     src    = (const v4u*) (stage + prev_buf * sstr);
-        if (PAY) {  // codes and their chunk positions (half a stage buffer each)
+        if (kAblProbe != 0) {  // (ablations: the run table only; 1 and 2 write empty runs)
+        } else if (PAY) {  // codes and their chunk positions (half a stage buffer each)
             const auto rp = buf_rsrc(P.surv_pos + (prev_out - P.surv), nbytes);
 #pragma unroll
             for (int k = 0; k < (kPC + 1) / 2; k++) {
@@ -1801,12 +1839,14 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
             }
         } else {
 #pragma unroll
-        for (int k = 0; k < kPC; k++) {
+        for (int k = 0; k < kPco; k++) {
             const uint32_t i = tid + k * NT;
+            if (HWBRJ_PCO_SKIP && (uint32_t) (wave * 64 + k * NT) * 16u >= nbytes) continue;  // wave-uniform
             const v4u      v = src[min(i, scap / 4 - 1)];  // reads past the stage are never stored
-            __builtin_amdgcn_raw_buffer_store_b128(v, ro, i * 16, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b128(v, ro, i * 16, 0, HWBRJ_PCO_AUX);
         }
         }
+        if (HWBRJ_PRT_W0 && wave != 0) return;
         const uint32_t tb = prev_it == kNoItem ? 0u : NSUB * 4;  // run table (wave 0 holds it)
         const auto rc = buf_rsrc(P.surv_cnt + (uint64_t) (prev_it & ~kNoItem) * NSUB, tb);
         const auto rf = buf_rsrc(P.surv_off + (uint64_t) (prev_it & ~kNoItem) * NSUB, tb);
@@ -1819,6 +1859,7 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
     };
     uint64_t filtered = 0;  // wave 0: survivors of this workgroup's items
     uint32_t nstep    = 0;  // items processed (selects the counter / stage buffers)
+    uint64_t abl_n    = 0;  // (probe ablations 1 and 2: this wave's survivors)
     // Outer loop: runs of items with one (q, seg), i.e. one slice segment in LDS. Inner loop:
     // the pieces of the run, software-pipelined: piece p is tested while p+1 and p+2 are in flight
     // (three register buffers rotate, so no load result is ever copied; past the end the loads
@@ -1920,7 +1961,7 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
                 // wave ballot compacts the survivors there (no exec masking: the others write a
                 // shared garbage slot). Otherwise no scratch write at all (high selectivity: the
                 // words are ranked one by one, and 12 LDS writes per thread would buy nothing)
-                if (!PAY && kScrCap > 0 && nsv <= kScrCap) {  // wave-uniform
+                if (!PAY && kScrCap > 0 && nsv <= kScrCap && kAblProbe != 1) {  // wave-uniform
 #ifdef HWBRJ_PR_BALLOT  // (dev A/B: slot-major compaction by wave ballots)
                     uint32_t at0 = 0;
 #pragma unroll
@@ -1966,7 +2007,9 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
             constexpr uint32_t kNoRank = 0xFFFFFFFFu;
             uint32_t   dr[kDense];
             uint32_t   rank2[NW / 2];            // word by word: two 16-bit ranks per register
-            if (dense) {
+            if (kAblProbe == 1 || kAblProbe == 2) {
+                abl_n += nsv;
+            } else if (dense) {
                 // KIND_BASIC_KK: bits 2..k of every slot's candidate from the slices in HBM, bit by
                 // bit, each bit loaded for all of the wave's live slots before any is tested
                 // (kDense loads in flight instead of one at a time); stops when no slot is live
@@ -2063,7 +2106,8 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
             const bool     staged = PAY ? total <= hp : total <= scap;
             uint32_t*      stg    = stage + buf * sstr;
             const auto     ro     = buf_rsrc(out, total * 4);
-            if (dense) {
+            if (kAblProbe == 1 || kAblProbe == 2) {
+            } else if (dense) {
 #pragma unroll
                 for (int k = 0; k < kDense; k++) {
                     const bool     ok = dr[k] != kNoRank;
@@ -2114,6 +2158,8 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
     __syncthreads();  // the last piece is staged
     copy_out();
     if (tid == 0 && filtered) atomicAdd((unsigned long long*) P.filtered, (unsigned long long) filtered);
+    if (kAblProbe == 1 || kAblProbe == 2)
+        if (lane == 0 && abl_n) atomicAdd((unsigned long long*) P.filtered, (unsigned long long) abl_n);
     if (P.dbg && tid == 0)
         for (int k = 0; k < 6; k++) P.dbg[blockIdx.x * 8 + k] = tph[k];
 }
@@ -3160,7 +3206,7 @@ __global__ __launch_bounds__(kMatThreads) __attribute__((amdgpu_waves_per_eu(8))
 
 void launch_join_mat(const MatJoinParams& p0, uint32_t jobs, hipStream_t st) {
     MatJoinParams p = p0;
-    p.xcd8          = ((jobs >> p.log2NSUB) % 8 == 0 && !getenv("HWBRJ_DEV_NOXCD")) ? 1u : 0u;
+    p.xcd8          = ((jobs >> p.log2NSUB) % 8 == 0 && !dev_knobs().noxcd) ? 1u : 0u;
     k_join_mat<<<jobs, kMatThreads, 0, st>>>(p);
 }
 
@@ -3818,6 +3864,7 @@ size_t probe_lds_bytes(const Geometry& g, uint32_t* stage_cap, bool pay) {
     // 2 buffers of cap words + 64 dummy slots each, in what the 512-byte static table leaves
     // (pay: codes and positions, half a buffer each)
     size_t cap = std::min<size_t>(kProbeCH * 32, (163840 - 512 - base) / 8 - 64) & ~(size_t) 7;
+    if (!pay) cap = std::min<size_t>(cap, (size_t) kPco * 4096);  // what the copy-out's stores cover
     if (stage_cap) *stage_cap = (uint32_t) cap;
     return base + 2 * (cap + 64) * 4;
 }
@@ -3854,6 +3901,123 @@ uint32_t join_extra_tasks() { return kJoinExtra; }
 void launch_export(const uint32_t* slices, const Geometry& g, uint32_t* out, uint64_t nwords,
                    hipStream_t st) {
     k_export<<<2048, 256, 0, st>>>(slices, g, out, nwords);
+}
+
+// ---------------------------------------------------------------- build knobs (hwbrj_version)
+// Every compile-time switch of this file whose value differs from the product default, as
+// "NAME=value" words; empty for the product build (tests/test_abi.py pins that).
+const char* kernel_build_knobs() {
+    static const std::string s = [] {
+        std::string r;
+        auto num = [&](const char* n, long v, long d) {
+            if (v != d) r += std::string(r.empty() ? "" : " ") + n + "=" + std::to_string(v);
+        };
+        auto flag = [&](const char* n) { r += std::string(r.empty() ? "" : " ") + n; };
+        (void) flag;
+#ifdef HWBRJ_DEV_BUILD
+        flag("HWBRJ_DEV_BUILD");
+#endif
+        num("HWBRJ_SC_T", HWBRJ_SC_T, 1024);
+        num("HWBRJ_SC_E", HWBRJ_SC_E, 8);
+        num("HWBRJ_SC_K", HWBRJ_SC_K, 2);
+        num("HWBRJ_SC_PRE", HWBRJ_SC_PRE, 1);
+        num("HWBRJ_SC_KEEPY", HWBRJ_SC_KEEPY, 1);
+        num("HWBRJ_SC_LAUX", HWBRJ_SC_LAUX, 2);
+        num("HWBRJ_SC_SAUX", HWBRJ_SC_SAUX, 2);
+        num("HWBRJ_SC_SAUX_R", HWBRJ_SC_SAUX_R, 2);
+        num("HWBRJ_SC_SB", HWBRJ_SC_SB, 2);
+        num("HWBRJ_SC_KP", HWBRJ_SC_KP, 3);
+        num("HWBRJ_PLANCOLS", HWBRJ_PLANCOLS, 16);
+        num("HWBRJ_LFPER", HWBRJ_LFPER, 28);
+        num("HWBRJ_BPQ", HWBRJ_BPQ, 2);
+        num("HWBRJ_BD_NT", HWBRJ_BD_NT, 0);
+        num("HWBRJ_PC", HWBRJ_PC, 3);
+        num("HWBRJ_SCR1", HWBRJ_SCR1, 128);
+        num("HWBRJ_PR_NT", HWBRJ_PR_NT, 0);
+        num("HWBRJ_SCRK", HWBRJ_SCRK, 256);
+        num("HWBRJ_JTU", HWBRJ_JTU, 8);
+        num("HWBRJ_JRR", HWBRJ_JRR, 4);
+        num("HWBRJ_JRW", HWBRJ_JRW, 4);
+        num("HWBRJ_JSR", HWBRJ_JSR, 8);
+        num("HWBRJ_JSW", HWBRJ_JSW, 2);
+        num("HWBRJ_JFR", HWBRJ_JFR, 8);
+        num("HWBRJ_JFW", HWBRJ_JFW, 5);
+        num("HWBRJ_ABL_PROBE", HWBRJ_ABL_PROBE, 0);
+        num("HWBRJ_PCO", HWBRJ_PCO, 1);
+        num("HWBRJ_PCO_AUX", HWBRJ_PCO_AUX, 0);
+        num("HWBRJ_PCO_SKIP", HWBRJ_PCO_SKIP, 0);
+        num("HWBRJ_PRT_W0", HWBRJ_PRT_W0, 0);
+#define HWBRJ_FLAG_KNOB(X) flag(#X)
+#ifdef HWBRJ_SC_LD32
+        HWBRJ_FLAG_KNOB(HWBRJ_SC_LD32);
+#endif
+#ifdef HWBRJ_SC_NOORD
+        HWBRJ_FLAG_KNOB(HWBRJ_SC_NOORD);
+#endif
+#ifdef HWBRJ_SC_NOPINW
+        HWBRJ_FLAG_KNOB(HWBRJ_SC_NOPINW);
+#endif
+#ifdef HWBRJ_PR_BALLOT
+        HWBRJ_FLAG_KNOB(HWBRJ_PR_BALLOT);
+#endif
+#ifdef HWBRJ_JSLOT1
+        HWBRJ_FLAG_KNOB(HWBRJ_JSLOT1);
+#endif
+#ifdef HWBRJ_NOJFUSE
+        HWBRJ_FLAG_KNOB(HWBRJ_NOJFUSE);
+#endif
+#ifdef HWBRJ_JDUPRTN
+        HWBRJ_FLAG_KNOB(HWBRJ_JDUPRTN);
+#endif
+#ifdef HWBRJ_STAMPS
+        HWBRJ_FLAG_KNOB(HWBRJ_STAMPS);
+#endif
+#ifdef HWBRJ_ABL_NOCRC
+        HWBRJ_FLAG_KNOB(HWBRJ_ABL_NOCRC);
+#endif
+#ifdef HWBRJ_ABL_NOCRAP
+        HWBRJ_FLAG_KNOB(HWBRJ_ABL_NOCRAP);
+#endif
+#ifdef HWBRJ_ABL_NOSTORE
+        HWBRJ_FLAG_KNOB(HWBRJ_ABL_NOSTORE);
+#endif
+#ifdef HWBRJ_ABL_SPLITH
+        HWBRJ_FLAG_KNOB(HWBRJ_ABL_SPLITH);
+#endif
+#ifdef HWBRJ_ABL_PNOPST
+        HWBRJ_FLAG_KNOB(HWBRJ_ABL_PNOPST);
+#endif
+#ifdef HWBRJ_ABL_BNOBITS
+        HWBRJ_FLAG_KNOB(HWBRJ_ABL_BNOBITS);
+#endif
+#ifdef HWBRJ_ABL_BNOSORT
+        HWBRJ_FLAG_KNOB(HWBRJ_ABL_BNOSORT);
+#endif
+#ifdef HWBRJ_ABL_PNOB1
+        HWBRJ_FLAG_KNOB(HWBRJ_ABL_PNOB1);
+#endif
+#ifdef HWBRJ_ABL_JNOR
+        HWBRJ_FLAG_KNOB(HWBRJ_ABL_JNOR);
+#endif
+#ifdef HWBRJ_ABL_JNOS
+        HWBRJ_FLAG_KNOB(HWBRJ_ABL_JNOS);
+#endif
+#ifdef HWBRJ_ABL_MJ_EMPTY
+        HWBRJ_FLAG_KNOB(HWBRJ_ABL_MJ_EMPTY);
+#endif
+#ifdef HWBRJ_ABL_MJ_NOLOAD
+        HWBRJ_FLAG_KNOB(HWBRJ_ABL_MJ_NOLOAD);
+#endif
+#ifdef HWBRJ_ABL_MJ_NOINS
+        HWBRJ_FLAG_KNOB(HWBRJ_ABL_MJ_NOINS);
+#endif
+#ifdef HWBRJ_ABL_MJ_R
+        HWBRJ_FLAG_KNOB(HWBRJ_ABL_MJ_R);
+#endif
+#undef HWBRJ_FLAG_KNOB
+        return r;
+    }();
+    return s.c_str();
 }
 
 }  // namespace hwbrj

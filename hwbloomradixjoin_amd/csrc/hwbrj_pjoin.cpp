@@ -171,10 +171,9 @@ int Engine::join_partitioned(const hwbrj_exchange_t* x, int rank, int world, con
         capR = pj_region_cap(nR, G, F), capS = pj_region_cap(nS, G, F);
         const uint64_t LR = (uint64_t) G * capR;
         LS = (uint64_t) G * capS;
-        // (HWBRJ_DEV_PJ_FAIL_RANK=r, tests: rank r fails this check, as an oversized shard would)
-        const char* fr = getenv("HWBRJ_DEV_PJ_FAIL_RANK");
+        // (HWBRJ_HOOK_PJ_FAIL_RANK = r, tests: rank r fails this check, as an oversized shard would)
         if (G > 512 || LS > (1ull << 27) || LR > (1ull << 27) || capS >= (1u << 22) || capR >= (1u << 22) ||
-            (fr && atoi(fr) == rank)) {
+            test_hooks().pj_fail_rank == rank) {
             set_last_error("shard too large for 27-bit chunk ids");
             return 3;
         }
@@ -573,7 +572,7 @@ int Engine::join_partitioned(const hwbrj_exchange_t* x, int rank, int world, con
     jp.extra           = jtask.as<uint2>();
     jp.nextra          = jparts.as<uint32_t>() + 2 * F * NSUB;
     jp.item_base       = pjIbase.as<uint64_t>();
-    if (const char* e = getenv("HWBRJ_DEV_JOIN_SPLIT")) jp.split_surv = (uint32_t) strtoul(e, nullptr, 10);
+    jp.split_surv      = test_hooks().join_split;
     launch_join(jp, NJ, pjJobs.as<uint32_t>(), stream);
     PJ_STAGE("k_join");
     PJ_CHECK(hipGetLastError());

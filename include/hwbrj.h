@@ -27,32 +27,52 @@
 extern "C" {
 #endif
 
-/* ---- reference-compatible types (layouts identical to src/types.h, src/bloom_filter.h) ---- */
+/* ---- reference-compatible types (layouts identical to src/types.h, src/bloom_filter.h) ----
+ * A translation unit may include the reference's own headers beside this one (its src/main.c
+ * relinked against this library): each type is then defined once.
+ *   - src/types.h (guard TYPES_H), in either order: this block defines TYPES_H, so a later
+ *     types.h is empty, and an earlier one makes this block empty.
+ *   - src/bloom_filter.h (guard BLOOM_FILTER_H): include it BEFORE this header (main.c's include
+ *     order); its BASIC/BLOCKED enum and bloom_filter_args_t are then used as they are, and the
+ *     sectorized variant is HWBRJ_SECTORIZED.
+ * This library is the reference's default build (32-bit keys, 8-byte tuples): KEY_8B is refused. */
+#ifdef KEY_8B
+#error "libhwbrj joins 8-byte tuples (src/types.h without KEY_8B); KEY_8B is not supported"
+#endif
+#ifndef TYPES_H
+#define TYPES_H
 typedef int32_t intkey_t;
 typedef int32_t value_t;
 
-typedef struct tuple_t {
+typedef struct tuple_t    tuple_t;
+typedef struct relation_t relation_t;
+typedef struct result_t       result_t;
+typedef struct threadresult_t threadresult_t;
+
+struct tuple_t {
     intkey_t key;
     value_t  payload;
-} tuple_t;
+};
 
-typedef struct relation_t {
+struct relation_t {
     tuple_t * tuples;
     uint64_t  num_tuples;
-} relation_t;
+};
 
-typedef struct threadresult_t {
+struct threadresult_t {
     int64_t  nresults;
     void *   results;
     uint32_t threadid;
-} threadresult_t;
+};
 
-typedef struct result_t {
+struct result_t {
     int64_t          totalresults;
     threadresult_t * resultlist; /* NULL: results are counted, not materialized (reference default) */
     int              nthreads;
-} result_t;
+};
+#endif /* TYPES_H */
 
+#ifndef BLOOM_FILTER_H
 /* BASIC = 0 and BLOCKED = 1 as in the reference. SECTORIZED is this build's extension
  * (DESIGN.md "Filter variants"); the reference has no such variant. */
 typedef enum { BASIC = 0, BLOCKED = 1, SECTORIZED = 2 } bloom_filter_variant_t;
@@ -64,11 +84,14 @@ typedef struct bloom_filter_args_t {
     uint64_t               B; /* block size in bits (power of 2, divides m) */
 } bloom_filter_args_t;
 
+void assert_args(bloom_filter_args_t * args);
+#endif /* BLOOM_FILTER_H */
+#define HWBRJ_SECTORIZED ((bloom_filter_variant_t) 2)
+
 /* ---- drop-in operator boundary ---- */
 result_t * BPRO(relation_t * relR, relation_t * relS, int nthreads,
                 bloom_filter_args_t * bloom_filter_args);
 result_t * PRO(relation_t * relR, relation_t * relS, int nthreads);
-void       assert_args(bloom_filter_args_t * args);
 /* The reference's other partitioned-join entries (src/main.c:331-339). They differ in the
  * per-partition join function plugged into join_init_run: the histogram join (Kim et al.) for
  * BPRH / PRH, with SIMD compares for BPRHO / PRHO (here: k_join's histogram variants, see
@@ -293,7 +316,25 @@ int          hwbrj_device_count(void);
 int          hwbrj_set_device(int device);
 void         hwbrj_release(void); /* free all device buffers */
 const char * hwbrj_last_error(void);
+/* "hwbloomradixjoin_amd <version> (gfx950)"; a build whose kernels were compiled with any
+ * non-default switch (tuning A/Bs, dev ablations) appends " knobs: NAME=value ..." naming them. */
 const char * hwbrj_version(void);
+
+/* Test hooks (no reference counterpart): process-wide settings that force rarely taken paths or
+ * inject a failure, so tests can reach them on one GPU. All are off (0 / -1) by default; none
+ * changes a result except HWBRJ_HOOK_BCAST_NONROOT = 2, which exists to show that it would.
+ *   HWBRJ_HOOK_JOIN_SPLIT     value > 0: the join's skew split cuts every (partition, sub) job
+ *                             above `value` survivors into parts (counts unchanged).
+ *   HWBRJ_HOOK_PJ_FAIL_RANK   rank `value` of a partitioned join fails its shard-size check
+ *                             (code 3), as an oversized shard would; -1 = off.
+ *   HWBRJ_HOOK_BCAST_NONROOT  with hwbrj_set_filter_broadcast(1): this rank runs the broadcast
+ *                             join's non-root side (k_build writes no filter slices; they come
+ *                             from ncclBroadcast, which at world 1 leaves the buffer as it is).
+ *                             1 = as is, 2 = the slice buffer zeroed first (the filter is then
+ *                             empty unless something writes it: the counts must drop).
+ * Returns 0, or 2 for an unknown hook or a value out of range. */
+enum { HWBRJ_HOOK_JOIN_SPLIT = 1, HWBRJ_HOOK_PJ_FAIL_RANK = 2, HWBRJ_HOOK_BCAST_NONROOT = 3 };
+int          hwbrj_set_test_hook(int hook, int64_t value);
 
 #ifdef __cplusplus
 }

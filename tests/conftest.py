@@ -34,3 +34,16 @@ def cuda():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     return torch
+
+
+@pytest.fixture
+def hook(hw):
+    """hook(HOOK, value): hwbrj_set_test_hook for this test only (switched off at teardown)."""
+    done = []
+
+    def set_hook(h, value):
+        hw.set_test_hook(h, int(value))
+        done.append(h)
+    yield set_hook
+    for h in done:
+        hw.set_test_hook(h, hw._HOOK_OFF[h])

@@ -19,6 +19,7 @@ INT_MAX = 2**31 - 1
 def declared_functions():
     src = open(os.path.join(ROOT, "include", "hwbrj.h")).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    src = re.sub(r"^\s*#.*$", "", src, flags=re.M)  # preprocessor lines (#error text, macros)
     # (function-pointer members, "int (*f)(...);", are not exported functions)
     names = re.findall(r"\b([A-Za-z_][A-Za-z0-9_]*)\s*\((?!\s*\*)[^;{]*\)\s*;", src)
     return sorted(set(n for n in names if n not in ("if", "while", "for", "sizeof")))
@@ -137,3 +138,23 @@ def test_write_relation_format(hw, tmp_path):
     assert f.read_text() == want
     hw.write_relation(np.zeros((0, 2), dtype=np.int32), str(f))
     assert f.read_text() == "#KEY, VAL\n"
+
+
+def test_product_build_reports_no_knobs(hw):
+    """hwbrj_version() names every compile-time switch and dev environment knob that differs from
+    the product default: the in-tree build reports none."""
+    v = hw.version()
+    assert v.startswith("hwbloomradixjoin_amd ") and "(gfx950)" in v
+    assert "knobs" not in v, v
+
+
+def test_ablations_need_dev_build(tmp_path):
+    """A results-invalid ablation cannot slip into a product build: hwbrj_kernels.hip refuses
+    HWBRJ_ABL_* / HWBRJ_STAMPS unless HWBRJ_DEV_BUILD is defined (preprocessing only)."""
+    src = os.path.join(ROOT, "hwbloomradixjoin_amd", "csrc", "hwbrj_kernels.hip")
+    inc = ["-I", os.path.join(ROOT, "hwbloomradixjoin_amd", "csrc"), "-I", os.path.join(ROOT, "include")]
+    base = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-std=c++17", "-E", "-o", str(tmp_path / "k.i")] + inc
+    r = subprocess.run(base + ["-DHWBRJ_ABL_NOCRC", src], capture_output=True, text=True)
+    assert r.returncode != 0 and "dev builds only" in r.stderr, r.stderr[-2000:]
+    r = subprocess.run(base + ["-DHWBRJ_ABL_NOCRC", "-DHWBRJ_DEV_BUILD", src], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-2000:]

@@ -36,22 +36,26 @@ def rel(keys):
     return np.stack([keys, np.arange(keys.size, dtype=np.int32)], 1)
 
 
-def torchrun(world, args, env_extra, timeout=300):
-    """bench.py under torch.distributed.run in its own process group, killed as a group on timeout
-    (no rank outlives the test). Returns (returncode, stdout, stderr); returncode None = timeout."""
+def torchrun(world, args, env_extra, timeout=300, script=None):
+    """bench.py (or `script` with `args`) under torch.distributed.run in its own process group,
+    killed as a group on timeout (no rank outlives the test). Returns (returncode, stdout, stderr);
+    returncode None = timeout."""
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
     env = dict(os.environ, **env_extra)
-    for k in ("HWBRJ_BENCH_SHARED_GPU", "HWBRJ_BENCH_DIST", "HWBRJ_PJ_FORCE_COLL", "HWBRJ_DEV_PJ_FAIL_RANK",
-              "HWBRJ_RCCL_SELF"):
+    for k in ("HWBRJ_BENCH_SHARED_GPU", "HWBRJ_BENCH_DIST", "HWBRJ_PJ_FORCE_COLL", "HWBRJ_RCCL_SELF"):
         if k not in env_extra:
             env.pop(k, None)
+    if script is None:
+        target = [os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--steps", "2", "--warmup", "1",
+                  "--no-cpu-baseline", "--no-e2e"]
+    else:
+        target = [os.path.join(HERE, script)]
     p = subprocess.Popen(["python", "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
-                          "--master-addr", "127.0.0.1", "--master-port", str(port),
-                          os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--steps", "2", "--warmup", "1",
-                          "--no-cpu-baseline", "--no-e2e"] + [str(x) for x in args],
+                          "--master-addr", "127.0.0.1", "--master-port", str(port)]
+                         + target + [str(x) for x in args],
                          stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env, cwd=ROOT,
                          start_new_session=True)
     try:
@@ -169,15 +173,67 @@ def test_bench_rccl_world1(hw, case):
 # ------------------------------------------------- status agreement (no hang on one rank's error)
 @pytest.mark.parametrize("fail_rank", [0, 1])
 def test_partitioned_rank_failure_does_not_hang(hw, fail_rank):
-    """One rank of two fails the capacity check alone (HWBRJ_DEV_PJ_FAIL_RANK, as an oversized
+    """One rank of two fails the capacity check alone (HWBRJ_HOOK_PJ_FAIL_RANK, as an oversized
     shard would): the ranks agree on their statuses before the first collective, so both return an
     error promptly (torch.distributed.run exits nonzero) instead of the other rank waiting in the
-    R all-to-all forever."""
+    R all-to-all forever. Without the hook the same run succeeds and its counts sum to the golden."""
     g = GOLD["F3_grid"]
-    rc, out, err = torchrun(2, ["--design", "partitioned", "-r", g["r"], "-s", g["s"], "-m", g["m"]],
-                            {"HWBRJ_BENCH_SHARED_GPU": "1", "HWBRJ_DEV_PJ_FAIL_RANK": str(fail_rank)},
-                            timeout=240)
+    args = [g["r"], g["s"], g["m"]]
+    rc, out, err = torchrun(2, [fail_rank] + args, {}, timeout=240, script="pj_rank_worker.py")
     assert rc is not None, "ranks hung: " + err[-3000:]
     assert rc != 0
     assert "shard too large" in err
     assert f"rank {fail_rank} failed" in err
+    if fail_rank == 1:
+        rc, out, err = torchrun(2, [-1] + args, {}, timeout=240, script="pj_rank_worker.py")
+        assert rc == 0, err[-3000:]
+        ok = [line.split()[-2:] for line in out.splitlines() if ": ok " in line]
+        assert len(ok) == 2
+        assert (sum(int(f) for f, _ in ok), sum(int(m) for _, m in ok)) == (g["rows"]["1024"][0], g["results"])
+
+
+def test_partitioned_rccl_failure_world1(hw, cuda, orc, rccl1, hook):
+    """The native transport's status agreement with a failing rank: at world 1
+    the rank fails its shard check (HWBRJ_HOOK_PJ_FAIL_RANK = 0), hwbrj_join_partitioned_rccl
+    returns the error instead of entering a collective, and the next join on the same Engine and
+    communicator is correct."""
+    g = GOLD["F3_grid"]
+    R = hw.generate_host(g["r"], 2, g["r"], g["r"], 1.0, 1)
+    S = hw.generate_host(g["s"], 2, INT_MAX, g["r"], g["q"], 2)
+    dR, dS = to_dev(cuda, R), to_dev(cuda, S)
+    args = hw.BloomFilterArgs(hw.BLOCKED, g["m"], 1, 1024)
+    hook(hw.HOOK_PJ_FAIL_RANK, 0)
+    with pytest.raises(RuntimeError, match="shard too large"):
+        rccl1.join_partitioned_rccl(dR, dS, g["r"], args)
+    hw.set_test_hook(hw.HOOK_PJ_FAIL_RANK, -1)
+    st = rccl1.join_partitioned_rccl(dR, dS, g["r"], args)
+    assert (st.filtered, st.matches) == (g["rows"]["1024"][0], g["results"])
+
+
+@pytest.mark.parametrize("a", [("blocked", 1 << 24, 1, 1024), ("sectorized", 1 << 24, 2, 1024),
+                               ("basic", 1 << 24, 1, 1024), ("blocked", 1 << 31, 2, 512)], ids=str)
+def test_filter_broadcast_nonroot_world1(hw, cuda, orc, rccl1, hook, a):
+    """The broadcast join's non-root side (BuildParams::no_slices: k_build sub-partitions R for the
+    join and writes no filter slice; the slices arrive by ncclBroadcast), which a world-1 run never
+    takes by itself. HWBRJ_HOOK_BCAST_NONROOT = 1: the slices the root join
+    left in place are received unchanged (a broadcast from rank 0 at world 1), and the counts equal
+    the oracle's, so the non-root R runs are right. = 2: the slices are zeroed first; the filter
+    then rejects every S tuple, so the non-root k_build wrote no slice."""
+    g = GOLD["F3_grid"]
+    R = hw.generate_host(g["r"], 2, g["r"], g["r"], 1.0, 1)
+    S = hw.generate_host(g["s"], 2, INT_MAX, g["r"], g["q"], 2)
+    args = hw.BloomFilterArgs.from_flag(*a)
+    dR, dS = to_dev(cuda, R), to_dev(cuda, S)
+    res, filt, _ = orc.bpro(R, S, 8, args.variant, args.m, args.k, args.B)
+    rccl1.set_filter_broadcast(True)
+    st = hw.join_device(dR, dS, args)  # as the root: builds the slices
+    assert (st.filtered, st.matches) == (filt, res)
+    hook(hw.HOOK_BCAST_NONROOT, 1)
+    st = hw.join_device(dR, dS, args)
+    assert (st.filtered, st.matches) == (filt, res)
+    hook(hw.HOOK_BCAST_NONROOT, 2)
+    st = hw.join_device(dR, dS, args)
+    assert (st.filtered, st.matches) == (0, 0)
+    hook(hw.HOOK_BCAST_NONROOT, 0)
+    st = hw.join_device(dR, dS, args)  # the root again rebuilds them
+    assert (st.filtered, st.matches) == (filt, res)

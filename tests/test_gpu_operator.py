@@ -310,7 +310,7 @@ def test_m_2_32(hw, cuda, orc, variant):
         oracle_check(hw, cuda, orc, rel(Rk), rel(Sk), hw.BloomFilterArgs(variant, 1 << 32, k, 1024))
 
 
-def test_basic_kk_materialize_and_skew(hw, cuda, orc, monkeypatch):
+def test_basic_kk_materialize_and_skew(hw, cuda, orc, hook):
     """Basic k = 3 on the materialization path and with the join's skew split forced."""
     rng = np.random.default_rng(13)
     nR = 200000
@@ -326,7 +326,7 @@ def test_basic_kk_materialize_and_skew(hw, cuda, orc, monkeypatch):
     assert st.matches == want.shape[0] == p.shape[0]
     key = lambda x: x[np.lexsort((x[:, 1], x[:, 0]))]  # noqa: E731
     assert np.array_equal(key(p), key(want))
-    monkeypatch.setenv("HWBRJ_DEV_JOIN_SPLIT", "700")
+    hook(hw.HOOK_JOIN_SPLIT, "700")
     oracle_check(hw, cuda, orc, R, S, a)
 
 
@@ -355,10 +355,10 @@ def test_partitioned_world1_vs_oracle(hw, cuda, orc, a):
         assert (st.filtered, st.matches) == (filt, res), (a, nR, nS, st)
 
 
-def test_partitioned_world1_skew_and_dups(hw, cuda, orc, gen3, monkeypatch):
+def test_partitioned_world1_skew_and_dups(hw, cuda, orc, gen3, hook):
     """Duplicate R keys (hash-path join jobs) and a Zipf S with the skew split forced."""
     from hwbloomradixjoin_amd import pjoin
-    monkeypatch.setenv("HWBRJ_DEV_JOIN_SPLIT", "700")
+    hook(hw.HOOK_JOIN_SPLIT, "700")
     for mode in ("nonunique", "zipf"):
         R, S = gen3[1][mode]
         S = S[:4000000]

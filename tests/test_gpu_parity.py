@@ -467,10 +467,10 @@ def test_bpro_materialized_result_list(hw, orc):
 
 
 @pytest.mark.parametrize("split", ["700", "5000"])
-def test_join_skew_split_forced(hw, cuda, orc, gen3, split, monkeypatch):
+def test_join_skew_split_forced(hw, cuda, orc, gen3, split, hook):
     """The join's skew split (extra parts over a job's probe items) forced on every job: the counts
     and materialized pairs still equal the oracle's (Zipf S; non-unique R takes the hash path)."""
-    monkeypatch.setenv("HWBRJ_DEV_JOIN_SPLIT", split)
+    hook(hw.HOOK_JOIN_SPLIT, split)
     for mode in ("zipf", "nonunique"):
         R, S = gen3[1][mode]
         S = S[:4000000]
