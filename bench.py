@@ -244,8 +244,8 @@ def main():
     alg_bytes = 8.0 * (nR + nS_total) if a.scaling == "strong" else 8.0 * (nR + nS) * world
     achieved = alg_bytes / (dev_ms * 1e-3) / 1e9
     peak = HBM_PEAK_GBS * world
-    pm = load_pmc(a.pmc_json, [nR, nS, a.s_sel, a.bloom_filter, a.bloom_size, a.bloom_hashes,
-                               a.bloom_block_size]) if world == 1 else None
+    pm, pmc_note = load_pmc(a.pmc_json, [nR, nS, a.s_sel, a.bloom_filter, a.bloom_size, a.bloom_hashes,
+                                         a.bloom_block_size], hw.version()) if world == 1 else (None, "N > 1")
     traffic = sum(p.get("hbm_bytes", 0) for p in pm["phases"].values()) if pm else None
     # the dominant kernel against its own s8(d) bytes: k_scatter_s reads every S tuple once (8 B)
     dom = max(("r_scatter", "build", "s_scatter", "probe", "join"), key=lambda p: mean["ms_" + p])
@@ -259,6 +259,8 @@ def main():
                 "modeled_bytes": modeled_bytes(nR, nS, st.filtered, a.bloom_size if args else 0,
                                                word_bytes),
                 "pmc_source": os.path.relpath(a.pmc_json, ROOT) if pm else None,
+                "pmc_library": pm.get("library") if pm else None,
+                "traffic_note": pmc_note,
                 "dominant_kernel": {
                     "name": {"s_scatter": "k_scatter_s", "r_scatter": "k_scatter_r",
                              "probe": "k_probe", "build": "k_build", "join": "k_join"}[dom],
@@ -416,14 +418,20 @@ def run_partitioned(a, hw, torch, dist, rank, world, local, dR, dS, args, shared
         dist.destroy_process_group()
 
 
-def load_pmc(path: str, key: list):
-    """Per-phase HBM bytes of one join (tools/prof_summary.py output) when it was collected on
-    this exact configuration, else None."""
+def load_pmc(path: str, key: list, library: str):
+    """Per-phase HBM bytes of one join (tools/prof_summary.py output) when they were collected on
+    this exact configuration AND on a library with this run's stamp (hwbrj_version(): the hash of
+    the product sources and every non-default knob), else None. Returns (pmc or None, note)."""
     try:
         pm = json.load(open(path))
     except (OSError, ValueError):
-        return None
-    return pm if pm.get("config_key") == key else None
+        return None, f"{os.path.relpath(path, ROOT)} missing"
+    if pm.get("config_key") != key:
+        return None, "no PMC traffic profiled for this configuration"
+    if pm.get("library") != library:
+        return None, (f"PMC traffic was profiled on '{pm.get('library')}', this run's library is "
+                      f"'{library}': not used")
+    return pm, "PMC traffic of this library (FETCH_SIZE x2 + WRITE_SIZE, one join)"
 
 
 def host_cpu() -> dict:
@@ -443,14 +451,60 @@ def host_cpu() -> dict:
 # Calibration (BASELINE.md "Calibration of the CPU port"): on the same 8-core host the reference
 # binary needs 6.0 s where this port needs 13.0-13.6 s (C2, -n 8, re-measured in round 3), i.e. the
 # port runs at 0.45x it.
-PORT_VS_REFERENCE = 6.0 / 13.5
+def filter_calibration(orc, R, S, variant, m, k, B, threads, nprobe=64_000_000):
+    """The reference's OWN filter code (oracle/_ref/libbloomref.so: its src/hash.c and
+    src/bloom_filter.c compiled unmodified) against the port's (oracle/oracle.c) on this host, at
+    `threads` threads over the same keys: the add loop over R and the contains loop over the first
+    `nprobe` S keys, ns per key per thread. These loops are where the reference spends ~90 % of its
+    time, so their ratio is the port's calibration, measured where it runs."""
+    import ctypes
+    import threading
+
+    import numpy as np
+    if not orc.have_ref():
+        return None
+    rk = np.ascontiguousarray(R[:, 0])
+    sk = np.ascontiguousarray(S[: min(nprobe, S.shape[0]), 0])
+
+    def par(fn, keys):
+        per = keys.shape[0] // threads
+        ts = [threading.Thread(target=fn, args=(keys.ctypes.data + 4 * t * per,
+                                                per if t < threads - 1 else keys.shape[0] - per * t))
+              for t in range(threads)]
+        t0 = time.perf_counter()
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        return (time.perf_counter() - t0) * 1e9 * threads / max(1, keys.shape[0])
+
+    ra = orc._RefArgs(variant, m, k, B)
+    st = orc.ref().bloom_filter_create(ctypes.byref(ra), 42)
+    ref_add = par(lambda p, n: orc.ref().ref_add_all(st, p, n), rk)
+    ref_has = par(lambda p, n: orc.ref().ref_count(st, p, n), sk)
+    orc.ref().bloom_filter_destroy(st)
+    f = orc._Bloom()
+    L = orc.lib()
+    if L.orc_bloom_init(ctypes.byref(f), variant, m, k, B, 42):
+        return None
+    port_add = par(lambda p, n: L.orc_bloom_add_all_atomic(ctypes.byref(f), p, n), rk)
+    port_has = par(lambda p, n: L.orc_count_filtered(ctypes.byref(f), p, n), sk)
+    L.orc_bloom_free(ctypes.byref(f))
+    return {"threads": threads, "keys_add": int(rk.shape[0]), "keys_contains": int(sk.shape[0]),
+            "ns_per_key_thread": {"reference_add": round(ref_add, 1), "port_add": round(port_add, 1),
+                                  "reference_contains": round(ref_has, 1), "port_contains": round(port_has, 1)},
+            "port_vs_reference_contains": round(ref_has / port_has, 3),
+            "what": "the reference's own bloom_filter.c (libbloomref.so, built from its sources) vs the "
+                    "port's filter code, same keys, same threads, this host; >1 = the port is faster"}
 
 
 def cpu_baseline(a, hw):
     """The oracle's pthreads restatement of BPRO (oracle/oracle.c, "port") on the GPU host's CPU:
     full |R| and filter, the first --cpu-sample tuples of S (default: all of it), timed over the
     reference's TOTAL-TIME region, once on every CPU this process may use (capped by
-    OMP_NUM_THREADS, the box's CPU share) and once at 8 threads (the reference's measured -n 8)."""
+    OMP_NUM_THREADS, the box's CPU share) and once at 8 threads (the reference's measured -n 8).
+    Beside it, the calibration: the reference's own filter loops against the port's, measured on
+    this host (filter_calibration)."""
     info = host_cpu()
     try:
         from oracle import pyoracle as orc
@@ -466,21 +520,30 @@ def cpu_baseline(a, hw):
         for t in sorted({threads, 8}):
             res, filt, tm = orc.bpro(R, S, t, variant, a.bloom_size, a.bloom_hashes,
                                      a.bloom_block_size, use)
-            runs[t] = (sample / (tm["total"] / 1e6), tm["total"] / 1e6, filt, res)
-        v, secs, filt, res = runs[threads]
+            runs[t] = (sample / (tm["total"] / 1e6), tm["total"] / 1e6, filt, res,
+                       [round(x / 1e6, 3) for x in tm["phases"]])
+        v, secs, filt, res, phases = runs[threads]
+        cal = None
+        if use and variant != 2:  # (the reference has no sectorized filter)
+            try:
+                cal = filter_calibration(orc, R, S, variant, a.bloom_size, a.bloom_hashes,
+                                         a.bloom_block_size, threads)
+            except Exception as e:  # noqa: BLE001 (reported, never required)
+                cal = {"failed": str(e)}
         return {"value": round(v, 1), "unit": "probe-tuples/s", "cores": threads, "kind": "port",
                 "host": info, "value_n8": round(runs[8][0], 1),
                 "cores_cap": (f"OMP_NUM_THREADS={cap}: the GPU pool's CPU share for one GPU's job "
-                              "(BASELINE.md, round-3 re-measurement)"),
-                "calibration_port_vs_reference": round(PORT_VS_REFERENCE, 3),
-                "reference_estimate": round(v / PORT_VS_REFERENCE, 1),
+                              "(BASELINE.md)"),
+                "phases_s": dict(zip(("r_loop1_add", "r_scatter", "s_loop1_contains", "s_scatter",
+                                      "pass2", "join"), phases)),
+                "calibration": cal,
                 "sample": (f"|R|={a.r_size}, |S|={sample} tuples of the same generator "
                            f"(q={a.s_sel}), m={a.bloom_size}"
                            + (" (the full workload)" if sample == a.s_size else " (S sample)")
                            + f"; oracle orc_bpro TOTAL-TIME {secs:.3f} s on {threads} threads "
-                           f"({runs[8][1]:.3f} s on 8), filtered={filt} matches={res}. The port "
-                           f"runs at {PORT_VS_REFERENCE:.2f}x the reference binary on the same "
-                           "host (BASELINE.md), so reference_estimate = value / that ratio")}
+                           f"({runs[8][1]:.3f} s on 8), filtered={filt} matches={res}. "
+                           "calibration: the reference's own filter code timed beside the port's "
+                           "on this host (BASELINE.md)")}
     except Exception as e:  # the baseline is reported, never required for the GPU line
         return {"value": None, "unit": "probe-tuples/s", "cores": None, "kind": "port",
                 "host": info, "sample": f"failed: {e}"}

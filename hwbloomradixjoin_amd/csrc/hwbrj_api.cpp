@@ -25,14 +25,18 @@ using namespace hwbrj;
 extern "C" {
 
 const char* hwbrj_last_error(void) { return g_last_error.c_str(); }
-// "<name> <version> (gfx950)", then " knobs: ..." naming every compile-time switch of the kernels
-// and every dev environment knob (dev builds only) that differs from the product default
+// "<name> <version> (gfx950) src <hash>", then " knobs: ..." naming every compile-time switch of
+// the kernels and every dev environment knob (dev builds only) that differs from the product
+// default. The hash is the Makefile's stamp of the product sources and flags ("dev" otherwise).
+#ifndef HWBRJ_SRC_SHA
+#define HWBRJ_SRC_SHA "dev"
+#endif
 const char* hwbrj_version(void) {
     static const std::string v = [] {
         std::string k = kernel_build_knobs();
         const std::string d = dev_knobs_string();
         if (!d.empty()) k += (k.empty() ? "" : " ") + d;
-        return std::string("hwbloomradixjoin_amd 0.4 (gfx950)") + (k.empty() ? "" : " knobs: " + k);
+        return std::string("hwbloomradixjoin_amd 0.4 (gfx950) src " HWBRJ_SRC_SHA) + (k.empty() ? "" : " knobs: " + k);
     }();
     return v.c_str();
 }

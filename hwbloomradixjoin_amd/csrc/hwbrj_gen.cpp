@@ -303,7 +303,8 @@ int hwbrj_create_relation_zipf_device(tuple_t* d_out, uint64_t n, uint64_t alpha
 
 // ---- relation files (the reference's PERSIST_RELATIONS output, the only on-disk format) ----
 // "%d %d\n" lines through a large buffer (fprintf per tuple is slow for 10^9 tuples).
-static int write_pairs(FILE* fp, const tuple_t* t, uint64_t n) {
+// backwards: t[n-1] first (write_result_relation's cb_read_backwards order, tuple_buffer.h:77-90)
+static int write_pairs(FILE* fp, const tuple_t* t, uint64_t n, bool backwards = false) {
     std::vector<char> buf(1 << 20);
     size_t            used = 0;
     auto put_int = [&](int32_t v, char end) {
@@ -323,8 +324,9 @@ static int write_pairs(FILE* fp, const tuple_t* t, uint64_t n) {
             if (fwrite(buf.data(), 1, used, fp) != used) return 1;
             used = 0;
         }
-        put_int(t[i].key, ' ');
-        put_int(t[i].payload, '\n');
+        const tuple_t& x = t[backwards ? n - 1 - i : i];
+        put_int(x.key, ' ');
+        put_int(x.payload, '\n');
     }
     return used && fwrite(buf.data(), 1, used, fp) != used ? 1 : 0;
 }
@@ -372,9 +374,11 @@ int hwbrj_write_result_relation(const result_t* res, const char* filename) {
         if (!cb) continue;
         uint64_t left = (uint64_t) res->resultlist[t].nresults;
         bool     head = true;  // the newest buffer holds writepos pairs, the older ones are full
+        // the reference's order exactly: newest buffer first, each read from its last pair to its
+        // first (cb_begin_backwards / cb_read_backwards, src/tuple_buffer.h:58-90, :221-226)
         for (const Buf* b = cb->buf; b && left && rc == 0; b = b->next, head = false) {
             const uint64_t n = std::min<uint64_t>(left, head ? cb->writepos : kPer);
-            rc = write_pairs(fp, b->tuples, n);
+            rc = write_pairs(fp, b->tuples, n, true);
             left -= n;
         }
     }

@@ -78,6 +78,10 @@ typedef struct orc_timing_t {
     double total_usec;     /* src/parallel_radix_join_bloom.c:1521-1522 */
     double partition_usec; /* :1525-1527 */
     double join_usec;      /* :1528-1530 */
+    /* thread 0's phases (for the CPU-baseline calibration): R loop 1 (histogram +
+     * bloom add) and its barrier, R scatter (+ barrier :1153), S loop 1 (histogram + contains),
+     * S scatter (+ barrier :1171), pass-2 (+ task creation), join */
+    double phase_usec[6];
 } orc_timing_t;
 
 /* src/parallel_radix_join_bloom.c:1560-1787 (BPRO -> join_init_run -> prj_thread):
@@ -94,6 +98,7 @@ int64_t  orc_bpro(const orc_tuple_t * R, uint64_t nR, const orc_tuple_t * S, uin
 int64_t  orc_join_pairs(const orc_tuple_t * R, uint64_t nR, const orc_tuple_t * S, uint64_t nS,
                         orc_tuple_t * out, uint64_t cap);
 
+void     orc_bloom_add_all_atomic(orc_bloom_t * f, const int32_t * keys, uint64_t n);
 /* Scalar helpers for tests (single-threaded, small inputs). */
 uint64_t orc_count_filtered(const orc_bloom_t * f, const int32_t * keys, uint64_t n);
 /* src/unit_tests.c:191-283: false-positive counts of the FPR unit test (blocked B=512, then

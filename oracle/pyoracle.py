@@ -49,6 +49,7 @@ def lib() -> ctypes.CDLL:
                                      ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32]
         L.orc_bloom_free.argtypes = [ctypes.c_void_p]
         L.orc_bloom_add_all.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]
+        L.orc_bloom_add_all_atomic.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]
         L.orc_count_filtered.restype = ctypes.c_uint64
         L.orc_count_filtered.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]
         L.orc_bloom_popcount.restype = ctypes.c_uint64
@@ -130,7 +131,7 @@ class _Bloom(ctypes.Structure):  # orc_bloom_t
 
 class _Timing(ctypes.Structure):
     _fields_ = [("total_usec", ctypes.c_double), ("partition_usec", ctypes.c_double),
-                ("join_usec", ctypes.c_double)]
+                ("join_usec", ctypes.c_double), ("phase_usec", ctypes.c_double * 6)]
 
 
 def crc(seed: int, key: int) -> int:
@@ -173,7 +174,7 @@ def bpro(R: np.ndarray, S: np.ndarray, nthreads: int = 8, variant: int = 1, m: i
     if res < 0:
         raise MemoryError("orc_bpro allocation failed")
     return int(res), int(f.value), {"total": tm.total_usec, "partition": tm.partition_usec,
-                                    "join": tm.join_usec}
+                                    "join": tm.join_usec, "phases": list(tm.phase_usec)}
 
 
 def bloom_bitmap(keys: np.ndarray, variant: int, m: int, k: int, B: int):

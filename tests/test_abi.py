@@ -158,3 +158,49 @@ def test_ablations_need_dev_build(tmp_path):
     assert r.returncode != 0 and "dev builds only" in r.stderr, r.stderr[-2000:]
     r = subprocess.run(base + ["-DHWBRJ_ABL_NOCRC", "-DHWBRJ_DEV_BUILD", src], capture_output=True, text=True)
     assert r.returncode == 0, r.stderr[-2000:]
+
+
+def test_bench_uses_pmc_traffic_only_for_the_profiled_library(tmp_path, hw):
+    """bench.py's roofline.traffic comes from profiles/pmc_traffic.json only when that file was
+    profiled on this configuration AND on a library with the same stamp."""
+    import importlib.util
+    import json as _json
+    spec = importlib.util.spec_from_file_location("bench", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    key = [1, 2, 0.01, "blocked", 1 << 30, 1, 1024]
+    f = tmp_path / "pmc.json"
+    f.write_text(_json.dumps({"config_key": key, "library": hw.version(), "phases": {}}))
+    pm, note = bench.load_pmc(str(f), key, hw.version())
+    assert pm is not None and "this library" in note
+    pm, note = bench.load_pmc(str(f), key, hw.version() + " knobs: X")
+    assert pm is None and "not used" in note
+    pm, note = bench.load_pmc(str(f), key[:-1] + [512], hw.version())
+    assert pm is None
+    assert "src " in hw.version()
+
+
+def test_write_result_relation_reference_order(hw, tmp_path):
+    """hwbrj_write_result_relation emits the pairs in write_result_relation's order
+    (src/tuple_buffer.h:205-231): per thread, the newest chained buffer first, every buffer from its
+    last pair to its first (cb_begin_backwards / cb_read_backwards, :58-90). Thread 0 holds a
+    partly filled newest buffer (3 pairs) and a full older one; thread 1 one pair."""
+    import ctypes
+    n_old = hw._CB_TUPLES
+    old = np.stack([np.arange(n_old), -np.arange(n_old)], 1).astype(np.int32)
+    new = np.array([[7, 70], [8, 80], [9, 90]], dtype=np.int32)
+    one = np.array([[5, 50]], dtype=np.int32)
+    TP = ctypes.POINTER(hw._Tuple)
+    b_old = hw._TupleBuffer(old.ctypes.data_as(TP), None)
+    b_new = hw._TupleBuffer(new.ctypes.data_as(TP), ctypes.pointer(b_old))
+    b_one = hw._TupleBuffer(one.ctypes.data_as(TP), None)
+    c0 = hw._ChainedTupleBuffer(ctypes.pointer(b_new), None, None, 3, 0, 0, 2)
+    c1 = hw._ChainedTupleBuffer(ctypes.pointer(b_one), None, None, 1, 0, 0, 1)
+    tl = (hw._ThreadResult * 2)(hw._ThreadResult(n_old + 3, ctypes.addressof(c0), 0),
+                                hw._ThreadResult(1, ctypes.addressof(c1), 1))
+    res = hw._Result(n_old + 4, ctypes.addressof(tl), 2)
+    out = tmp_path / "Out.tbl"
+    assert hw.lib().hwbrj_write_result_relation(ctypes.addressof(res), str(out).encode()) == 0
+    got = np.loadtxt(out, dtype=np.int64, ndmin=2)
+    want = np.concatenate([new[::-1], old[::-1], one]).astype(np.int64)
+    assert got.shape == want.shape and np.array_equal(got, want)

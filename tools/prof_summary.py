@@ -10,6 +10,7 @@ Infinity-Cache hits are included in these counters.
 import csv
 import glob
 import json
+import os
 import sys
 from collections import defaultdict
 
@@ -77,9 +78,13 @@ def main():
         fetch[lab] += v
     for lab, v in counters(wdir, "WRITE_SIZE"):
         write[lab] += v
-    res = {"config_key": None, "phases": {}}
+    res = {"config_key": None, "library": None, "phases": {}}
     if len(sys.argv) > 5:
         res["config_key"] = json.loads(sys.argv[5])
+    # the library that was profiled (bench.py uses this traffic only for the same stamp)
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import hwbloomradixjoin_amd as hw
+    res["library"] = hw.version()
     for lab, p in phases.items():
         res["phases"][lab] = {
             "ms": round(p["ms"], 4), "kernels": p["kernels"],
