@@ -185,6 +185,31 @@ int nx_allgather(void* ctx, int slot, uint64_t bytes) {
 
 }  // namespace
 
+// All-to-all of n u64 per rank between device buffers, enqueued on the engine's stream (no host
+// synchronisation): the partitioned join's counts messages (d_send[j n ..) to rank j).
+int rccl_alltoall_u64_dev(Engine* e, const uint64_t* d_send, uint64_t* d_recv, uint64_t n) {
+    const int   W  = e->comm_world();
+    const int   me = e->comm_rank();
+    hipStream_t st = e->stream();
+    if (!rccl_self() &&
+        hipMemcpyAsync(d_recv + (uint64_t) me * n, d_send + (uint64_t) me * n, n * 8, hipMemcpyDeviceToDevice, st) != hipSuccess) {
+        set_last_error("device copy of the rank's own counts failed");
+        return 1;
+    }
+    if (W == 1 && !rccl_self()) return 0;
+    if (int rc = need_rccl()) return rc;
+    const Rccl& R = rccl();
+    ncclComm_t  c = (ncclComm_t) e->comm();
+    RC_CALL(R.GroupStart(), "ncclGroupStart");
+    for (int j = 0; j < W; j++) {
+        if (j == me && !rccl_self()) continue;
+        RC_CALL(R.Send(d_send + (uint64_t) j * n, n, ncclUint64, j, c, st), "ncclSend (counts)");
+        RC_CALL(R.Recv(d_recv + (uint64_t) j * n, n, ncclUint64, j, c, st), "ncclRecv (counts)");
+    }
+    RC_CALL(R.GroupEnd(), "ncclGroupEnd");
+    return 0;
+}
+
 int rccl_broadcast(void* comm, void* buf, size_t bytes, int root, hipStream_t stream) {
     if (int rc = need_rccl()) return rc;
     RC_CALL(rccl().Broadcast(buf, buf, bytes, ncclUint8, root, (ncclComm_t) comm, stream),

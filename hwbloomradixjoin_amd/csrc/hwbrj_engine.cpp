@@ -209,6 +209,8 @@ bool plan_geometry(const bloom_filter_args_t* a, uint64_t nR, Geometry* g, std::
         while (l2s < 6 && (rper >> l2s) > 1536) l2s++;
     } else if (g->sub_shift > 0 && g->log2F + 6 >= 14) {
         l2s = g->log2F >= 14 ? 0 : 14 - g->log2F;
+        if (dev_knobs().l2sub && g->log2F + dev_knobs().l2sub >= 14)  // dev A/B: more, smaller jobs
+            l2s = std::min<uint32_t>(6, dev_knobs().l2sub);
     } else {
         while (l2s < 6 && (rper >> l2s) > 4096) l2s++;
     }
@@ -255,6 +257,7 @@ const DevKnobs& dev_knobs() {
         d.maxf      = u("HWBRJ_DEV_MAXF");
         d.scwpc     = u("HWBRJ_DEV_SCWPC");
         if (getenv("HWBRJ_DEV_EVFLAGS")) d.evflags = (int) u("HWBRJ_DEV_EVFLAGS");
+        d.l2sub     = u("HWBRJ_DEV_L2SUB");
 #endif
         return d;
     }();
@@ -273,6 +276,7 @@ std::string dev_knobs_string() {
     if (d.maxf) add("HWBRJ_DEV_MAXF=" + std::to_string(d.maxf));
     if (d.scwpc) add("HWBRJ_DEV_SCWPC=" + std::to_string(d.scwpc));
     if (d.evflags >= 0) add("HWBRJ_DEV_EVFLAGS=" + std::to_string(d.evflags));
+    if (d.l2sub) add("HWBRJ_DEV_L2SUB=" + std::to_string(d.l2sub));
     return r;
 }
 

@@ -153,6 +153,8 @@ void    set_last_error(const std::string& s);
 // an error code with the message in set_last_error.
 int rccl_broadcast(void* comm, void* buf, size_t bytes, int root, hipStream_t stream);
 int rccl_agree_status(void* comm, int world, int rank, int rc, hipStream_t stream, DevBuf* tmp);
+class Engine;
+int rccl_alltoall_u64_dev(Engine* e, const uint64_t* d_send, uint64_t* d_recv, uint64_t n);
 
 // glibc's rand() (stdlib/random_r.c TYPE_3) with private state (hwbrj_gen.cpp).
 struct GlibcRand {

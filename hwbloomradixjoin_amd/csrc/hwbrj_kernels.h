@@ -198,6 +198,9 @@ void   launch_pj_item_tables(const uint32_t* tab, uint32_t pairs, uint32_t W, co
                              uint32_t* jobs, hipStream_t st);
 void   launch_pj_gather(const uint32_t* pool, const uint32_t* list, uint32_t n, void* out, uint32_t* ent,
                         hipStream_t st);
+// the native transport's per-destination counts message (k_pj_counts), built on the device
+void   launch_pj_counts(const uint32_t* starts, const uint64_t* bound, uint32_t W, uint32_t QL, uint32_t NC,
+                        uint64_t status, uint64_t extra, uint64_t* out, hipStream_t st);
 void   launch_pj_relist(const uint32_t* rent, const int64_t* tab, uint32_t pairs, uint32_t* list,
                         hipStream_t st);
 void   launch_pj_surv_pack(const uint32_t* surv, const uint64_t* region, const uint32_t* tot,
@@ -224,6 +227,7 @@ struct DevKnobs {
     uint32_t maxf = 0;           // HWBRJ_DEV_MAXF: cap on the partition count F
     uint32_t scwpc = 0;          // HWBRJ_DEV_SCWPC: scatter workgroups per CU
     int      evflags = -1;       // HWBRJ_DEV_EVFLAGS: phase-event creation flags
+    uint32_t l2sub = 0;          // HWBRJ_DEV_L2SUB: join sub-partition bits (code-digit joins)
 };
 const DevKnobs& dev_knobs();
 // "name=value" of every dev knob that is set ("" in product builds); hwbrj_version() appends it

@@ -3644,6 +3644,28 @@ void launch_pj_item_tables(const uint32_t* tab, uint32_t pairs, uint32_t W, cons
     if (pairs) k_pj_item_tables<<<pairs, 256, 0, st>>>(tab, W, rcnt, wscan, NSUB, ibase, icnt, ioff, jobs);
 }
 
+// The native transport's counts message to every destination j (out[j NC .. (j + 1) NC)), packed on
+// the device so no host read precedes its exchange: the item (or chunk) counts of j's QL partitions
+// from starts[], then words = bound[(j + 1) QL] - bound[j QL] when bound is given (survivors), else
+// starts[j QL] (the position of j's first chunk), then this rank's status and `extra`.
+__global__ void k_pj_counts(const uint32_t* __restrict__ starts, const uint64_t* __restrict__ bound, uint32_t W,
+                            uint32_t QL, uint32_t NC, uint64_t status, uint64_t extra, uint64_t* __restrict__ out) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= W * NC) return;
+    const uint32_t j = t / NC, i = t % NC;
+    uint64_t v;
+    if (i < QL) v = starts[j * QL + i + 1] - starts[j * QL + i];
+    else if (i == QL) v = bound ? bound[(j + 1) * QL] - bound[j * QL] : starts[j * QL];
+    else if (i == QL + 1) v = status;
+    else v = extra;
+    out[t] = v;
+}
+
+void launch_pj_counts(const uint32_t* starts, const uint64_t* bound, uint32_t W, uint32_t QL, uint32_t NC,
+                      uint64_t status, uint64_t extra, uint64_t* out, hipStream_t st) {
+    k_pj_counts<<<(W * NC + 255) / 256, 256, 0, st>>>(starts, bound, W, QL, NC, status, extra, out);
+}
+
 void launch_pj_gather(const uint32_t* pool, const uint32_t* list, uint32_t n, void* out, uint32_t* ent,
                       hipStream_t st) {
     if (n) k_pj_gather<<<4096, 256, 0, st>>>(pool, list, n, (uint4*) out, ent);

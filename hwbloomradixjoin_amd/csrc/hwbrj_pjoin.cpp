@@ -17,6 +17,11 @@
 // join stream). Host tables between them are built from counts the host has waited for. Before
 // every collective the ranks agree on their statuses, so a rank that fails alone (an oversized
 // shard, an allocation) makes every rank return instead of leaving its peers in the collective.
+// The native transport waits on the host three times per join (the R counts, the survivor counts,
+// the result): each counts message is packed on the device and exchanged on the join stream, and
+// every receive buffer is allocated at its worst case before the counts step that could size it,
+// so its status rides in that step's message and no separate agreement is needed (the callback
+// path: a starts read and a counts all-to-all per step, plus three agreements).
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -144,7 +149,8 @@ int Engine::join_partitioned(const hwbrj_exchange_t* x, int rank, int world, con
         }
         return peers(r.data(), 1, rc);
     };
-    const uint32_t NC = QL + 2;  // counts exchanges: QL partition counts, a total, the status
+    // counts exchanges: QL partition counts, a total, the status, this rank's |S| shard
+    const uint32_t NC = QL + 3;
     std::vector<double> ms(8, 0.0);
     auto lap = [&, t = std::chrono::steady_clock::now()](int k) mutable {
         const auto n = std::chrono::steady_clock::now();
@@ -159,11 +165,48 @@ int Engine::join_partitioned(const hwbrj_exchange_t* x, int rank, int world, con
     uint64_t* d_result   = nullptr;
     uint64_t* d_filtered = nullptr;
     std::vector<uint32_t> ls(F + 1, 0), isS(F + 1, 0);
-    std::vector<uint64_t> scnt((size_t) W * NC, 0), rcnt((size_t) W * NC, 0);
+    std::vector<uint64_t> scnt((size_t) W * NC, 0), rcnt((size_t) W * NC, 0), bnd(F + 1, 0);
     std::vector<uint64_t> soff(W), sbytes(W), roff(W), rbytes(W);
     uint64_t              RC = 0, sweeps = 0, RI = 0, RW = 0;
+    uint64_t              RCmax = 0, RImax = 0, RWmax = 0;  // native: receive capacities (worst case)
     std::vector<uint64_t> ritems(W), rwords(W), sofs;
     ScatterParams sp{};
+    // The native transport's counts step: the message to every destination is packed on the device
+    // (k_pj_counts; or, after a local failure, just the status from the host), exchanged by RCCL on
+    // the join stream and read back together with the partition starts: ONE host wait per exchange
+    // step, where the callback path needs a read of the starts, then a counts all-to-all. Every
+    // receive buffer of the native path is allocated before the exchange at its worst-case size
+    // (memory is plentiful, 288 GB per GPU), so no allocation can fail alone after a counts step
+    // and the status agreements before the data all-to-alls are not needed.
+    std::vector<uint64_t> hstat;
+    auto native_counts = [&](const uint32_t* d_starts, const uint64_t* d_bound, int rc_local, uint64_t extra,
+                             uint32_t* h_starts, uint64_t* h_bound) -> int {
+        const uint64_t n  = (uint64_t) W * NC;
+        uint64_t*      ds = xcnt()->as<uint64_t>();
+        uint64_t*      dr = ds + n;
+        if (rc_local == 0) {
+            launch_pj_counts(d_starts, d_bound, W, QL, NC, 0, extra, ds, stream);
+        } else {
+            hstat.assign(n, 0);
+            for (uint32_t j = 0; j < W; j++) hstat[(uint64_t) j * NC + QL + 1] = (uint64_t) (uint32_t) rc_local;
+            PJ_CHECK(hipMemcpyAsync(ds, hstat.data(), n * 8, hipMemcpyHostToDevice, stream));
+        }
+        if (rccl_alltoall_u64_dev(this, ds, dr, NC) != 0) {
+            set_last_error("exchange failed: counts");
+            return 20;
+        }
+        PJ_CHECK(hipMemcpyAsync(rcnt.data(), dr, n * 8, hipMemcpyDeviceToHost, stream));
+        if (rc_local == 0) {
+            PJ_CHECK(hipMemcpyAsync(h_starts, d_starts, (F + 1) * 4, hipMemcpyDeviceToHost, stream));
+            if (h_bound) PJ_CHECK(hipMemcpyAsync(h_bound, d_bound, (F + 1) * 8, hipMemcpyDeviceToHost, stream));
+        }
+        PJ_CHECK(hipStreamSynchronize(stream));
+        return 0;
+    };
+    if (native && !xcnt()->ensure((size_t) 2 * W * NC * 8)) {  // (tiny; before any collective)
+        set_last_error("hipMalloc failed (exchange counts)");
+        return 4;
+    }
 
     // ------------------------------------------------------------- 1. R shard: local partitions
     const int rc1 = [&]() -> int {
@@ -189,6 +232,19 @@ int Engine::join_partitioned(const hwbrj_exchange_t* x, int rank, int world, con
         ok &= surv.ensure(nseg * LS * 128) && survcnt.ensure(items_max * NSUB * 4) && survoff.ensure(items_max * NSUB * 4);
         ok &= small.ensure(128 + 64 * 128) && colR.ensure(F * 12) && colS.ensure(F * 12);
         ok &= jtask.ensure((size_t) join_extra_tasks() * 8) && jparts.ensure((size_t) (2 * F * NSUB + 1) * 4);
+        if (native) {
+            // R received by this rank: its QL partitions' chunks from every source, each source
+            // region holding at most one partial chunk per partition
+            RCmax = nR_total / 32 + (uint64_t) W * G * QL + QL + 1;
+            const uint64_t sw_max = RCmax / BSW + QL + 1;
+            ok &= pjList.ensure(RCmax * 4) && rjoin.ensure(sw_max * SLOT * 4) && rrun.ensure(2 * sw_max * NSUB * 4);
+            ok &= pjTab.ensure((size_t) 4 * QL * W * 8) && pjLstart.ensure((QL + 1) * 4) && pjSweep.ensure((QL + 1) * 4);
+            recvC = x->buffer(x->ctx, HWBRJ_PJ_R_RECV, RCmax * 128 + 16);
+            recvE = (uint32_t*) x->buffer(x->ctx, HWBRJ_PJ_R_RECV_ENT, RCmax * 4);
+            sendC = x->buffer(x->ctx, HWBRJ_PJ_R_SEND, std::max<uint64_t>(16, LR * 128));
+            sendE = (uint32_t*) x->buffer(x->ctx, HWBRJ_PJ_R_SEND_ENT, std::max<uint64_t>(16, LR * 4));
+            ok &= recvC && recvE && sendC && sendE;
+        }
         if (!ok) {
             set_last_error("hipMalloc failed (device memory)");
             return 4;
@@ -219,6 +275,7 @@ int Engine::join_partitioned(const hwbrj_exchange_t* x, int rank, int world, con
         launch_list_fill(metaR.as<uint32_t>(), usedR.as<uint32_t>(), capR, g.log2F, wgqoR.as<uint32_t>(),
                          colR.as<uint32_t>() + 2 * F, colR.as<uint64_t>(), (uint32_t) BSW, 1, lstartR.as<uint32_t>(),
                          estartR.as<uint64_t>(), istartR.as<uint32_t>(), listR.as<uint32_t>(), G, stream);
+        if (native) return 0;  // (the counts message is built on the device)
         PJ_CHECK(hipMemcpyAsync(ls.data(), lstartR.p, (F + 1) * 4, hipMemcpyDeviceToHost, stream));
         PJ_CHECK(hipStreamSynchronize(stream));
         const uint32_t nch = ls[F];
@@ -234,15 +291,24 @@ int Engine::join_partitioned(const hwbrj_exchange_t* x, int rank, int world, con
         // per destination j: chunks of its QL partitions, then the position of its block's first chunk
         for (uint32_t j = 0; j < W; j++) {
             for (uint32_t i = 0; i < QL; i++) scnt[j * NC + i] = ls[j * QL + i + 1] - ls[j * QL + i];
-            scnt[j * NC + QL] = ls[j * QL];
+            scnt[j * NC + QL]     = ls[j * QL];
+            scnt[j * NC + QL + 2] = nS;
         }
         return drain();
     }();
     lap(0);
     // ------------------------------------------------------------- 2. R exchange
-    for (uint32_t j = 0; j < W; j++) scnt[j * NC + QL + 1] = (uint64_t) (uint32_t) rc1;
-    PJ_XCHG(x->alltoall_u64(x->ctx, scnt.data(), rcnt.data(), NC), "R chunk counts");
-    if (const int rc = peers(rcnt.data() + QL + 1, NC, rc1)) return rc;
+    if (native) {
+        if (const int rc = native_counts(lstartR.as<uint32_t>(), nullptr, rc1, nS, ls.data(), nullptr)) return rc;
+        if (const int rc = peers(rcnt.data() + QL + 1, NC, rc1)) return rc;
+        PJ_STAGE("R scatter");
+        launch_pj_gather(poolR.as<uint32_t>(), listR.as<uint32_t>(), ls[F], sendC, sendE, stream);
+        PJ_STAGE("k_pj_gather");
+    } else {
+        for (uint32_t j = 0; j < W; j++) scnt[j * NC + QL + 1] = (uint64_t) (uint32_t) rc1;
+        PJ_XCHG(x->alltoall_u64(x->ctx, scnt.data(), rcnt.data(), NC), "R chunk counts");
+        if (const int rc = peers(rcnt.data() + QL + 1, NC, rc1)) return rc;
+    }
     const int rc2 = [&]() -> int {
         for (uint32_t j = 0; j < W; j++) {
             soff[j]   = (uint64_t) ls[j * QL] * 128;
@@ -253,6 +319,13 @@ int Engine::join_partitioned(const hwbrj_exchange_t* x, int rank, int world, con
             rbytes[j] = c * 128;
             RC += c;
         }
+        if (native) {  // (allocated at RCmax before the counts step)
+            if (RC > RCmax) {
+                set_last_error("partitioned join: received R chunks above their bound");
+                return 21;
+            }
+            return 0;
+        }
         recvC = x->buffer(x->ctx, HWBRJ_PJ_R_RECV, std::max<uint64_t>(16, RC * 128 + 16));
         recvE = (uint32_t*) x->buffer(x->ctx, HWBRJ_PJ_R_RECV_ENT, std::max<uint64_t>(16, RC * 4));
         if (!recvC || !recvE) {
@@ -261,7 +334,11 @@ int Engine::join_partitioned(const hwbrj_exchange_t* x, int rank, int world, con
         }
         return 0;
     }();
-    if (const int rc = agree(rc2)) return rc;
+    if (native) {
+        if (rc2) return rc2;  // (a broken bound: no rank can get here but by a bug)
+    } else if (const int rc = agree(rc2)) {
+        return rc;
+    }
     PJ_XCHG(x->alltoallv(x->ctx, HWBRJ_PJ_R_SEND, soff.data(), sbytes.data(), HWBRJ_PJ_R_RECV, roff.data(), rbytes.data()),
             "R chunks");
     for (uint32_t j = 0; j < W; j++) soff[j] /= 32, sbytes[j] /= 32, roff[j] /= 32, rbytes[j] /= 32;
@@ -346,13 +423,21 @@ int Engine::join_partitioned(const hwbrj_exchange_t* x, int rank, int world, con
         return drain();
     }();
     lap(2);
-    if (const int rc = agree(rc3)) return rc;
+    // (native: every buffer of this step was allocated before the counts step, so it fails alike
+    // or not at all, except under HWBRJ_PJ_CHECK's host checks, which then agree as the callback
+    // path does)
+    if (!native || pj_check_on()) {
+        if (const int rc = agree(rc3)) return rc;
+    } else if (rc3) {
+        return rc3;
+    }
     // ------------------------------------------------------------- 4. the whole filter on every rank
     if (slice_mode && W > 1)
         PJ_XCHG(x->allgather(x->ctx, HWBRJ_PJ_SLICES, (uint64_t) QL * nseg * g.seg_words * 4), "filter slices");
     lap(3);
     // ------------------------------------------------------------- 5. S shard: partition, probe
     uint32_t I = 0;
+    const uint32_t items_max = (uint32_t) ((LS / CH + F + 1) * nseg);
     const int rc5 = [&]() -> int {
         sp.src        = dS;
         sp.n          = nS;
@@ -389,8 +474,7 @@ int Engine::join_partitioned(const hwbrj_exchange_t* x, int rank, int world, con
         // ------------------------------------------------------------- 6. survivor exchange
         // item tables on the device (k_pj_items: regions, survivor totals, their scan); the host
         // reads only the item starts and the scan at every partition's first item
-        const uint32_t items_max = (uint32_t) ((LS / CH + F + 1) * nseg);
-        const uint32_t nbk       = items_max / 1024 + 1;
+        const uint32_t nbk = items_max / 1024 + 1;
         if (!pjRegion.ensure((uint64_t) items_max * 8 + 8) || !pjTot.ensure((uint64_t) items_max * 4 + 4) ||
             !pjSoff.ensure((uint64_t) items_max * 8 + 8) || !pjBsum.ensure((uint64_t) nbk * 8) ||
             !pjBound.ensure((uint64_t) (F + 1) * 8)) {
@@ -400,12 +484,44 @@ int Engine::join_partitioned(const hwbrj_exchange_t* x, int rank, int world, con
         launch_pj_items(istartS.as<uint32_t>(), lstartS.as<uint32_t>(), survcnt.as<uint32_t>(), items_max, F, nseg,
                         CH, LS * 32, NSUB, pjRegion.as<uint64_t>(), pjTot.as<uint32_t>(), pjBsum.as<uint64_t>(),
                         pjSoff.as<uint64_t>(), pjBound.as<uint64_t>(), stream);
-        std::vector<uint64_t> bnd(F + 1);
+        if (native) {
+            // every buffer the survivor exchange and the owner's join need, at its worst case:
+            // survivors sent <= this shard's S tuples; received <= every shard's (their |S| came
+            // with the R counts); items and their run tables likewise
+            uint64_t nS_all = 0;
+            RImax = 0;
+            for (uint32_t j = 0; j < W; j++) {
+                const uint64_t nSj = rcnt[(uint64_t) j * NC + QL + 2];
+                nS_all += nSj;
+                RImax += ((uint64_t) G * pj_region_cap(nSj, G, F) / CH + F + 1) * nseg;
+            }
+            RWmax = nS_all;
+            const uint32_t NJ  = QL * NSUB;
+            bool ok = true;
+            sendS = (uint32_t*) x->buffer(x->ctx, HWBRJ_PJ_S_SEND, std::max<uint64_t>(16, nS * 4));
+            sendM = (uint32_t*) x->buffer(x->ctx, HWBRJ_PJ_M_SEND, std::max<uint64_t>(16, (uint64_t) items_max * NSUB * 4));
+            recvS = (uint32_t*) x->buffer(x->ctx, HWBRJ_PJ_S_RECV, std::max<uint64_t>(16, RWmax * 4));
+            recvM = (uint32_t*) x->buffer(x->ctx, HWBRJ_PJ_M_RECV, std::max<uint64_t>(16, RImax * NSUB * 4));
+            ok &= sendS && sendM && recvS && recvM;
+            ok &= pjIbase.ensure(std::max<uint64_t>(16, RImax * 8)) && pjCnt.ensure(std::max<uint64_t>(16, RImax * NSUB * 4)) &&
+                  pjOff.ensure(std::max<uint64_t>(16, RImax * NSUB * 4)) && pjJobs.ensure((uint64_t) NJ * 4) &&
+                  pjWtot.ensure(std::max<uint64_t>(16, RImax * 4)) && pjWscan.ensure((RImax + 1) * 8) &&
+                  pjBsum.ensure((uint64_t) std::max<uint64_t>(nbk, RImax / 1024 + 1) * 8) &&
+                  pjTab2.ensure((size_t) 3 * QL * W * 4) && pjIstart.ensure((QL + 1) * 4);
+            if (!ok) {
+                set_last_error("hipMalloc failed (device memory)");
+                return 4;
+            }
+            return 0;  // (the counts message is built on the device)
+        }
         PJ_CHECK(hipMemcpyAsync(isS.data(), istartS.p, (F + 1) * 4, hipMemcpyDeviceToHost, stream));
         PJ_CHECK(hipMemcpyAsync(bnd.data(), pjBound.p, (F + 1) * 8, hipMemcpyDeviceToHost, stream));
         PJ_CHECK(hipStreamSynchronize(stream));
+        return 0;
+    }();
+    // survivors of this shard packed per destination (after the starts have reached the host)
+    auto pack_survivors = [&]() -> int {
         I = isS[F];
-        lap(4);
         sofs = bnd;  // (sofs at partition starts: all the host needs)
         sendS = (uint32_t*) x->buffer(x->ctx, HWBRJ_PJ_S_SEND, std::max<uint64_t>(16, bnd[F] * 4));
         sendM = (uint32_t*) x->buffer(x->ctx, HWBRJ_PJ_M_SEND, std::max<uint64_t>(16, (uint64_t) I * NSUB * 4));
@@ -430,17 +546,30 @@ int Engine::join_partitioned(const hwbrj_exchange_t* x, int rank, int world, con
                             I, sendS, stream);
         PJ_STAGE("k_pj_surv_pack");
         if (I) PJ_CHECK(hipMemcpyAsync(sendM, survcnt.p, (size_t) I * NSUB * 4, hipMemcpyDeviceToDevice, stream));
-        // per destination j: items of each of its partitions, then its survivor words
-        for (uint32_t j = 0; j < W; j++) {
-            for (uint32_t i = 0; i < QL; i++) scnt[j * NC + i] = isS[j * QL + i + 1] - isS[j * QL + i];
-            scnt[j * NC + QL] = bnd[(j + 1) * QL] - bnd[j * QL];
-        }
-        return drain();
-    }();
+        return 0;
+    };
     lap(4);
-    for (uint32_t j = 0; j < W; j++) scnt[j * NC + QL + 1] = (uint64_t) (uint32_t) rc5;
-    PJ_XCHG(x->alltoall_u64(x->ctx, scnt.data(), rcnt.data(), NC), "survivor counts");
-    if (const int rc = peers(rcnt.data() + QL + 1, NC, rc5)) return rc;
+    if (native) {
+        if (const int rc = native_counts(istartS.as<uint32_t>(), pjBound.as<uint64_t>(), rc5, 0, isS.data(), bnd.data()))
+            return rc;
+        if (const int rc = peers(rcnt.data() + QL + 1, NC, rc5)) return rc;
+        // (what follows allocates nothing: a failure here is a bug or a broken device, and returns)
+        if (const int rc = pack_survivors()) return rc;
+    } else {
+        int rc5b = rc5 ? rc5 : pack_survivors();
+        if (!rc5b) {
+            // per destination j: items of each of its partitions, then its survivor words
+            for (uint32_t j = 0; j < W; j++) {
+                for (uint32_t i = 0; i < QL; i++) scnt[j * NC + i] = isS[j * QL + i + 1] - isS[j * QL + i];
+                scnt[j * NC + QL] = bnd[(j + 1) * QL] - bnd[j * QL];
+            }
+            rc5b = drain();
+        }
+        for (uint32_t j = 0; j < W; j++) scnt[j * NC + QL + 1] = (uint64_t) (uint32_t) rc5b;
+        PJ_XCHG(x->alltoall_u64(x->ctx, scnt.data(), rcnt.data(), NC), "survivor counts");
+        if (const int rc = peers(rcnt.data() + QL + 1, NC, rc5b)) return rc;
+    }
+    lap(4);
     const int rc6 = [&]() -> int {
         for (uint32_t j = 0; j < W; j++) {
             uint64_t c = 0;
@@ -450,6 +579,13 @@ int Engine::join_partitioned(const hwbrj_exchange_t* x, int rank, int world, con
             RI += c;
             RW += rwords[j];
         }
+        if (native) {  // (allocated at RImax / RWmax before the counts step)
+            if (RI > RImax || RW > RWmax) {
+                set_last_error("partitioned join: received survivors above their bound");
+                return 21;
+            }
+            return 0;
+        }
         recvS = (uint32_t*) x->buffer(x->ctx, HWBRJ_PJ_S_RECV, std::max<uint64_t>(16, RW * 4));
         recvM = (uint32_t*) x->buffer(x->ctx, HWBRJ_PJ_M_RECV, std::max<uint64_t>(16, RI * NSUB * 4));
         if (!recvS || !recvM) {
@@ -458,7 +594,11 @@ int Engine::join_partitioned(const hwbrj_exchange_t* x, int rank, int world, con
         }
         return 0;
     }();
-    if (const int rc = agree(rc6)) return rc;
+    if (native) {
+        if (rc6) return rc6;
+    } else if (const int rc = agree(rc6)) {
+        return rc;
+    }
     {
         uint64_t ro = 0;
         for (uint32_t j = 0; j < W; j++) {

@@ -1,8 +1,8 @@
 """torch.distributed.run worker of tests/test_gpu_multi.py (not a test module): the partitioned
 join of the F3 relations, R and S range-sharded over the ranks, with rank argv[1] made to fail its
 shard check (hwbrj_set_test_hook HWBRJ_HOOK_PJ_FAIL_RANK, -1 = none). The ranks share the one GPU
-and exchange through torch.distributed over gloo (pjoin.TorchExchange). Exit 0 with one
-"rank r: ok filtered matches" line per rank, or 3 with the library's error on stderr."""
+and exchange through torch.distributed over gloo (pjoin.TorchExchange). Exit 0 with rank 0 printing
+"sum: ok filtered matches" (summed over the ranks), or 3 with the library's error on stderr."""
 import os
 import sys
 
@@ -34,7 +34,10 @@ def main():
     except RuntimeError as e:
         print(f"rank {rank}: {e}", file=sys.stderr, flush=True)
         sys.exit(3)
-    print(f"rank {rank}: ok {st.filtered} {st.matches}", flush=True)
+    t = torch.tensor([st.filtered, st.matches], dtype=torch.int64)
+    dist.all_reduce(t)  # (gloo: host tensors)
+    if rank == 0:
+        print(f"sum: ok {int(t[0])} {int(t[1])}", flush=True)
     dist.destroy_process_group()
 
 
