@@ -640,7 +640,6 @@ __device__ __forceinline__ void scatter_body(const ScatterParams& P) {
                 R.k[j]  = len ? ((const uint32_t*) P.src)[2 * t] : 0u;  // (len = 0: R may be empty)
                 R.jb[j] = jj;
             }
-#ifndef HWBRJ_SC_LD32  // (dev A/B: one 4-byte key load per tuple)
         } else if (SRC == SRC_TUPLES && base + kScRound <= len) {  // two tuples per 16-byte load
 #pragma unroll
             for (int h = 0; h < kScE / 2; h++) {
@@ -659,18 +658,6 @@ __device__ __forceinline__ void scatter_body(const ScatterParams& P) {
                 R.k[j] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, i < len ? i * EB : kOob, 0, 0);
                 if (HWBRJ_SC_KEEPY) R.y[j] = 0;
             }
-#else
-        } else if (SRC == SRC_TUPLES && base + kScRound <= len) {
-#pragma unroll
-            for (int j = 0; j < kScE; j++)
-                R.k[j] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, tid * EB, (base + j * kScThreads) * EB, 0);
-        } else if (SRC == SRC_TUPLES) {  // keys only (the payload is not needed by the count join)
-#pragma unroll
-            for (int j = 0; j < kScE; j++) {
-                const uint32_t i = base + j * kScThreads + tid;
-                R.k[j] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, i < len ? i * EB : kOob, 0, 0);
-            }
-#endif
         } else {
 #pragma unroll
             for (int h = 0; h < NL; h++) {
@@ -684,11 +671,7 @@ __device__ __forceinline__ void scatter_body(const ScatterParams& P) {
     auto elem = [&](const ScRaw<SRC>& R, uint32_t base, int j, uint32_t& x, uint32_t& idx) {
         if (SRC == SRC_TUPLES) {
             x   = R.k[j];
-#ifndef HWBRJ_SC_LD32  // (dev A/B: one 4-byte key load per tuple)
             idx = MODE == MODE_BASIC_POS ? base + j * kScThreads + tid : base + (j >> 1) * 2 * kScThreads + 2 * tid + (j & 1);
-#else
-            idx = base + j * kScThreads + tid;
-#endif
         } else {
             const int h = j >> 2, t = j & 3;
             x   = t == 0 ? R.v[h].x : t == 1 ? R.v[h].y : t == 2 ? R.v[h].z : R.v[h].w;
@@ -798,11 +781,9 @@ __device__ __forceinline__ void scatter_body(const ScatterParams& P) {
             } else {
                 sc_word_lds0<SRC, MODE, FMT>(x, P.g, crc_tab, w[j], q[j]);
             }
-#ifndef HWBRJ_SC_NOPINW
             // the word (CrapWow) computed here, among the CRC reads, not after the barrier where the
             // compiler would sink it (phase B is the longer one: 2.66 -> 2.56 ms at the north star)
             asm volatile("" : "+v"(w[j]));
-#endif
 #ifndef HWBRJ_SC_SB
 #define HWBRJ_SC_SB 2
 #endif
@@ -823,11 +804,9 @@ __device__ __forceinline__ void scatter_body(const ScatterParams& P) {
         hash(base, R);
         stamp(0);
         load_round(base + kScPre * kScRound, R);
-#ifndef HWBRJ_SC_NOORD
         uint32_t slot[kScE];  // ranks issued first: their returns overlap the copy-out
 #pragma unroll
         for (int j = 0; j < kScE; j++) slot[j] = atomicAdd(&fill[q[j]], 1u);
-#endif
         flush_copy();
         if (tid == 0) {
             misc[1 + par]        = 0;  // (last read by the previous round's flush_copy)
@@ -837,11 +816,7 @@ __device__ __forceinline__ void scatter_body(const ScatterParams& P) {
         bool sk = false;  // a slot >= 63: some partition reaches 64 words this round
 #pragma unroll
         for (int j = 0; j < kScE; j++) {
-#ifndef HWBRJ_SC_NOORD
             q[j] |= slot[j] << 11;
-#else
-            q[j] |= atomicAdd(&fill[q[j]], 1u) << 11;  // q | slot << 11
-#endif
             sk |= q[j] >= (63u << 11) && (q[j] & 2047u) < F;
         }
         if (__builtin_amdgcn_ballot_w64(sk) != 0 && lane == 0) misc[3 + par] = 1u;
@@ -1743,12 +1718,6 @@ constexpr int kAblProbe = HWBRJ_ABL_PROBE;
 #ifndef HWBRJ_PCO_AUX
 #define HWBRJ_PCO_AUX 0
 #endif
-#ifndef HWBRJ_PCO_SKIP  // (A/B) 1: a wave with no quad of the stage in range skips its store
-#define HWBRJ_PCO_SKIP 0
-#endif
-#ifndef HWBRJ_PRT_W0  // (A/B) 1: only wave 0 issues the run-table stores and the job-count atomic
-#define HWBRJ_PRT_W0 0
-#endif
 constexpr int kPco = HWBRJ_PCO < kPC ? HWBRJ_PCO : kPC;
 
 __device__ __forceinline__ uint32_t find_q(const uint32_t* item_start, uint32_t F, uint32_t it) {
@@ -1841,12 +1810,10 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
 #pragma unroll
         for (int k = 0; k < kPco; k++) {
             const uint32_t i = tid + k * NT;
-            if (HWBRJ_PCO_SKIP && (uint32_t) (wave * 64 + k * NT) * 16u >= nbytes) continue;  // wave-uniform
             const v4u      v = src[min(i, scap / 4 - 1)];  // reads past the stage are never stored
             __builtin_amdgcn_raw_buffer_store_b128(v, ro, i * 16, 0, HWBRJ_PCO_AUX);
         }
         }
-        if (HWBRJ_PRT_W0 && wave != 0) return;
         const uint32_t tb = prev_it == kNoItem ? 0u : NSUB * 4;  // run table (wave 0 holds it)
         const auto rc = buf_rsrc(P.surv_cnt + (uint64_t) (prev_it & ~kNoItem) * NSUB, tb);
         const auto rf = buf_rsrc(P.surv_off + (uint64_t) (prev_it & ~kNoItem) * NSUB, tb);
@@ -1962,18 +1929,6 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
                 // shared garbage slot). Otherwise no scratch write at all (high selectivity: the
                 // words are ranked one by one, and 12 LDS writes per thread would buy nothing)
                 if (!PAY && kScrCap > 0 && nsv <= kScrCap && kAblProbe != 1) {  // wave-uniform
-#ifdef HWBRJ_PR_BALLOT  // (dev A/B: slot-major compaction by wave ballots)
-                    uint32_t at0 = 0;
-#pragma unroll
-                    for (int i = 0; i < NW; i++) {
-                        const bool     ok  = (pass >> i) & 1u;
-                        const uint64_t m   = __builtin_amdgcn_ballot_w64(ok);
-                        const uint32_t pre = __builtin_amdgcn_mbcnt_hi((uint32_t) (m >> 32),
-                                                                       __builtin_amdgcn_mbcnt_lo((uint32_t) m, 0u));
-                        *(ok ? &scr[at0 + pre] : &scrdum[lane]) = sweep_word(Sc, i >> 2, i & 3);  // others: garbage slot
-                        at0 += (uint32_t) __builtin_popcountll(m);
-                    }
-#else
                     // lane-major: this lane's survivors from its exclusive prefix (the scan above) on.
                     // Word i goes to byte address dmy + t_i * x (t_i its pass bit, x = the next
                     // survivor slot - dmy, dmy the lane's garbage slot below the scratch): one bfe,
@@ -1986,7 +1941,6 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
                         lds_store_u32(mad_u24(t, x, dmy), sweep_word(Sc, i >> 2, i & 3));
                         x = shl_add(t, 2, x);
                     }
-#endif
                 }
             } else {
 #pragma unroll
@@ -2355,7 +2309,6 @@ __device__ __forceinline__ uint32_t join_slot(uint32_t v) {
 // in the first bucket from its home that had a free slot when it was inserted. Slots are never
 // freed, so every bucket before it stays full, and a lookup can stop at the first bucket that
 // has a free slot (every copy of a key lies at or before it).
-#ifndef HWBRJ_JSLOT1
 __device__ __forceinline__ uint32_t join_count(const uint32_t* keys, uint32_t v) {
     uint32_t b = join_slot(v) & ~3u, cnt = 0;
     for (;;) {
@@ -2377,21 +2330,6 @@ __device__ __forceinline__ void join_insert(uint32_t* keys, uint32_t v) {
         b = (b + 4u) & (kJoinT - 1u);
     }
 }
-#else  // (dev A/B: slot-by-slot linear probing)
-__device__ __forceinline__ uint32_t join_count(const uint32_t* keys, uint32_t v) {
-    uint32_t h = join_slot(v), cnt = 0;
-    for (uint32_t k = keys[h]; k != kEmpty; k = keys[h]) {
-        cnt += k == v;
-        h = (h + 1u) & (kJoinT - 1u);
-    }
-    return cnt;
-}
-
-__device__ __forceinline__ void join_insert(uint32_t* keys, uint32_t v) {
-    uint32_t h = join_slot(v);
-    while (atomicCAS(&keys[h], kEmpty, v) != kEmpty) h = (h + 1u) & (kJoinT - 1u);
-}
-#endif
 
 // Join tasks. A (q, sub) job whose survivors exceed kJoinTaskSurv (probe-side skew, e.g. the
 // hot keys of a Zipf S) is split into parts over q's probe items; every part rebuilds the job's
@@ -2567,33 +2505,23 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
 #endif
     constexpr int FR = HWBRJ_JFR, FW = HWBRJ_JFW;
     const uint32_t nRd = w1 - w0, nSd = i1 - i0;
-#ifdef HWBRJ_NOJFUSE
-    if (false) {
-#else
     if (!hashed && nRd <= (uint32_t) (kJoinWaves * FR) && nSd <= kJoinDesc) {
-#endif
         // Fused bitmap path (every job of the north star): both descriptor sets in one phase, then
         // the loads of all R runs and of the first survivor runs are issued before any is used, so
         // a job costs two memory latencies (descriptors, data) instead of one per batch.
         for (uint32_t i = tid; i < kJoinWords / 4; i += kJoinThreads) ((uint4*) tab)[i] = make_uint4(0, 0, 0, 0);
         if (tid == 0) dupflag = 0;
-#ifndef HWBRJ_JDUPRTN
         uint32_t rc = 0;
-#endif
         if ((uint32_t) tid < nRd) {
             const uint64_t r = (uint64_t) (w0 + tid) * NSUB + s;
             rcnt[tid]        = P.r_cnt[r];
             rbase[tid]       = (uint64_t) (w0 + tid) * P.slot + P.r_off[r];
-#ifndef HWBRJ_JDUPRTN
             rc = rcnt[tid];
-#endif
         }
-#ifndef HWBRJ_JDUPRTN
         if (wave == 0) {  // the job's R keys (nRd <= 64: every R descriptor is in wave 0)
             const uint32_t t = __builtin_amdgcn_readlane(wave_incl_scan_dpp(rc), 63);
             if (lane == 0) npieces = t;
         }
-#endif
         if ((uint32_t) tid < nSd) {
             const uint32_t it    = i0 + tid;
             const uint32_t local = it - qi0;
@@ -2635,17 +2563,9 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
                 sv[r][j]         = o < sn[r] ? P.surv[bb + o] : 0u;
             }
         }
-#ifndef HWBRJ_JDUPRTN
         // bits set without returns (no wave waits on them); a duplicate R key shows as fewer set
         // bits than the job's R keys (popcount after the barrier)
         auto set = [&](uint32_t x) { __hip_atomic_fetch_or(&tab[x >> 5], 1u << (x & 31u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); };
-#else
-        uint32_t dup = 0;
-        auto     set = [&](uint32_t x) {
-            const uint32_t bit = 1u << (x & 31u);
-            dup |= atomicOr(&tab[x >> 5], bit) & bit;
-        };
-#endif
 #pragma unroll
         for (int r = 0; r < FR; r++) {
 #pragma unroll
@@ -2656,7 +2576,6 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
                 tail_run(P.r_codes, bb, 64u * FW, rn[r], set);
             }
         }
-#ifndef HWBRJ_JDUPRTN
         __syncthreads();
         {
             uint32_t pc = 0;
@@ -2669,11 +2588,6 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
         }
         __syncthreads();
         hashed = dupflag != npieces;  // uniform
-#else
-        if (dup) dupflag = 1;
-        __syncthreads();
-        hashed = dupflag != 0;  // uniform
-#endif
         if (!hashed) {
             probe_begin();
             auto test = [&](uint32_t x) { cnt += (tab[x >> 5] >> (x & 31u)) & 1u; };
@@ -3967,30 +3881,7 @@ const char* kernel_build_knobs() {
         num("HWBRJ_ABL_PROBE", HWBRJ_ABL_PROBE, 0);
         num("HWBRJ_PCO", HWBRJ_PCO, 1);
         num("HWBRJ_PCO_AUX", HWBRJ_PCO_AUX, 0);
-        num("HWBRJ_PCO_SKIP", HWBRJ_PCO_SKIP, 0);
-        num("HWBRJ_PRT_W0", HWBRJ_PRT_W0, 0);
 #define HWBRJ_FLAG_KNOB(X) flag(#X)
-#ifdef HWBRJ_SC_LD32
-        HWBRJ_FLAG_KNOB(HWBRJ_SC_LD32);
-#endif
-#ifdef HWBRJ_SC_NOORD
-        HWBRJ_FLAG_KNOB(HWBRJ_SC_NOORD);
-#endif
-#ifdef HWBRJ_SC_NOPINW
-        HWBRJ_FLAG_KNOB(HWBRJ_SC_NOPINW);
-#endif
-#ifdef HWBRJ_PR_BALLOT
-        HWBRJ_FLAG_KNOB(HWBRJ_PR_BALLOT);
-#endif
-#ifdef HWBRJ_JSLOT1
-        HWBRJ_FLAG_KNOB(HWBRJ_JSLOT1);
-#endif
-#ifdef HWBRJ_NOJFUSE
-        HWBRJ_FLAG_KNOB(HWBRJ_NOJFUSE);
-#endif
-#ifdef HWBRJ_JDUPRTN
-        HWBRJ_FLAG_KNOB(HWBRJ_JDUPRTN);
-#endif
 #ifdef HWBRJ_STAMPS
         HWBRJ_FLAG_KNOB(HWBRJ_STAMPS);
 #endif
