@@ -2286,14 +2286,17 @@ void launch_probe_bitj(const ProbeParams& p, uint32_t grid, hipStream_t st) {
 //    R keys; survivors count equal keys (S re-streamed per piece).
 // Survivor runs of (q, s) -- one per probe item of q, written in place by k_probe -- are taken a
 // wave per run, several runs in flight per wave.
-constexpr int      kJoinThreads = 256;
+#ifndef HWBRJ_JT
+#define HWBRJ_JT 256  // threads per join workgroup (A/B)
+#endif
+constexpr int      kJoinThreads = HWBRJ_JT;
 constexpr int      kJoinWaves   = kJoinThreads / 64;
 constexpr uint32_t kJoinBmLog2  = 18;                  // bitmap path: v < 2^18
 constexpr uint32_t kJoinWords   = 1u << (kJoinBmLog2 - 5);  // 8192 LDS words (32 KiB)
 constexpr uint32_t kJoinLog2T   = 13;                  // hash path: 8192 slots in the same words
 constexpr uint32_t kJoinT       = 1u << kJoinLog2T;
 constexpr uint32_t kJoinPiece   = kJoinT / 2;
-constexpr uint32_t kJoinDesc    = kJoinThreads;        // run descriptors per batch
+constexpr uint32_t kJoinDesc    = 256;                 // run descriptors per batch
 #ifndef HWBRJ_JTU
 #define HWBRJ_JTU 8
 #endif
@@ -3872,6 +3875,7 @@ const char* kernel_build_knobs() {
         num("HWBRJ_PR_NT", HWBRJ_PR_NT, 0);
         num("HWBRJ_SCRK", HWBRJ_SCRK, 256);
         num("HWBRJ_JTU", HWBRJ_JTU, 8);
+        num("HWBRJ_JT", HWBRJ_JT, 256);
         num("HWBRJ_JRR", HWBRJ_JRR, 4);
         num("HWBRJ_JRW", HWBRJ_JRW, 4);
         num("HWBRJ_JSR", HWBRJ_JSR, 8);
