@@ -74,14 +74,21 @@ def parse():
     return ap.parse_args()
 
 
-def modeled_bytes(nR: int, nS: int, filtered: int, m: int, word_bytes: float) -> dict:
+def join_key_bytes(st) -> float:
+    """Bytes per join key between build/probe and k_join: 3 when v = code >> hash_shift fits 24
+    bits (hash_shift = log2(F) + log2(subparts) >= 8 where the partition digit is a code digit, i.e.
+    not the slice-basic mode 2; hwbrj_kernels.h join_pack3), else 4."""
+    return 3.0 if st.mode != 2 and st.partitions * st.subparts >= 256 else 4.0
+
+
+def modeled_bytes(nR: int, nS: int, filtered: int, m: int, word_bytes: float, key_bytes: float = 4.0) -> dict:
     """Implementation bytes beyond the algorithmic 8-byte tuple reads (reported,
-    never in the headline): partition words written and read back, survivor codes, the filter."""
+    never in the headline): partition words written and read back, survivor keys, the filter."""
     return {
         "partition_words_R": 2.0 * 4.0 * nR,          # k_scatter_r writes, k_build reads
         "partition_words_S": 2.0 * word_bytes * nS,   # k_scatter_s writes, k_probe reads
-        "join_codes_R": 2.0 * 4.0 * nR,               # k_build writes, k_join reads
-        "survivors": 2.0 * 4.0 * filtered,            # k_probe writes, k_join reads
+        "join_codes_R": 2.0 * key_bytes * nR,         # k_build writes, k_join reads
+        "survivors": 2.0 * key_bytes * filtered,      # k_probe writes, k_join reads
         "filter_slices": 2.0 * m / 8.0,               # k_build writes, k_probe loads
     }
 
@@ -257,7 +264,7 @@ def main():
                 "algorithmic_bytes": alg_bytes, "launch": "one full join (every kernel of BPRO)",
                 "launch_ms": round(dev_ms, 4),
                 "modeled_bytes": modeled_bytes(nR, nS, st.filtered, a.bloom_size if args else 0,
-                                               word_bytes),
+                                               word_bytes, join_key_bytes(st)),
                 "pmc_source": os.path.relpath(a.pmc_json, ROOT) if pm else None,
                 "pmc_library": pm.get("library") if pm else None,
                 "traffic_note": pmc_note,

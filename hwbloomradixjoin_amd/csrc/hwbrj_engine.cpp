@@ -518,6 +518,8 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     bp.run_off     = rrun.as<uint32_t>() + sweeps_max * NSUB;
     bp.ppool       = mat ? ppoolR.as<uint32_t>() : nullptr;
     bp.out_pay     = mat ? rpay.as<uint32_t>() : nullptr;
+    const bool pack3 = !mat && join_pack3(g);  // 3-byte join keys from build / probe to k_join
+    bp.pack3       = pack3 ? 1u : 0u;
     // the broadcast: rank 0 builds the slices, the other ranks only sub-partition R for the join
     // and receive them over RCCL (HWBRJ_HOOK_BCAST_NONROOT: this rank takes the non-root side, for
     // tests at world 1; value 2 zeroes the slices first, so the counts show whether k_build wrote any)
@@ -609,6 +611,7 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     pp.filtered        = d_filtered;
     pp.job_surv        = jparts.as<uint32_t>() + NJ;
     pp.surv_pos        = mat ? survpos.as<uint32_t>() : nullptr;
+    pp.pack3           = pack3 ? 1u : 0u;
     const size_t   pl_lds = probe_lds_bytes(g, nullptr, mat != nullptr);
     const uint32_t PG = (uint32_t) cus_ * (uint32_t) std::max<size_t>(1, std::min<size_t>(2, 163840 / pl_lds));
     const bool dbg_on = dbg;  // dev-only phase stamps (HWBRJ_DBG)
@@ -647,6 +650,7 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     jp.nextra          = jparts.as<uint32_t>() + 2 * NJ;
     jp.jkind           = (uint32_t) jkind;
     jp.split_surv      = test_hooks().join_split;  // (tests: force the skew split)
+    jp.r_pack3         = pack3 ? 1u : 0u;
     if (mat) {
         // (k_join_split, which leaves job_surv zero for the next join, does not run here)
         HWBRJ_CHECK(hipMemsetAsync(jparts.as<uint32_t>() + NJ, 0, (size_t) NJ * 4, stream));

@@ -37,6 +37,14 @@ struct ScatterParams {
     const CrcTables* tabs;
 };
 
+// 3-byte join keys between the build / probe and the join (BuildParams::pack3): on when the
+// join key v = code >> hash_shift fits 24 bits and the run formats are private to k_join (not the
+// materializing join, which reads codes, nor the partitioned join, which ships survivor words).
+#ifndef HWBRJ_PACK3
+#define HWBRJ_PACK3 1
+#endif
+inline bool join_pack3(const Geometry& g) { return HWBRJ_PACK3 != 0 && g.sub_shift > 0 && g.hash_shift >= 8; }
+
 struct BuildParams {
     Geometry         g;
     const CrcTables* tabs;
@@ -53,6 +61,8 @@ struct BuildParams {
     const uint32_t*  ppool;       // payloads of pool's words (materialization), or nullptr
     uint32_t*        out_pay;     // [sweeps][kBSlot]: the payloads of out_codes (ppool set)
     uint32_t         no_slices;   // 1: join runs only (the slices arrive by broadcast from rank 0)
+    uint32_t         pack3;       // 1: out_codes hold 3-byte join keys (code >> hash_shift), 4 per
+                                  // 12 bytes from the slot's byte 0 (hash_shift >= 8; not PAY)
 };
 
 struct ProbeParams {
@@ -75,6 +85,8 @@ struct ProbeParams {
     uint32_t*        wg_cnt;      // k_probe_bitj: words appended to workgroup w's region
                                   // (surv + w * surv_seg_stride)
     uint64_t*        dbg;         // dev-only: per-workgroup phase cycles (HWBRJ_DBG), or nullptr
+    uint32_t         pack3;       // 1: survivor runs hold 3-byte join keys (code >> hash_shift) at
+                                  // 3 bytes per key from the item region's byte 0 (hash_shift >= 8)
 };
 
 struct JoinParams {
@@ -103,6 +115,8 @@ struct JoinParams {
                                   // table, PRO), 1 histogram join (PRH), 2 + 16-byte compares (PRHO)
     const uint64_t* item_base;    // [items] survivor region of each item (partitioned multi-GPU
                                   // join: received runs), or nullptr (k_probe's item regions)
+    uint32_t        r_pack3;      // 1: r_codes and surv hold 3-byte join keys (BuildParams::pack3,
+                                  // ProbeParams::pack3)
 };
 
 // The materializing join (k_join_mat): R codes + payloads of the build sweeps, survivors + their

@@ -82,6 +82,18 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, uin
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int) bytes, 0x00020000);
 }
 
+// 3-byte join keys (pack3): the join needs only v = code >> hash_shift, < 2^24 when hash_shift >= 8
+// (18 bits at the north star), so the build's R runs and the probe's staged survivor runs store
+// 4 keys per 12 bytes -- 25 % fewer bytes written there and read back by the join. Key i of a run
+// at byte b is the low 24 bits of the (unaligned) dword at b + 3 i; the last key's dword ends
+// inside the run's 4-byte-per-key region, so no read leaves it.
+typedef unsigned int v3u __attribute__((ext_vector_type(3)));
+__device__ __forceinline__ v3u pack3x4(v4u v, uint32_t sh) {
+    const uint32_t a = v.x >> sh, b = v.y >> sh, c = v.z >> sh, d = v.w >> sh;
+    return v3u{a | (b << 24), (b >> 8) | (c << 16), (c >> 16) | (d << 8)};
+}
+typedef uint32_t u32_unaligned __attribute__((aligned(1)));
+
 // Copy a slice segment (words, a multiple of 4) from HBM into LDS with global_load_lds (16 bytes
 // per lane, no VGPR destination), all loads issued before any wait: one latency per slice instead
 // of one per 16 KiB (a register copy loop waits for each load before its ds_write). The caller's
@@ -1655,7 +1667,14 @@ __global__ __launch_bounds__(1024) void k_build(BuildParams P) {
                 nsw++;
                 __syncthreads();  // B3: the sweep is sorted
                 uint32_t* __restrict__ dst = P.out_codes + (uint64_t) sw * kBSlot;
-                for (uint32_t i = tid; i < tot; i += blockDim.x) dst[i] = stage[i];
+                if (!PAY && P.pack3) {  // 3-byte keys: one 12-byte store per 4 codes (uniform)
+                    const uint32_t i = tid;  // kBSlot / 4 == blockDim.x quads
+                    const v4u      v = ((const v4u*) stage)[i];
+                    __builtin_amdgcn_raw_buffer_store_b96(pack3x4(v, g.hash_shift), buf_rsrc(dst, (tot + 3u) / 4u * 12u),
+                                                          i * 12u, 0, 0);
+                } else {
+                    for (uint32_t i = tid; i < tot; i += blockDim.x) dst[i] = stage[i];
+                }
             }
 #pragma unroll
             for (int jj = 0; jj < kBPQ; jj++) {
@@ -1792,6 +1811,7 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
     constexpr uint32_t kNoItem = 0x80000000u;
     uint32_t  prev_total = 0, prev_it = kNoItem, prev_buf = 0, subc_v = 0, subo_v = 0, prev_q = 0;
     uint32_t* prev_out   = P.surv;
+    const bool pk3       = !PAY && P.pack3 != 0;  // 3-byte join keys (uniform)
     auto copy_out = [&]() {
         const uint32_t nbytes = ((prev_total + 3u) & ~3u) * 4u;  // item region holds round_up(total, 4)
         const auto     ro     = buf_rsrc(prev_out, nbytes);
@@ -1805,6 +1825,15 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
                 const uint32_t j = min(i, hp / 4 - 1);  // reads past the half are never stored
                 __builtin_amdgcn_raw_buffer_store_b128(src[j], ro, i * 16, 0, 0);
                 __builtin_amdgcn_raw_buffer_store_b128(src[hp / 4 + j], rp, i * 16, 0, 0);
+            }
+        } else if (pk3) {  // 3-byte keys: 12 bytes per staged quad (whole quads: the item
+                               // region holds round_up(total, 4) words, more than these bytes)
+            const auto rp3 = buf_rsrc(prev_out, (prev_total + 3u) / 4u * 12u);
+#pragma unroll
+            for (int k = 0; k < kPco; k++) {
+                const uint32_t i = tid + k * NT;
+                const v4u      v = src[min(i, scap / 4 - 1)];
+                __builtin_amdgcn_raw_buffer_store_b96(pack3x4(v, g.hash_shift), rp3, i * 12, 0, HWBRJ_PCO_AUX);
             }
         } else {
 #pragma unroll
@@ -2060,6 +2089,18 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
             const bool     staged = PAY ? total <= hp : total <= scap;
             uint32_t*      stg    = stage + buf * sstr;
             const auto     ro     = buf_rsrc(out, total * 4);
+            // an unstaged survivor straight to its slot o (out-of-range offsets: dropped); 3-byte
+            // keys as three byte stores (neighbouring keys share words)
+            auto put = [&](uint32_t c, bool ok, uint32_t o) {
+                if (pk3) {
+                    const uint32_t v = c >> g.hash_shift, b = ok ? o * 3u : 0x7FFFFFF0u;
+                    __builtin_amdgcn_raw_buffer_store_b8((uint8_t) v, ro, b, 0, 0);
+                    __builtin_amdgcn_raw_buffer_store_b8((uint8_t) (v >> 8), ro, b + 1u, 0, 0);
+                    __builtin_amdgcn_raw_buffer_store_b8((uint8_t) (v >> 16), ro, b + 2u, 0, 0);
+                } else {
+                    __builtin_amdgcn_raw_buffer_store_b32(c, ro, ok ? o * 4u : 0x7FFFFFF0u, 0, 0);
+                }
+            };
             if (kAblProbe == 1 || kAblProbe == 2) {
             } else if (dense) {
 #pragma unroll
@@ -2068,7 +2109,7 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
                     const uint32_t c  = decode_k<KIND>(scr[lane + 64u * k], q, g);
                     const uint32_t o  = subo[dr[k] & 0xFFFFu] + (dr[k] >> 16);
                     if (staged) stg[ok ? o : scap + lane] = c;
-                    else __builtin_amdgcn_raw_buffer_store_b32(c, ro, ok ? o * 4 : 0x7FFFFFF0u, 0, 0);
+                    else put(c, ok, o);
                 }
             } else if (staged) {  // LDS stage (copied out coalesced at the next piece)
 #pragma unroll
@@ -2087,7 +2128,7 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
                     const uint32_t c  = decode_k<KIND>(sweep_word(Sc, i >> 2, i & 3), q, g);
                     const uint32_t o  = subo[(c >> g.sub_shift) & (NSUB - 1u)] + ((rank2[i / 2] >> (16 * (i & 1))) & 0xFFFFu);
                     const uint32_t oo = ((pass >> i) & 1u) ? o * 4 : 0x7FFFFFF0u;
-                    __builtin_amdgcn_raw_buffer_store_b32(c, ro, oo, 0, 0);
+                    put(c, ((pass >> i) & 1u) != 0, o);
                     if (PAY)
                         __builtin_amdgcn_raw_buffer_store_b32(Sc.id[i >> 2] * 32u + ((uint32_t) tid & 7u) * 4u + (uint32_t) (i & 3),
                                                               rpo, oo, 0, 0);
@@ -2376,7 +2417,7 @@ __global__ __launch_bounds__(256) void k_join_split(const uint32_t* __restrict__
 
 __global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
     __shared__ __attribute__((aligned(16))) uint32_t tab[kJoinWords];  // bitmap or hash table
-    __shared__ uint64_t dbase[kJoinDesc];  // run starts (words) of a batch: S survivor runs
+    __shared__ uint64_t dbase[kJoinDesc];  // run starts (byte offsets) of a batch: S survivor runs
     __shared__ uint32_t dcnt[kJoinDesc];
     __shared__ uint64_t rbase[kJoinDesc];  // R runs (one per build sweep of q)
     __shared__ uint32_t rcnt[kJoinDesc];
@@ -2412,22 +2453,40 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
     auto probe_end   = [&]() { t_probe += wall_clock64() - t_mark; };
     // The words [from, n) of one run (long runs: high-selectivity survivors, large R runs), with
     // kJoinTailU loads in flight per lane instead of one dependent load per iteration.
-    auto tail_run = [&](const uint32_t* data, uint64_t bb, uint32_t from, uint32_t n, auto&& op) {
+    // Runs are addressed by byte offsets from their array's base: with pack3 (P.r_pack3, both
+    // sides) key o of a run at byte b is the low 24 bits of the unaligned dword at b + 3 o, else
+    // v = (the code at b + 4 o) >> sh. Stride, shift and mask are uniform: one mad, one load, one
+    // shift and one and per key, no per-run state. The loads stay raw until used (key()): ALU work
+    // on a conditionally loaded value would make the wave wait for it at once.
+    const uint32_t kst = P.r_pack3 ? 3u : 4u, ksh = P.r_pack3 ? 0u : sh, kmk = P.r_pack3 ? 0xFFFFFFu : 0xFFFFFFFFu;
+    auto ldv = [&](const uint8_t* b8, uint64_t b, uint32_t o) -> uint32_t {
+        return *(const u32_unaligned*) (b8 + b + o * kst);
+    };
+    auto key = [&](uint32_t x) -> uint32_t { return (x >> ksh) & kmk; };
+    const uint8_t* const r8 = (const uint8_t*) P.r_codes;
+    const uint8_t* const s8 = (const uint8_t*) P.surv;
+    // R run of (sweep, sub) at key offset off of the sweep's slot; survivor run at key offset off of
+    // the item region at element e0 (regions and slots keep their 4-byte-per-key sizes)
+    auto rtag = [&](uint32_t sweep, uint32_t off) -> uint64_t {
+        return (uint64_t) sweep * P.slot * 4u + (uint64_t) off * kst;
+    };
+    auto stag = [&](uint64_t e0, uint32_t off) -> uint64_t { return e0 * 4u + (uint64_t) off * kst; };
+    auto tail_run = [&](const uint8_t* data, uint64_t bb, uint32_t from, uint32_t n, auto&& op) {
         for (uint32_t o = from + lane; o < n; o += 64u * kJoinTailU) {
             uint32_t v[kJoinTailU];
 #pragma unroll
             for (int u = 0; u < (int) kJoinTailU; u++) {
                 const uint32_t oo = o + 64u * u;
-                v[u]              = oo < n ? data[bb + oo] : 0u;
+                v[u]              = oo < n ? ldv(data, bb, oo) : 0u;
             }
 #pragma unroll
             for (int u = 0; u < (int) kJoinTailU; u++)
-                if (o + 64u * u < n) op(v[u] >> sh);
+                if (o + 64u * u < n) op(key(v[u]));
         }
     };
     // Every word of runs [da, db) of a descriptor batch through op(word): a wave per run, RUNS runs
     // in flight per wave with WPL words per lane each; longer runs finish in a tail loop.
-    auto walk = [&](auto runs_c, auto wpl_c, const uint32_t* data, const uint32_t* nc,
+    auto walk = [&](auto runs_c, auto wpl_c, const uint8_t* data, const uint32_t* nc,
                     const uint64_t* nb, uint32_t da, uint32_t db, auto&& op) {
         constexpr int RUNS = decltype(runs_c)::value, WPL = decltype(wpl_c)::value;
         for (uint32_t d = da + wave; d < db; d += kJoinWaves * RUNS) {
@@ -2440,14 +2499,14 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
 #pragma unroll
                 for (int j = 0; j < WPL; j++) {
                     const uint32_t o = lane + 64u * j;
-                    v[r][j]          = o < n[r] ? data[bb + o] : 0u;
+                    v[r][j]          = o < n[r] ? ldv(data, bb, o) : 0u;
                 }
             }
 #pragma unroll
             for (int r = 0; r < RUNS; r++) {
 #pragma unroll
                 for (int j = 0; j < WPL; j++)
-                    if (lane + 64u * j < n[r]) op(v[r][j] >> sh);
+                    if (lane + 64u * j < n[r]) op(key(v[r][j]));
                 if (n[r] > 64u * WPL) {
                     const uint64_t bb = nb[d + r * kJoinWaves];
                     tail_run(data, bb, 64u * WPL, n[r], op);
@@ -2477,12 +2536,12 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
                 const uint32_t seg   = local / npc;
                 const uint32_t piece = local - seg * npc;
                 dcnt[tid]  = P.surv_cnt[(uint64_t) it * NSUB + s];
-                dbase[tid] = (P.item_base ? P.item_base[it]  // (the partitioned multi-GPU join)
-                                          : (uint64_t) seg * P.surv_seg_stride + (uint64_t) (lq0 + piece * P.CH) * 32) +
-                             P.surv_off[(uint64_t) it * NSUB + s];
+                dbase[tid] = stag(P.item_base ? P.item_base[it]  // (the partitioned multi-GPU join)
+                                              : (uint64_t) seg * P.surv_seg_stride + (uint64_t) (lq0 + piece * P.CH) * 32,
+                                  P.surv_off[(uint64_t) it * NSUB + s]);
             }
             __syncthreads();
-            walk(SR{}, SW{}, P.surv, dcnt, dbase, 0, nd, op);
+            walk(SR{}, SW{}, s8, dcnt, dbase, 0, nd, op);
         }
         probe_end();
     };
@@ -2494,7 +2553,7 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
             const uint64_t r = (uint64_t) (d0 + tid) * NSUB + s;
             c                = P.r_cnt[r];
             rcnt[tid]        = c;
-            rbase[tid]       = (uint64_t) (d0 + tid) * P.slot + P.r_off[r];
+            rbase[tid]       = rtag(d0 + tid, P.r_off[r]);
         }
         (void) c;
         __syncthreads();
@@ -2518,7 +2577,7 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
         if ((uint32_t) tid < nRd) {
             const uint64_t r = (uint64_t) (w0 + tid) * NSUB + s;
             rcnt[tid]        = P.r_cnt[r];
-            rbase[tid]       = (uint64_t) (w0 + tid) * P.slot + P.r_off[r];
+            rbase[tid]       = rtag(w0 + tid, P.r_off[r]);
             rc = rcnt[tid];
         }
         if (wave == 0) {  // the job's R keys (nRd <= 64: every R descriptor is in wave 0)
@@ -2531,9 +2590,9 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
             const uint32_t seg   = local / npc;
             const uint32_t piece = local - seg * npc;
             dcnt[tid]  = P.surv_cnt[(uint64_t) it * NSUB + s];
-            dbase[tid] = (P.item_base ? P.item_base[it]  // (the partitioned multi-GPU join)
-                                      : (uint64_t) seg * P.surv_seg_stride + (uint64_t) (lq0 + piece * P.CH) * 32) +
-                         P.surv_off[(uint64_t) it * NSUB + s];
+            dbase[tid] = stag(P.item_base ? P.item_base[it]  // (the partitioned multi-GPU join)
+                                          : (uint64_t) seg * P.surv_seg_stride + (uint64_t) (lq0 + piece * P.CH) * 32,
+                              P.surv_off[(uint64_t) it * NSUB + s]);
         }
         __syncthreads();
         constexpr int FS = HWBRJ_JSR, FSW = HWBRJ_JSW;
@@ -2549,7 +2608,7 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
 #pragma unroll
             for (int j = 0; j < FW; j++) {
                 const uint32_t o = lane + 64u * j;
-                rv[r][j]         = o < rn[r] ? P.r_codes[bb + o] : 0u;
+                rv[r][j]         = o < rn[r] ? ldv(r8, bb, o) : 0u;
             }
         }
 #pragma unroll
@@ -2563,7 +2622,7 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
 #pragma unroll
             for (int j = 0; j < FSW; j++) {
                 const uint32_t o = lane + 64u * j;
-                sv[r][j]         = o < sn[r] ? P.surv[bb + o] : 0u;
+                sv[r][j]         = o < sn[r] ? ldv(s8, bb, o) : 0u;
             }
         }
         // bits set without returns (no wave waits on them); a duplicate R key shows as fewer set
@@ -2573,10 +2632,10 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
         for (int r = 0; r < FR; r++) {
 #pragma unroll
             for (int j = 0; j < FW; j++)
-                if (lane + 64u * j < rn[r]) set(rv[r][j] >> sh);
+                if (lane + 64u * j < rn[r]) set(key(rv[r][j]));
             if (rn[r] > 64u * FW) {  // (rare) longer run
                 const uint64_t bb = rbase[wave + r * kJoinWaves];
-                tail_run(P.r_codes, bb, 64u * FW, rn[r], set);
+                tail_run(r8, bb, 64u * FW, rn[r], set);
             }
         }
         __syncthreads();
@@ -2598,14 +2657,14 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
             for (int r = 0; r < FS; r++) {
 #pragma unroll
                 for (int j = 0; j < FSW; j++)
-                    if (lane + 64u * j < sn[r]) test(sv[r][j] >> sh);
+                    if (lane + 64u * j < sn[r]) test(key(sv[r][j]));
                 if (sn[r] > 64u * FSW) {
                     const uint64_t bb = dbase[wave + r * kJoinWaves];
-                    tail_run(P.surv, bb, 64u * FSW, sn[r], test);
+                    tail_run(s8, bb, 64u * FSW, sn[r], test);
                 }
             }
 #ifndef HWBRJ_ABL_JNOS
-            walk(SR{}, SW{}, P.surv, dcnt, dbase, (uint32_t) (kJoinWaves * FS), nSd, test);
+            walk(SR{}, SW{}, s8, dcnt, dbase, (uint32_t) (kJoinWaves * FS), nSd, test);
 #endif
             probe_end();
             done = true;
@@ -2618,7 +2677,7 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
         for (uint32_t d0 = w0; d0 < w1; d0 += kJoinDesc) {
             const uint32_t nd = min(kJoinDesc, w1 - d0);
             load_r(d0, nd);
-            walk(RR{}, RW{}, P.r_codes, rcnt, rbase, 0, nd, [&](uint32_t x) {
+            walk(RR{}, RW{}, r8, rcnt, rbase, 0, nd, [&](uint32_t x) {
                 const uint32_t bit = 1u << (x & 31u);
                 dup |= atomicOr(&tab[x >> 5], bit) & bit;
             });
@@ -2655,7 +2714,7 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
                     for (uint32_t i = tid; i < kJoinT / 4; i += kJoinThreads)
                         ((uint4*) tab)[i] = make_uint4(kEmpty, kEmpty, kEmpty, kEmpty);
                     __syncthreads();
-                    walk(RR{}, RW{}, P.r_codes, rcnt, rbase, da, db, [&](uint32_t x) { join_insert(tab, x); });
+                    walk(RR{}, RW{}, r8, rcnt, rbase, da, db, [&](uint32_t x) { join_insert(tab, x); });
                     probe_survivors([&](uint32_t x) { cnt += join_count(tab, x); });  // (starts with a barrier)
                     continue;
                 }
@@ -2673,7 +2732,7 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
                 uint32_t* hist = tab + kJoinPiece;
                 for (uint32_t i = tid; i < NH + 2; i += kJoinThreads) hist[i] = 0;
                 __syncthreads();
-                walk(RR{}, RW{}, P.r_codes, rcnt, rbase, da, db, [&](uint32_t x) { atomicAdd(&hist[(x & (NH - 1u)) + 2], 1u); });
+                walk(RR{}, RW{}, r8, rcnt, rbase, da, db, [&](uint32_t x) { atomicAdd(&hist[(x & (NH - 1u)) + 2], 1u); });
                 __syncthreads();
                 if (wave == 0) {  // inclusive prefix sum of hist[2, NH + 2): 16 buckets per lane
                     const uint32_t per = (NH + 63) / 64, b0 = 2 + lane * per;
@@ -2688,7 +2747,7 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
                         }
                 }
                 __syncthreads();
-                walk(RR{}, RW{}, P.r_codes, rcnt, rbase, da, db, [&](uint32_t x) {
+                walk(RR{}, RW{}, r8, rcnt, rbase, da, db, [&](uint32_t x) {
                     keys[atomicAdd(&hist[(x & (NH - 1u)) + 1], 1u)] = x;  // bucket b: [hist[b], hist[b + 1])
                 });
                 if (P.jkind == 1) {
@@ -3876,6 +3935,7 @@ const char* kernel_build_knobs() {
         num("HWBRJ_SCRK", HWBRJ_SCRK, 256);
         num("HWBRJ_JTU", HWBRJ_JTU, 8);
         num("HWBRJ_JT", HWBRJ_JT, 256);
+        num("HWBRJ_PACK3", HWBRJ_PACK3, 1);
         num("HWBRJ_JRR", HWBRJ_JRR, 4);
         num("HWBRJ_JRW", HWBRJ_JRW, 4);
         num("HWBRJ_JSR", HWBRJ_JSR, 8);
