@@ -616,7 +616,7 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     const uint32_t PG = (uint32_t) cus_ * (uint32_t) std::max<size_t>(1, std::min<size_t>(2, 163840 / pl_lds));
     const bool dbg_on = dbg;  // dev-only phase stamps (HWBRJ_DBG)
     if (dbg_on) {
-        ok &= dbgP.ensure((size_t) std::max<uint32_t>(PG, F) * 64) && dbgJ.ensure((size_t) F * 64);
+        ok &= dbgP.ensure((size_t) std::max<uint32_t>(PG, F) * 64) && dbgJ.ensure((size_t) std::max<uint64_t>(F, 1024) * 64);
         HWBRJ_CHECK(hipMemsetAsync(dbgP.p, 0, dbgP.bytes, stream));
         HWBRJ_CHECK(hipMemsetAsync(dbgJ.p, 0, dbgJ.bytes, stream));
         pp.dbg = dbgP.as<uint64_t>();
@@ -694,14 +694,11 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
 
     if (dbg_on) {
         HWBRJ_CHECK(hipEventSynchronize(ev_[8]));
-        std::vector<uint64_t> hp(PG * 8), hj(F * 8);
+        std::vector<uint64_t> hp(PG * 8);
         HWBRJ_CHECK(hipMemcpy(hp.data(), dbgP.p, hp.size() * 8, hipMemcpyDeviceToHost));
-        HWBRJ_CHECK(hipMemcpy(hj.data(), dbgJ.p, hj.size() * 8, hipMemcpyDeviceToHost));
-        double sp_[6] = {0}, sj[6] = {0};
+        double sp_[6] = {0};
         for (uint32_t b = 0; b < PG; b++)
             for (int k = 0; k < 6; k++) sp_[k] += (double) hp[b * 8 + k] / PG;
-        for (uint32_t b = 0; b < F; b++)
-            for (int k = 0; k < 6; k++) sj[k] += (double) hj[b * 8 + k] / F;
         std::vector<uint64_t> hs(G * 8);
         HWBRJ_CHECK(hipMemcpy(hs.data(), dbgS.p, hs.size() * 8, hipMemcpyDeviceToHost));
         double ss[6] = {0};
@@ -724,6 +721,16 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
         }
         fprintf(stderr, "[dbg] probe cyc/WG: top %.0f test %.0f b1 %.0f scan+b2 %.0f write %.0f b3+copy %.0f\n",
                 sp_[0], sp_[1], sp_[2], sp_[3], sp_[4], sp_[5]);
+        {  // k_join: workgroups summed into 1024 slots
+            std::vector<uint64_t> hj2(1024 * 8);
+            HWBRJ_CHECK(hipMemcpy(hj2.data(), dbgJ.p, hj2.size() * 8, hipMemcpyDeviceToHost));
+            double sj2[6] = {0};
+            const double nwg = (double) F * (1u << g.log2NSUB);
+            for (uint32_t b = 0; b < 1024; b++)
+                for (int k = 0; k < 6; k++) sj2[k] += (double) hj2[b * 8 + k] / nwg;
+            fprintf(stderr, "[dbg] join cyc/WG (wave 0): desc %.0f R+sets %.0f popcnt %.0f surv1 %.0f surv2 %.0f end %.0f\n",
+                    sj2[0], sj2[1], sj2[2], sj2[3], sj2[4], sj2[5]);
+        }
     }
     return 0;
 }

@@ -2451,6 +2451,22 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
     uint64_t       t_probe = 0, t_mark = 0;
     auto probe_begin = [&]() { t_mark = wall_clock64(); };
     auto probe_end   = [&]() { t_probe += wall_clock64() - t_mark; };
+    // dev-only phase stamps of wave 0 (build with -DHWBRJ_STAMPS, run with HWBRJ_DBG): fused path
+    // 0 descriptors, 1 R loads + bit sets, 2 popcount, 3 first survivor runs, 4 further runs, 5 sum
+    uint64_t tph[6] = {0, 0, 0, 0, 0, 0}, tlast = __builtin_amdgcn_s_memtime();
+    (void) tlast;
+    (void) tph;
+    auto stamp = [&](int k) {
+#ifdef HWBRJ_STAMPS
+        if (P.dbg) {
+            const uint64_t t = __builtin_amdgcn_s_memtime();
+            tph[k] += t - tlast;
+            tlast = t;
+        }
+#else
+        (void) k;
+#endif
+    };
     // The words [from, n) of one run (long runs: high-selectivity survivors, large R runs), with
     // kJoinTailU loads in flight per lane instead of one dependent load per iteration.
     // Runs are addressed by byte offsets from their array's base: with pack3 (P.r_pack3, both
@@ -2580,6 +2596,7 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
             rbase[tid]       = rtag(w0 + tid, P.r_off[r]);
             rc = rcnt[tid];
         }
+        stamp(0);
         if (wave == 0) {  // the job's R keys (nRd <= 64: every R descriptor is in wave 0)
             const uint32_t t = __builtin_amdgcn_readlane(wave_incl_scan_dpp(rc), 63);
             if (lane == 0) npieces = t;
@@ -2595,7 +2612,10 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
                               P.surv_off[(uint64_t) it * NSUB + s]);
         }
         __syncthreads();
-        constexpr int FS = HWBRJ_JSR, FSW = HWBRJ_JSW;
+#ifndef HWBRJ_JFS
+#define HWBRJ_JFS HWBRJ_JSR
+#endif
+        constexpr int FS = HWBRJ_JFS, FSW = HWBRJ_JSW;  // survivor runs per wave loaded with R's
         uint32_t rv[FR][FW], rn[FR], sv[FS][FSW], sn[FS];
 #pragma unroll
         for (int r = 0; r < FR; r++) {
@@ -2639,6 +2659,7 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
             }
         }
         __syncthreads();
+        stamp(1);
         {
             uint32_t pc = 0;
             for (uint32_t i = tid; i < kJoinWords / 4; i += kJoinThreads) {
@@ -2650,6 +2671,7 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
         }
         __syncthreads();
         hashed = dupflag != npieces;  // uniform
+        stamp(2);
         if (!hashed) {
             probe_begin();
             auto test = [&](uint32_t x) { cnt += (tab[x >> 5] >> (x & 31u)) & 1u; };
@@ -2663,9 +2685,11 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
                     tail_run(s8, bb, 64u * FSW, sn[r], test);
                 }
             }
+            stamp(3);
 #ifndef HWBRJ_ABL_JNOS
             walk(SR{}, SW{}, s8, dcnt, dbase, (uint32_t) (kJoinWaves * FS), nSd, test);
 #endif
+            stamp(4);
             probe_end();
             done = true;
         }
@@ -2779,6 +2803,11 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
         atomicAdd((unsigned long long*) (slot + 1), (unsigned long long) t_probe);
         atomicAdd((unsigned long long*) (slot + 2), (unsigned long long) (wall_clock64() - t_start));
     }
+    stamp(5);
+#ifdef HWBRJ_STAMPS
+    if (P.dbg && tid == 0)
+        for (int k = 0; k < 6; k++) atomicAdd((unsigned long long*) &P.dbg[(blockIdx.x & 1023u) * 8 + k], (unsigned long long) tph[k]);
+#endif
 }
 
 // result[0] += matches; result[3], result[4] += probe / total ticks of the join workgroups
@@ -3939,6 +3968,7 @@ const char* kernel_build_knobs() {
         num("HWBRJ_JRR", HWBRJ_JRR, 4);
         num("HWBRJ_JRW", HWBRJ_JRW, 4);
         num("HWBRJ_JSR", HWBRJ_JSR, 8);
+        num("HWBRJ_JFS", HWBRJ_JFS, HWBRJ_JSR);
         num("HWBRJ_JSW", HWBRJ_JSW, 2);
         num("HWBRJ_JFR", HWBRJ_JFR, 8);
         num("HWBRJ_JFW", HWBRJ_JFW, 5);
