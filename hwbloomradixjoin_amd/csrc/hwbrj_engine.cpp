@@ -258,6 +258,8 @@ const DevKnobs& dev_knobs() {
         d.scwpc     = u("HWBRJ_DEV_SCWPC");
         if (getenv("HWBRJ_DEV_EVFLAGS")) d.evflags = (int) u("HWBRJ_DEV_EVFLAGS");
         d.l2sub     = u("HWBRJ_DEV_L2SUB");
+        d.ovl       = getenv("HWBRJ_DEV_OVL") != nullptr;
+        d.rfirst    = getenv("HWBRJ_DEV_RFIRST") != nullptr;
 #endif
         return d;
     }();
@@ -277,6 +279,8 @@ std::string dev_knobs_string() {
     if (d.scwpc) add("HWBRJ_DEV_SCWPC=" + std::to_string(d.scwpc));
     if (d.evflags >= 0) add("HWBRJ_DEV_EVFLAGS=" + std::to_string(d.evflags));
     if (d.l2sub) add("HWBRJ_DEV_L2SUB=" + std::to_string(d.l2sub));
+    if (d.ovl) add("HWBRJ_DEV_OVL");
+    if (d.rfirst) add("HWBRJ_DEV_RFIRST");
     return r;
 }
 
@@ -479,7 +483,69 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     sp.zero_small = small.as<uint32_t>();  // (the R scatter only: cleared below)
     sp.zero_word  = jparts.as<uint32_t>() + 2 * NJ;
 
+    // S pass-1 and its lists (below; dev A/B HWBRJ_DEV_OVL: on a second stream, concurrent with
+    // the R side)
+    auto s_pass = [&](hipStream_t st, bool marks) -> int {
+        ScatterParams ss = sp;
+        ss.zero_small    = nullptr;
+        ss.zero_word     = nullptr;
+        if (g.mode == MODE_GLOBAL) {
+            launch_probe_global(dS, nS, g, d_tabs_, bitmap.as<uint32_t>(), dense.as<uint32_t>(),
+                                d_dcount, st);
+            ss.src   = dense.p;
+            ss.n     = nS;
+            ss.n_dev = d_dcount;
+        } else {
+            ss.src   = dS;
+            ss.n     = nS;
+            ss.n_dev = nullptr;
+        }
+        ss.pool       = poolS.as<uint32_t>();
+        ss.meta       = metaS.as<uint32_t>();
+        ss.wg_used    = usedS.as<uint32_t>();
+        ss.wgq_chunks = wgqcS.as<uint32_t>();
+        ss.wgq_elems  = wgqeS.as<uint32_t>();
+        ss.cap        = capS;
+        if (dbg) {  // dev-only phase stamps (HWBRJ_DBG)
+            if (!dbgS.ensure((size_t) G * 64)) {
+                set_last_error("hipMalloc failed (device memory)");
+                return 4;
+            }
+            HWBRJ_CHECK(hipMemsetAsync(dbgS.p, 0, dbgS.bytes, st));
+            ss.dbg = dbgS.as<uint64_t>();
+        }
+        ss.ppool = mat ? ppoolS.as<uint32_t>() : nullptr;
+        launch_scatter(ss, g.mode == MODE_GLOBAL ? SRC_CODES : SRC_TUPLES, SIDE_S, G, st);
+        if (marks) HWBRJ_CHECK(mark(4, st));
+        launch_plan(wgqcS.as<uint32_t>(), wgqeS.as<uint32_t>(), G, g.log2F, wgqoS.as<uint32_t>(),
+                    colS.as<uint32_t>() + 2 * F, colS.as<uint64_t>(), st);
+        launch_list_fill(metaS.as<uint32_t>(), usedS.as<uint32_t>(), capS, g.log2F, wgqoS.as<uint32_t>(),
+                         colS.as<uint32_t>() + 2 * F, colS.as<uint64_t>(), CH, nseg, lstartS.as<uint32_t>(),
+                         estartS.as<uint64_t>(), istartS.as<uint32_t>(), listS.as<uint32_t>(), G, st);
+        if (marks) HWBRJ_CHECK(mark(5, st));
+        return 0;
+    };
     HWBRJ_CHECK(mark(0, stream));
+    const bool ovl = dev_knobs().ovl && g.mode != MODE_GLOBAL && !basic_kk && !mat && !bcast;
+    if (ovl) {  // dev A/B: S pass on the side stream (its phases then show inside the R side's)
+        if (!ovl_stream_) {
+            HWBRJ_CHECK(hipStreamCreateWithFlags(&ovl_stream_, hipStreamNonBlocking));
+            HWBRJ_CHECK(hipEventCreateWithFlags(&ovl_ev_[0], hipEventDisableTiming));
+            HWBRJ_CHECK(hipEventCreateWithFlags(&ovl_ev_[1], hipEventDisableTiming));
+        }
+        HWBRJ_CHECK(hipEventRecord(ovl_ev_[0], stream));
+        HWBRJ_CHECK(hipStreamWaitEvent(ovl_stream_, ovl_ev_[0], 0));
+        if (const int rc = s_pass(ovl_stream_, false)) return rc;
+        HWBRJ_CHECK(hipEventRecord(ovl_ev_[1], ovl_stream_));
+    }
+    // The S pass runs first: then the filter slices (written by k_build) and the R pool (written by
+    // k_scatter_r) are the most recent writes when k_probe and k_build read them, so the Infinity
+    // Cache still holds much of them. Not in the global mode (the R scatter's workgroup 0 zeroes the
+    // dense count the S pass's global probe adds to) nor for basic k >= 2 (the R side borrows the
+    // S-side buffers).
+    const bool s_first = !ovl && !dev_knobs().rfirst && g.mode != MODE_GLOBAL && !basic_kk;
+    if (s_first)
+        if (const int rc = s_pass(stream, true)) return rc;
     // ---------------------------------------------------------------- R: pass-1 (+ filter)
     if (g.mode == MODE_GLOBAL)
         launch_build_global(dR, nR, g, d_tabs_, bitmap.as<uint32_t>(), stream);
@@ -563,39 +629,13 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     }
     HWBRJ_CHECK(mark(3, stream));
     // ---------------------------------------------------------------- S: pass-1 (+ probe)
-    if (g.mode == MODE_GLOBAL) {
-        launch_probe_global(dS, nS, g, d_tabs_, bitmap.as<uint32_t>(), dense.as<uint32_t>(),
-                            d_dcount, stream);
-        sp.src   = dense.p;
-        sp.n     = nS;
-        sp.n_dev = d_dcount;
-    } else {
-        sp.src   = dS;
-        sp.n     = nS;
-        sp.n_dev = nullptr;
+    if (ovl) {
+        HWBRJ_CHECK(hipStreamWaitEvent(stream, ovl_ev_[1], 0));
+        HWBRJ_CHECK(mark(4, stream));
+        HWBRJ_CHECK(mark(5, stream));
+    } else if (!s_first) {
+        if (const int rc = s_pass(stream, true)) return rc;
     }
-    sp.pool       = poolS.as<uint32_t>();
-    sp.meta       = metaS.as<uint32_t>();
-    sp.wg_used    = usedS.as<uint32_t>();
-    sp.wgq_chunks = wgqcS.as<uint32_t>();
-    sp.wgq_elems  = wgqeS.as<uint32_t>();
-    sp.cap        = capS;
-    const bool dbg_sc = dbg;  // dev-only phase stamps (HWBRJ_DBG)
-    if (dbg_sc) {
-        ok &= dbgS.ensure((size_t) G * 64);
-        HWBRJ_CHECK(hipMemsetAsync(dbgS.p, 0, dbgS.bytes, stream));
-        sp.dbg = dbgS.as<uint64_t>();
-    }
-    sp.ppool = mat ? ppoolS.as<uint32_t>() : nullptr;
-    launch_scatter(sp, g.mode == MODE_GLOBAL ? SRC_CODES : SRC_TUPLES, SIDE_S, G, stream);
-    sp.dbg = nullptr;
-    HWBRJ_CHECK(mark(4, stream));
-    launch_plan(wgqcS.as<uint32_t>(), wgqeS.as<uint32_t>(), G, g.log2F, wgqoS.as<uint32_t>(),
-                colS.as<uint32_t>() + 2 * F, colS.as<uint64_t>(), stream);
-    launch_list_fill(metaS.as<uint32_t>(), usedS.as<uint32_t>(), capS, g.log2F, wgqoS.as<uint32_t>(),
-                     colS.as<uint32_t>() + 2 * F, colS.as<uint64_t>(), CH, nseg, lstartS.as<uint32_t>(),
-                     estartS.as<uint64_t>(), istartS.as<uint32_t>(), listS.as<uint32_t>(), G, stream);
-    HWBRJ_CHECK(mark(5, stream));
     ProbeParams pp{};
     pp.g               = g;
     pp.tabs            = d_tabs_;
@@ -688,6 +728,7 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     pending_args_ = args != nullptr;
     pending_nS_   = nS;
     pending_ev_   = phase_ev_;
+    pending_sfirst_ = s_first;
     pending_stream_ = stream;
     have_filter_  = args != nullptr;
     last_g_       = g;
@@ -965,6 +1006,7 @@ int Engine::enqueue_basic_kk(const uint2* dR, uint64_t nR, const uint2* dS, uint
     pending_args_ = true;
     pending_nS_   = nS;
     pending_ev_   = phase_ev_;
+    pending_sfirst_ = false;
     pending_stream_ = stream;
     have_filter_  = true;
     last_g_       = g;
@@ -1005,7 +1047,11 @@ int Engine::wait(hwbrj_stats_t* st) {
             hipEvent_t e[9];
             for (int i = 0; i <= 8; i++) e[i] = ev_[i];
             if (surv_fused_) e[7] = ev_[6];
-            for (int i = 1; i <= 8; i++) HWBRJ_CHECK(hipEventElapsedTime(&ms[i], e[i - 1], e[i]));
+            // phase i ends at boundary i and starts at boundary from[i] (S pass first: it starts the
+            // join, the R scatter starts after the S lists, the probe after the build)
+            static const int kFrom[2][9] = {{0, 0, 1, 2, 3, 4, 5, 6, 7}, {0, 5, 1, 2, 0, 4, 3, 6, 7}};
+            const int* from = kFrom[pending_sfirst_ ? 1 : 0];
+            for (int i = 1; i <= 8; i++) HWBRJ_CHECK(hipEventElapsedTime(&ms[i], e[from[i]], e[i]));
             HWBRJ_CHECK(hipEventElapsedTime(&ms[0], e[0], e[8]));
         }
         st->ms_total     = ms[0];

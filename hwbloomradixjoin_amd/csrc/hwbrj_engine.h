@@ -99,6 +99,8 @@ class Engine {
     int          device_;
     int          cus_ = 256;
     hipStream_t  own_stream_ = nullptr;
+    hipStream_t  ovl_stream_ = nullptr;             // dev A/B HWBRJ_DEV_OVL: the S pass's stream
+    hipEvent_t   ovl_ev_[2]  = {nullptr, nullptr};  // (fork, join of ovl_stream_)
     hipEvent_t   ev_[10];
     bool         have_filter_ = false;
     Geometry     last_g_{};
@@ -115,6 +117,7 @@ class Engine {
     // join on another stream waits for ev_[8]. Compared by handle: a stream must outlive the
     // joins enqueued on it (a destroyed stream's handle can be reused by a new one).
     hipStream_t  pending_stream_ = nullptr;
+    bool         pending_sfirst_ = false;  // the pending join ran its S pass first (phase boundaries)
     int          pending_rc_     = 0;   // nonzero: the pending join failed after enqueuing kernels
     std::string  pending_err_;
     bool         surv_fused_   = false;

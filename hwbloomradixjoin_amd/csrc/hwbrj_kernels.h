@@ -242,6 +242,8 @@ struct DevKnobs {
     uint32_t scwpc = 0;          // HWBRJ_DEV_SCWPC: scatter workgroups per CU
     int      evflags = -1;       // HWBRJ_DEV_EVFLAGS: phase-event creation flags
     uint32_t l2sub = 0;          // HWBRJ_DEV_L2SUB: join sub-partition bits (code-digit joins)
+    bool     ovl   = false;      // HWBRJ_DEV_OVL: S pass on a second stream beside the R side
+    bool     rfirst = false;     // HWBRJ_DEV_RFIRST: R side before the S pass (the round-3 order)
 };
 const DevKnobs& dev_knobs();
 // "name=value" of every dev knob that is set ("" in product builds); hwbrj_version() appends it

@@ -180,6 +180,23 @@ def test_bench_uses_pmc_traffic_only_for_the_profiled_library(tmp_path, hw):
     assert "src " in hw.version()
 
 
+def test_bench_modeled_join_key_bytes():
+    """modeled_bytes prices the join's runs at 3 bytes per key exactly where the engine stores
+    3-byte keys (hwbrj_kernels.h join_pack3: hash_shift = log2 F + log2 subparts >= 8, code-digit
+    partitions), else 4."""
+    import importlib.util
+    from types import SimpleNamespace as NS
+    spec = importlib.util.spec_from_file_location("bench", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    assert bench.join_key_bytes(NS(mode=1, partitions=1024, subparts=16)) == 3.0  # north star
+    assert bench.join_key_bytes(NS(mode=0, partitions=1024, subparts=16)) == 3.0  # PRO
+    assert bench.join_key_bytes(NS(mode=1, partitions=16, subparts=8)) == 4.0     # hash_shift 7
+    assert bench.join_key_bytes(NS(mode=2, partitions=1024, subparts=64)) == 4.0  # slice-basic: mixed keys
+    mb = bench.modeled_bytes(10, 20, 5, 0, 4.0, 3.0)
+    assert mb["join_codes_R"] == 60.0 and mb["survivors"] == 30.0
+
+
 def test_write_result_relation_reference_order(hw, tmp_path):
     """hwbrj_write_result_relation emits the pairs in write_result_relation's order
     (src/tuple_buffer.h:205-231): per thread, the newest chained buffer first, every buffer from its
