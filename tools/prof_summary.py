@@ -14,7 +14,7 @@ import os
 import sys
 from collections import defaultdict
 
-# dispatch order of one join (hwbrj_engine.cpp Engine::run) -> phase
+# kernel -> phase (hwbrj_engine.cpp Engine::enqueue)
 PHASE_OF = {"k_build_global": "build", "k_build": "build", "k_probe_global": "probe",
             "k_probe": "probe", "k_join_split": "join", "k_join": "join", "k_join_sum": "join", "k_plan": "index",
             "k_list_fill": "index", "k_mat_build": "materialize", "k_mat_probe": "materialize"}
@@ -28,24 +28,26 @@ def one(path_glob):
 
 
 def last_join(names):
-    """Indices of the dispatches of the last join: from the last R scatter to the join's final
-    count reduction (k_join_sum), so kernels the bench runs after the joins (its copy-rate
-    measurement) are not counted."""
-    sc = [i for i, n in enumerate(names) if n == "k_scatter_r"]
-    b = sc[-1] if sc else 0
-    end = next((i for i in range(b, len(names)) if names[i] == "k_join_sum"), len(names) - 1)
-    return list(range(b, end + 1))
+    """Indices of the dispatches of the last join: after the previous join's final count reduction
+    (k_join_sum) up to its own, so kernels the bench runs after the joins (its copy-rate
+    measurement) are not counted. The S pass may come first (Engine::enqueue) or the R side."""
+    ends = [i for i, n in enumerate(names) if n == "k_join_sum"]
+    if not ends:
+        return list(range(len(names)))
+    b = ends[-2] + 1 if len(ends) > 1 else 0
+    return list(range(b, ends[-1] + 1))
 
 
 def label(names, idx):
-    out, nsc = [], 0
+    """Phase of each dispatch: plan / list-fill kernels belong to the side of the last scatter."""
+    out, side = [], "r"
     for i in idx:
         n = names[i]
         if n in ("k_scatter_r", "k_scatter_s"):
-            out.append(n[2:].replace("scatter_", "") + "_scatter")
-            nsc += 1
+            side = n[-1]
+            out.append(side + "_scatter")
         elif n in ("k_plan", "k_list_fill"):
-            out.append("r_index" if nsc <= 1 else "s_index")
+            out.append(side + "_index")
         else:
             out.append(PHASE_OF.get(n, "other"))
     return out
