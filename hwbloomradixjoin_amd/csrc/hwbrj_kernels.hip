@@ -2426,6 +2426,13 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
     __shared__ uint32_t dupflag, npieces;
     const uint32_t NSUB = 1u << P.log2NSUB;
     uint32_t       job = blockIdx.x, part = 0;  // workgroup j < jobs: part 0 of job j
+#ifndef HWBRJ_JXCD
+#define HWBRJ_JXCD 1
+#endif
+    // XCD-aware job order: blocks b, b + 8, ... share an XCD (dealt round-robin), so they take
+    // consecutive jobs -- the 16 subs of a partition run on one XCD, where the lines their runs
+    // share (adjacent sub runs in every sweep slot and item region) are fetched into its L2 once
+    if (HWBRJ_JXCD && blockIdx.x < P.jobs && (P.jobs & 7u) == 0) job = (blockIdx.x & 7u) * (P.jobs >> 3) + (blockIdx.x >> 3);
     if (blockIdx.x >= P.jobs) {                 // extra workgroups: further parts of skewed jobs
         const uint32_t e = blockIdx.x - P.jobs;
         if (e >= min(*P.nextra, kJoinExtra)) return;
@@ -3964,6 +3971,7 @@ const char* kernel_build_knobs() {
         num("HWBRJ_SCRK", HWBRJ_SCRK, 256);
         num("HWBRJ_JTU", HWBRJ_JTU, 8);
         num("HWBRJ_JT", HWBRJ_JT, 256);
+        num("HWBRJ_JXCD", HWBRJ_JXCD, 1);
         num("HWBRJ_PACK3", HWBRJ_PACK3, 1);
         num("HWBRJ_JRR", HWBRJ_JRR, 4);
         num("HWBRJ_JRW", HWBRJ_JRW, 4);
