@@ -1593,19 +1593,25 @@ __global__ __launch_bounds__(1024) void k_build(BuildParams P) {
         for (uint32_t i = tid; i < segw; i += blockDim.x) slice[i] = 0;
         __syncthreads();
         const bool  last = seg + 1 == nseg;
-        uint32_t    eA[kBPQ], eB[kBPQ];
+        // list entries two groups ahead, chunks one group ahead: a group's chunk loads never wait
+        // for the list loads just issued (one exposed memory latency per group otherwise)
+        uint32_t    eB[kBPQ], eC[kBPQ];
         Sweep<kBPQ> SA, SB, PA, PB;  // words; payloads (PAY)
         if (l0 < l1) {
+            uint32_t eA[kBPQ];
             load_list_u<kBPQ>(P.list, l0, l1, eA);
+            const uint32_t n1 = min(l0 + GRP, l1 - 1u);
+            load_list_u<kBPQ>(P.list, n1, min(n1 + GRP, l1), eB);
             load_chunks_u<kBPQ, false, kBdNT>(P.pool, eA, l0, l1, SA);
             if (PAY) load_chunks_u<kBPQ>(P.ppool, eA, l0, l1, PA);
         }
         for (uint32_t lb = l0; lb < l1; lb += GRP) {
             const uint32_t nb = min(lb + GRP, l1 - 1u);  // next group (re-reads the last entry past the end)
             const uint32_t ne = min(nb + GRP, l1);
-            load_list_u<kBPQ>(P.list, nb, ne, eB);
+            const uint32_t nnb = min(nb + GRP, l1 - 1u);  // the group after it (its list entries)
             load_chunks_u<kBPQ, false, kBdNT>(P.pool, eB, nb, ne, SB);
             if (PAY) load_chunks_u<kBPQ>(P.ppool, eB, nb, ne, PB);
+            load_list_u<kBPQ>(P.list, nnb, min(nnb + GRP, l1), eC);
 #pragma unroll
             for (int jj = 0; jj < kBPQ; jj++) {
                 const uint32_t sb = lb + (uint32_t) jj * kBSweep;  // first list position of the sweep
@@ -1681,7 +1687,7 @@ __global__ __launch_bounds__(1024) void k_build(BuildParams P) {
                 SA.v[jj] = SB.v[jj];
                 SA.n[jj] = SB.n[jj];
                 if (PAY) PA.v[jj] = PB.v[jj];
-                eA[jj]   = eB[jj];
+                eB[jj]   = eC[jj];
             }
         }
         __syncthreads();
