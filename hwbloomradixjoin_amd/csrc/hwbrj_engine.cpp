@@ -584,7 +584,10 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     bp.run_off     = rrun.as<uint32_t>() + sweeps_max * NSUB;
     bp.ppool       = mat ? ppoolR.as<uint32_t>() : nullptr;
     bp.out_pay     = mat ? rpay.as<uint32_t>() : nullptr;
-    const bool pack3 = !mat && join_pack3(g);  // 3-byte join keys from build / probe to k_join
+    // 3-byte join keys from build / probe to k_join, unless the last join this Engine waited for had
+    // probe items too large for the stage (their 32-bit survivor runs make the join read two formats,
+    // k_join_mixed): a performance hint only, both paths give the same counts
+    const bool pack3 = !mat && join_pack3(g) && pack3_hint_;
     bp.pack3       = pack3 ? 1u : 0u;
     // the broadcast: rank 0 builds the slices, the other ranks only sub-partition R for the join
     // and receive them over RCCL (HWBRJ_HOOK_BCAST_NONROOT: this rank takes the non-root side, for
@@ -652,6 +655,7 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     pp.job_surv        = jparts.as<uint32_t>() + NJ;
     pp.surv_pos        = mat ? survpos.as<uint32_t>() : nullptr;
     pp.pack3           = pack3 ? 1u : 0u;
+    pp.fmt_cnt         = mat ? nullptr : small.as<uint32_t>() + 10;  // (u64 slot 5 of small: zeroed by the R scatter)
     const size_t   pl_lds = probe_lds_bytes(g, nullptr, mat != nullptr);
     const uint32_t PG = (uint32_t) cus_ * (uint32_t) std::max<size_t>(1, std::min<size_t>(2, 163840 / pl_lds));
     const bool dbg_on = dbg;  // dev-only phase stamps (HWBRJ_DBG)
@@ -691,6 +695,7 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     jp.jkind           = (uint32_t) jkind;
     jp.split_surv      = test_hooks().join_split;  // (tests: force the skew split)
     jp.r_pack3         = pack3 ? 1u : 0u;
+    jp.fmt_cnt         = pp.fmt_cnt;
     if (mat) {
         // (k_join_split, which leaves job_surv zero for the next join, does not run here)
         HWBRJ_CHECK(hipMemsetAsync(jparts.as<uint32_t>() + NJ, 0, (size_t) NJ * 4, stream));
@@ -729,6 +734,7 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     pending_nS_   = nS;
     pending_ev_   = phase_ev_;
     pending_sfirst_ = s_first;
+    pending_fmt_    = pp.fmt_cnt != nullptr;
     pending_stream_ = stream;
     have_filter_  = args != nullptr;
     last_g_       = g;
@@ -1007,6 +1013,7 @@ int Engine::enqueue_basic_kk(const uint2* dR, uint64_t nR, const uint2* dS, uint
     pending_nS_   = nS;
     pending_ev_   = phase_ev_;
     pending_sfirst_ = false;
+    pending_fmt_    = false;
     pending_stream_ = stream;
     have_filter_  = true;
     last_g_       = g;
@@ -1029,8 +1036,9 @@ int Engine::wait(hwbrj_stats_t* st) {
     const uint32_t  nseg = (g.mode == MODE_SLICE_BLOCK || g.mode == MODE_SLICE_BASIC) ? g.nseg : 1;
     const uint64_t* d_result   = small.as<uint64_t>();      // (see enqueue)
     const uint64_t* d_filtered = small.as<uint64_t>() + 2;
-    uint64_t small_h[5] = {0, 0, 0, 0, 0};  // matches, dcount, filtered, probe ticks, join ticks
+    uint64_t small_h[6] = {0, 0, 0, 0, 0, 0};  // matches, dcount, filtered, probe ticks, join ticks, unstaged items
     HWBRJ_CHECK(hipMemcpy(small_h, d_result, sizeof small_h, hipMemcpyDeviceToHost));
+    if (pending_fmt_) pack3_hint_ = (uint32_t) small_h[5] == 0;  // (k_probe's count, ProbeParams::fmt_cnt)
     (void) d_filtered;
     const uint64_t matches = small_h[0], filtered = small_h[2];
     if (st) {

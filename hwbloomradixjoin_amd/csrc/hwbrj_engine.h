@@ -118,6 +118,8 @@ class Engine {
     // joins enqueued on it (a destroyed stream's handle can be reused by a new one).
     hipStream_t  pending_stream_ = nullptr;
     bool         pending_sfirst_ = false;  // the pending join ran its S pass first (phase boundaries)
+    bool         pending_fmt_    = false;  // the pending join counted its unstaged probe items
+    bool         pack3_hint_     = true;   // the last waited join had none: 3-byte join keys pay
     int          pending_rc_     = 0;   // nonzero: the pending join failed after enqueuing kernels
     std::string  pending_err_;
     bool         surv_fused_   = false;

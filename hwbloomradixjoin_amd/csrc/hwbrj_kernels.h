@@ -85,8 +85,10 @@ struct ProbeParams {
     uint32_t*        wg_cnt;      // k_probe_bitj: words appended to workgroup w's region
                                   // (surv + w * surv_seg_stride)
     uint64_t*        dbg;         // dev-only: per-workgroup phase cycles (HWBRJ_DBG), or nullptr
-    uint32_t         pack3;       // 1: survivor runs hold 3-byte join keys (code >> hash_shift) at
-                                  // 3 bytes per key from the item region's byte 0 (hash_shift >= 8)
+    uint32_t         pack3;       // 1: staged items store 3-byte join keys (code >> hash_shift), 3
+                                  // bytes per key from the item region's byte 0, flagged by bit 31 of
+                                  // their surv_off entries (unstaged items keep 32-bit codes)
+    uint32_t*        fmt_cnt;     // pack3: += the unstaged items (zeroed by the R scatter), or nullptr
 };
 
 struct JoinParams {
@@ -115,8 +117,9 @@ struct JoinParams {
                                   // table, PRO), 1 histogram join (PRH), 2 + 16-byte compares (PRHO)
     const uint64_t* item_base;    // [items] survivor region of each item (partitioned multi-GPU
                                   // join: received runs), or nullptr (k_probe's item regions)
-    uint32_t        r_pack3;      // 1: r_codes and surv hold 3-byte join keys (BuildParams::pack3,
-                                  // ProbeParams::pack3)
+    uint32_t        r_pack3;      // 1: r_codes hold 3-byte join keys (BuildParams::pack3); survivor
+                                  // runs say so per item (bit 31 of surv_off)
+    const uint32_t* fmt_cnt;      // ProbeParams::fmt_cnt (the launch's survivor-run formats), or nullptr
 };
 
 // The materializing join (k_join_mat): R codes + payloads of the build sweeps, survivors + their

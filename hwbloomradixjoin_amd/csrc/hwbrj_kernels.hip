@@ -1817,7 +1817,9 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
     constexpr uint32_t kNoItem = 0x80000000u;
     uint32_t  prev_total = 0, prev_it = kNoItem, prev_buf = 0, subc_v = 0, subo_v = 0, prev_q = 0;
     uint32_t* prev_out   = P.surv;
-    const bool pk3       = !PAY && P.pack3 != 0;  // 3-byte join keys (uniform)
+    const bool pk3       = !PAY && P.pack3 != 0;  // 3-byte join keys for staged items
+    bool       prev_pk   = false;  // the previous item's run is staged and stored as 3-byte keys
+    uint32_t   n_unst    = 0;      // items of this workgroup too large for the stage (32-bit runs)
     auto copy_out = [&]() {
         const uint32_t nbytes = ((prev_total + 3u) & ~3u) * 4u;  // item region holds round_up(total, 4)
         const auto     ro     = buf_rsrc(prev_out, nbytes);
@@ -1832,7 +1834,7 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
                 __builtin_amdgcn_raw_buffer_store_b128(src[j], ro, i * 16, 0, 0);
                 __builtin_amdgcn_raw_buffer_store_b128(src[hp / 4 + j], rp, i * 16, 0, 0);
             }
-        } else if (pk3) {  // 3-byte keys: 12 bytes per staged quad (whole quads: the item
+        } else if (prev_pk) {  // 3-byte keys: 12 bytes per staged quad (whole quads: the item
                                // region holds round_up(total, 4) words, more than these bytes)
             const auto rp3 = buf_rsrc(prev_out, (prev_total + 3u) / 4u * 12u);
 #pragma unroll
@@ -1857,7 +1859,7 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
         // atomic; only wave 0's first NSUB lanes are in range)
         const auto rj = buf_rsrc(P.job_surv + (uint64_t) prev_q * NSUB, tb);
         __builtin_amdgcn_raw_ptr_buffer_atomic_add_i32((int) subc_v, rj, tid * 4, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b32(subo_v, rf, tid * 4, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(subo_v | (prev_pk ? 0x80000000u : 0u), rf, tid * 4, 0, 0);
     };
     uint64_t filtered = 0;  // wave 0: survivors of this workgroup's items
     uint32_t nstep    = 0;  // items processed (selects the counter / stage buffers)
@@ -2095,18 +2097,6 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
             const bool     staged = PAY ? total <= hp : total <= scap;
             uint32_t*      stg    = stage + buf * sstr;
             const auto     ro     = buf_rsrc(out, total * 4);
-            // an unstaged survivor straight to its slot o (out-of-range offsets: dropped); 3-byte
-            // keys as three byte stores (neighbouring keys share words)
-            auto put = [&](uint32_t c, bool ok, uint32_t o) {
-                if (pk3) {
-                    const uint32_t v = c >> g.hash_shift, b = ok ? o * 3u : 0x7FFFFFF0u;
-                    __builtin_amdgcn_raw_buffer_store_b8((uint8_t) v, ro, b, 0, 0);
-                    __builtin_amdgcn_raw_buffer_store_b8((uint8_t) (v >> 8), ro, b + 1u, 0, 0);
-                    __builtin_amdgcn_raw_buffer_store_b8((uint8_t) (v >> 16), ro, b + 2u, 0, 0);
-                } else {
-                    __builtin_amdgcn_raw_buffer_store_b32(c, ro, ok ? o * 4u : 0x7FFFFFF0u, 0, 0);
-                }
-            };
             if (kAblProbe == 1 || kAblProbe == 2) {
             } else if (dense) {
 #pragma unroll
@@ -2115,7 +2105,7 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
                     const uint32_t c  = decode_k<KIND>(scr[lane + 64u * k], q, g);
                     const uint32_t o  = subo[dr[k] & 0xFFFFu] + (dr[k] >> 16);
                     if (staged) stg[ok ? o : scap + lane] = c;
-                    else put(c, ok, o);
+                    else __builtin_amdgcn_raw_buffer_store_b32(c, ro, ok ? o * 4 : 0x7FFFFFF0u, 0, 0);
                 }
             } else if (staged) {  // LDS stage (copied out coalesced at the next piece)
 #pragma unroll
@@ -2134,7 +2124,7 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
                     const uint32_t c  = decode_k<KIND>(sweep_word(Sc, i >> 2, i & 3), q, g);
                     const uint32_t o  = subo[(c >> g.sub_shift) & (NSUB - 1u)] + ((rank2[i / 2] >> (16 * (i & 1))) & 0xFFFFu);
                     const uint32_t oo = ((pass >> i) & 1u) ? o * 4 : 0x7FFFFFF0u;
-                    put(c, ((pass >> i) & 1u) != 0, o);
+                    __builtin_amdgcn_raw_buffer_store_b32(c, ro, oo, 0, 0);
                     if (PAY)
                         __builtin_amdgcn_raw_buffer_store_b32(Sc.id[i >> 2] * 32u + ((uint32_t) tid & 7u) * 4u + (uint32_t) (i & 3),
                                                               rpo, oo, 0, 0);
@@ -2142,6 +2132,8 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
             }
             stamp(4);
             prev_total = staged ? total : 0u;
+            prev_pk    = pk3 && staged;
+            n_unst += staged ? 0u : 1u;
             prev_out   = out;
             prev_buf   = buf;
             prev_it    = rit0 + (p - p0);
@@ -2159,6 +2151,7 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
     __syncthreads();  // the last piece is staged
     copy_out();
     if (tid == 0 && filtered) atomicAdd((unsigned long long*) P.filtered, (unsigned long long) filtered);
+    if (tid == 0 && n_unst && P.fmt_cnt) atomicAdd(P.fmt_cnt, n_unst);
     if (kAblProbe == 1 || kAblProbe == 2)
         if (lane == 0 && abl_n) atomicAdd((unsigned long long*) P.filtered, (unsigned long long) abl_n);
     if (P.dbg && tid == 0)
@@ -2421,7 +2414,9 @@ __global__ __launch_bounds__(256) void k_join_split(const uint32_t* __restrict__
     nparts[job] = np;
 }
 
-__global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
+// One (job, part) of the join on workgroup slot blk; MIXED: survivor runs of both formats (below).
+template <bool MIXED>
+__device__ __forceinline__ void join_job(const JoinParams& P, const uint32_t blk) {
     __shared__ __attribute__((aligned(16))) uint32_t tab[kJoinWords];  // bitmap or hash table
     __shared__ uint64_t dbase[kJoinDesc];  // run starts (byte offsets) of a batch: S survivor runs
     __shared__ uint32_t dcnt[kJoinDesc];
@@ -2431,16 +2426,16 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
     __shared__ uint64_t wsum[kJoinWaves];
     __shared__ uint32_t dupflag, npieces;
     const uint32_t NSUB = 1u << P.log2NSUB;
-    uint32_t       job = blockIdx.x, part = 0;  // workgroup j < jobs: part 0 of job j
+    uint32_t       job = blk, part = 0;  // workgroup j < jobs: part 0 of job j
 #ifndef HWBRJ_JXCD
 #define HWBRJ_JXCD 1
 #endif
     // XCD-aware job order: blocks b, b + 8, ... share an XCD (dealt round-robin), so they take
     // consecutive jobs -- the 16 subs of a partition run on one XCD, where the lines their runs
     // share (adjacent sub runs in every sweep slot and item region) are fetched into its L2 once
-    if (HWBRJ_JXCD && blockIdx.x < P.jobs && (P.jobs & 7u) == 0) job = (blockIdx.x & 7u) * (P.jobs >> 3) + (blockIdx.x >> 3);
-    if (blockIdx.x >= P.jobs) {                 // extra workgroups: further parts of skewed jobs
-        const uint32_t e = blockIdx.x - P.jobs;
+    if (HWBRJ_JXCD && blk < P.jobs && (P.jobs & 7u) == 0) job = (blk & 7u) * (P.jobs >> 3) + (blk >> 3);
+    if (blk >= P.jobs) {                 // extra workgroups: further parts of skewed jobs
+        const uint32_t e = blk - P.jobs;
         if (e >= min(*P.nextra, kJoinExtra)) return;
         const uint2 x = P.extra[e];
         job           = x.x;
@@ -2450,6 +2445,7 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
     const uint32_t w0 = P.r_sweep_start[q], w1 = P.r_sweep_start[q + 1];
     const uint32_t qi0 = P.item_start[q], qi1 = P.item_start[q + 1];  // q's items (segment-major)
     const uint32_t np  = P.nparts[job];
+    const bool     rpk = P.r_pack3 != 0;
     const uint32_t i0  = qi0 + (uint32_t) ((uint64_t) (qi1 - qi0) * part / np);
     const uint32_t i1  = qi0 + (uint32_t) ((uint64_t) (qi1 - qi0) * (part + 1) / np);
     if (w1 == w0 || i1 == i0) return;
@@ -2480,65 +2476,85 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
         (void) k;
 #endif
     };
-    // The words [from, n) of one run (long runs: high-selectivity survivors, large R runs), with
-    // kJoinTailU loads in flight per lane instead of one dependent load per iteration.
-    // Runs are addressed by byte offsets from their array's base: with pack3 (P.r_pack3, both
-    // sides) key o of a run at byte b is the low 24 bits of the unaligned dword at b + 3 o, else
-    // v = (the code at b + 4 o) >> sh. Stride, shift and mask are uniform: one mad, one load, one
-    // shift and one and per key, no per-run state. The loads stay raw until used (key()): ALU work
-    // on a conditionally loaded value would make the wave wait for it at once.
-    const uint32_t kst = P.r_pack3 ? 3u : 4u, ksh = P.r_pack3 ? 0u : sh, kmk = P.r_pack3 ? 0xFFFFFFu : 0xFFFFFFFFu;
-    auto ldv = [&](const uint8_t* b8, uint64_t b, uint32_t o) -> uint32_t {
-        return *(const u32_unaligned*) (b8 + b + o * kst);
-    };
-    auto key = [&](uint32_t x) -> uint32_t { return (x >> ksh) & kmk; };
+    // Run formats. A run is addressed by a tagged byte offset tb from its array's base: bit 63 set =
+    // 3-byte keys (pack3), key o the low 24 bits of the unaligned dword at tb + 3 o; else 32-bit
+    // codes at tb + 4 o, key = code >> sh. R runs share one format (the build's); survivor runs are
+    // packed when their probe item was staged (bit 31 of surv_off). P.fmt_cnt counts the unstaged
+    // items: with none (or no pack3 at all) every run of the launch has one format, whose stride,
+    // shift and mask are uniform (k_join); otherwise the survivor runs are mixed and read with a
+    // per-run format (k_join_mixed: only where probe items overflow their stage), R runs packed.
+    // Loads stay raw until used (key()): ALU work on a conditionally loaded value would make the
+    // wave wait for it at once.
+    constexpr uint64_t kPk = 1ull << 63;
+    const uint32_t kst = rpk ? 3u : 4u, ksh = rpk ? 0u : sh, kmk = rpk ? 0xFFFFFFu : 0xFFFFFFFFu;
     const uint8_t* const r8 = (const uint8_t*) P.r_codes;
     const uint8_t* const s8 = (const uint8_t*) P.surv;
+    using SideR = std::integral_constant<int, 0>;
+    using SideS = std::integral_constant<int, 1>;
     // R run of (sweep, sub) at key offset off of the sweep's slot; survivor run at key offset off of
     // the item region at element e0 (regions and slots keep their 4-byte-per-key sizes)
     auto rtag = [&](uint32_t sweep, uint32_t off) -> uint64_t {
-        return (uint64_t) sweep * P.slot * 4u + (uint64_t) off * kst;
+        return rpk ? kPk | ((uint64_t) sweep * P.slot * 4u + (uint64_t) off * 3u) : ((uint64_t) sweep * P.slot + off) * 4u;
     };
-    auto stag = [&](uint64_t e0, uint32_t off) -> uint64_t { return e0 * 4u + (uint64_t) off * kst; };
-    auto tail_run = [&](const uint8_t* data, uint64_t bb, uint32_t from, uint32_t n, auto&& op) {
+    auto stag = [&](uint64_t e0, uint32_t offw) -> uint64_t {
+        const uint64_t off = offw & 0x7FFFFFFFu;
+        return (offw >> 31) ? kPk | (e0 * 4u + off * 3u) : (e0 + off) * 4u;
+    };
+    auto body = [&]() {
+    auto ldv = [&](auto side_c, uint64_t tb, uint32_t o) -> uint32_t {
+        constexpr int SIDE = decltype(side_c)::value;
+        uint32_t      st   = kst;
+        if constexpr (MIXED) st = (tb & kPk) ? 3u : 4u;
+        return *(const u32_unaligned*) ((SIDE == 0 ? r8 : s8) + (tb & ~kPk) + o * st);
+    };
+    auto key = [&](auto side_c, uint32_t x, bool pk) -> uint32_t {  // (side_c: as ldv's, unused)
+        (void) side_c;
+        if constexpr (MIXED) return pk ? x & 0xFFFFFFu : x >> sh;
+        (void) pk;
+        return (x >> ksh) & kmk;
+    };
+    // The words [from, n) of one run (long runs: high-selectivity survivors, large R runs), with
+    // kJoinTailU loads in flight per lane instead of one dependent load per iteration.
+    auto tail_run = [&](auto side_c, uint64_t bb, uint32_t from, uint32_t n, auto&& op) {
         for (uint32_t o = from + lane; o < n; o += 64u * kJoinTailU) {
             uint32_t v[kJoinTailU];
 #pragma unroll
             for (int u = 0; u < (int) kJoinTailU; u++) {
                 const uint32_t oo = o + 64u * u;
-                v[u]              = oo < n ? ldv(data, bb, oo) : 0u;
+                v[u]              = oo < n ? ldv(side_c, bb, oo) : 0u;
             }
 #pragma unroll
             for (int u = 0; u < (int) kJoinTailU; u++)
-                if (o + 64u * u < n) op(key(v[u]));
+                if (o + 64u * u < n) op(key(side_c, v[u], (bb & kPk) != 0));
         }
     };
     // Every word of runs [da, db) of a descriptor batch through op(word): a wave per run, RUNS runs
     // in flight per wave with WPL words per lane each; longer runs finish in a tail loop.
-    auto walk = [&](auto runs_c, auto wpl_c, const uint8_t* data, const uint32_t* nc,
+    auto walk = [&](auto runs_c, auto wpl_c, auto side_c, const uint32_t* nc,
                     const uint64_t* nb, uint32_t da, uint32_t db, auto&& op) {
         constexpr int RUNS = decltype(runs_c)::value, WPL = decltype(wpl_c)::value;
         for (uint32_t d = da + wave; d < db; d += kJoinWaves * RUNS) {
-            uint32_t v[RUNS][WPL], n[RUNS];
+            uint32_t v[RUNS][WPL], n[RUNS], pkm = 0;  // pkm bit r: run r holds 3-byte keys
 #pragma unroll
             for (int r = 0; r < RUNS; r++) {
                 const uint32_t dd = d + r * kJoinWaves;
                 n[r]              = dd < db ? nc[dd] : 0u;
                 const uint64_t bb = dd < db ? nb[dd] : 0ull;
+                pkm |= (uint32_t) (bb >> 63) << r;
 #pragma unroll
                 for (int j = 0; j < WPL; j++) {
                     const uint32_t o = lane + 64u * j;
-                    v[r][j]          = o < n[r] ? ldv(data, bb, o) : 0u;
+                    v[r][j]          = o < n[r] ? ldv(side_c, bb, o) : 0u;
                 }
             }
 #pragma unroll
             for (int r = 0; r < RUNS; r++) {
 #pragma unroll
                 for (int j = 0; j < WPL; j++)
-                    if (lane + 64u * j < n[r]) op(key(v[r][j]));
+                    if (lane + 64u * j < n[r]) op(key(side_c, v[r][j], (pkm >> r) & 1u));
                 if (n[r] > 64u * WPL) {
                     const uint64_t bb = nb[d + r * kJoinWaves];
-                    tail_run(data, bb, 64u * WPL, n[r], op);
+                    tail_run(side_c, bb, 64u * WPL, n[r], op);
                 }
             }
         }
@@ -2570,7 +2586,7 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
                                   P.surv_off[(uint64_t) it * NSUB + s]);
             }
             __syncthreads();
-            walk(SR{}, SW{}, s8, dcnt, dbase, 0, nd, op);
+            walk(SR{}, SW{}, SideS{}, dcnt, dbase, 0, nd, op);
         }
         probe_end();
     };
@@ -2629,7 +2645,7 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
 #define HWBRJ_JFS HWBRJ_JSR
 #endif
         constexpr int FS = HWBRJ_JFS, FSW = HWBRJ_JSW;  // survivor runs per wave loaded with R's
-        uint32_t rv[FR][FW], rn[FR], sv[FS][FSW], sn[FS];
+        uint32_t rv[FR][FW], rn[FR], sv[FS][FSW], sn[FS], spk = 0;  // spk bit r: survivor run r packed
 #pragma unroll
         for (int r = 0; r < FR; r++) {
             const uint32_t dd = wave + r * kJoinWaves;
@@ -2641,7 +2657,7 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
 #pragma unroll
             for (int j = 0; j < FW; j++) {
                 const uint32_t o = lane + 64u * j;
-                rv[r][j]         = o < rn[r] ? ldv(r8, bb, o) : 0u;
+                rv[r][j]         = o < rn[r] ? ldv(SideR{}, bb, o) : 0u;
             }
         }
 #pragma unroll
@@ -2652,10 +2668,11 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
             sn[r] = 0;  // dev ablation (results invalid)
 #endif
             const uint64_t bb = dd < nSd ? dbase[dd] : 0ull;
+            spk |= (uint32_t) (bb >> 63) << r;
 #pragma unroll
             for (int j = 0; j < FSW; j++) {
                 const uint32_t o = lane + 64u * j;
-                sv[r][j]         = o < sn[r] ? ldv(s8, bb, o) : 0u;
+                sv[r][j]         = o < sn[r] ? ldv(SideS{}, bb, o) : 0u;
             }
         }
         // bits set without returns (no wave waits on them); a duplicate R key shows as fewer set
@@ -2665,10 +2682,10 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
         for (int r = 0; r < FR; r++) {
 #pragma unroll
             for (int j = 0; j < FW; j++)
-                if (lane + 64u * j < rn[r]) set(key(rv[r][j]));
+                if (lane + 64u * j < rn[r]) set(key(SideR{}, rv[r][j], rpk));
             if (rn[r] > 64u * FW) {  // (rare) longer run
                 const uint64_t bb = rbase[wave + r * kJoinWaves];
-                tail_run(r8, bb, 64u * FW, rn[r], set);
+                tail_run(SideR{}, bb, 64u * FW, rn[r], set);
             }
         }
         __syncthreads();
@@ -2692,15 +2709,15 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
             for (int r = 0; r < FS; r++) {
 #pragma unroll
                 for (int j = 0; j < FSW; j++)
-                    if (lane + 64u * j < sn[r]) test(key(sv[r][j]));
+                    if (lane + 64u * j < sn[r]) test(key(SideS{}, sv[r][j], (spk >> r) & 1u));
                 if (sn[r] > 64u * FSW) {
                     const uint64_t bb = dbase[wave + r * kJoinWaves];
-                    tail_run(s8, bb, 64u * FSW, sn[r], test);
+                    tail_run(SideS{}, bb, 64u * FSW, sn[r], test);
                 }
             }
             stamp(3);
 #ifndef HWBRJ_ABL_JNOS
-            walk(SR{}, SW{}, s8, dcnt, dbase, (uint32_t) (kJoinWaves * FS), nSd, test);
+            walk(SR{}, SW{}, SideS{}, dcnt, dbase, (uint32_t) (kJoinWaves * FS), nSd, test);
 #endif
             stamp(4);
             probe_end();
@@ -2714,7 +2731,7 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
         for (uint32_t d0 = w0; d0 < w1; d0 += kJoinDesc) {
             const uint32_t nd = min(kJoinDesc, w1 - d0);
             load_r(d0, nd);
-            walk(RR{}, RW{}, r8, rcnt, rbase, 0, nd, [&](uint32_t x) {
+            walk(RR{}, RW{}, SideR{}, rcnt, rbase, 0, nd, [&](uint32_t x) {
                 const uint32_t bit = 1u << (x & 31u);
                 dup |= atomicOr(&tab[x >> 5], bit) & bit;
             });
@@ -2751,7 +2768,7 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
                     for (uint32_t i = tid; i < kJoinT / 4; i += kJoinThreads)
                         ((uint4*) tab)[i] = make_uint4(kEmpty, kEmpty, kEmpty, kEmpty);
                     __syncthreads();
-                    walk(RR{}, RW{}, r8, rcnt, rbase, da, db, [&](uint32_t x) { join_insert(tab, x); });
+                    walk(RR{}, RW{}, SideR{}, rcnt, rbase, da, db, [&](uint32_t x) { join_insert(tab, x); });
                     probe_survivors([&](uint32_t x) { cnt += join_count(tab, x); });  // (starts with a barrier)
                     continue;
                 }
@@ -2769,7 +2786,7 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
                 uint32_t* hist = tab + kJoinPiece;
                 for (uint32_t i = tid; i < NH + 2; i += kJoinThreads) hist[i] = 0;
                 __syncthreads();
-                walk(RR{}, RW{}, r8, rcnt, rbase, da, db, [&](uint32_t x) { atomicAdd(&hist[(x & (NH - 1u)) + 2], 1u); });
+                walk(RR{}, RW{}, SideR{}, rcnt, rbase, da, db, [&](uint32_t x) { atomicAdd(&hist[(x & (NH - 1u)) + 2], 1u); });
                 __syncthreads();
                 if (wave == 0) {  // inclusive prefix sum of hist[2, NH + 2): 16 buckets per lane
                     const uint32_t per = (NH + 63) / 64, b0 = 2 + lane * per;
@@ -2784,7 +2801,7 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
                         }
                 }
                 __syncthreads();
-                walk(RR{}, RW{}, r8, rcnt, rbase, da, db, [&](uint32_t x) {
+                walk(RR{}, RW{}, SideR{}, rcnt, rbase, da, db, [&](uint32_t x) {
                     keys[atomicAdd(&hist[(x & (NH - 1u)) + 1], 1u)] = x;  // bucket b: [hist[b], hist[b + 1])
                 });
                 if (P.jkind == 1) {
@@ -2805,13 +2822,15 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
             }
         }
     }
+    };
+    body();
     cnt = wave_sum_u64(cnt);
     if (lane == 0) wsum[wave] = cnt;
     __syncthreads();
     if (tid == 0) {
         uint64_t t = 0;
         for (int w = 0; w < kJoinWaves; w++) t += wsum[w];
-        uint64_t* slot = &P.jsum[(blockIdx.x % kJoinSumSlots) * kJoinSumStride];
+        uint64_t* slot = &P.jsum[(blk % kJoinSumSlots) * kJoinSumStride];
         if (t) atomicAdd((unsigned long long*) slot, (unsigned long long) t);
         atomicAdd((unsigned long long*) (slot + 1), (unsigned long long) t_probe);
         atomicAdd((unsigned long long*) (slot + 2), (unsigned long long) (wall_clock64() - t_start));
@@ -2819,8 +2838,25 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
     stamp(5);
 #ifdef HWBRJ_STAMPS
     if (P.dbg && tid == 0)
-        for (int k = 0; k < 6; k++) atomicAdd((unsigned long long*) &P.dbg[(blockIdx.x & 1023u) * 8 + k], (unsigned long long) tph[k]);
+        for (int k = 0; k < 6; k++) atomicAdd((unsigned long long*) &P.dbg[(blk & 1023u) * 8 + k], (unsigned long long) tph[k]);
 #endif
+}
+
+// The uniform-format join (every launch without unstaged probe items, the north star's) and the
+// mixed one; both are launched, the one whose case this is not returns at once. The mixed one runs
+// on a small grid of persistent workgroups (an empty launch of it costs ~1 us, a full grid ~14 us);
+// it is rare: the Engine stops packing after a join that had unstaged items (pack3_hint_).
+__global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
+    if (P.r_pack3 && P.fmt_cnt && *P.fmt_cnt) return;
+    join_job<false>(P, blockIdx.x);
+}
+
+__global__ __launch_bounds__(kJoinThreads) void k_join_mixed(JoinParams P) {
+    if (!(P.r_pack3 && P.fmt_cnt && *P.fmt_cnt)) return;
+    for (uint32_t b = blockIdx.x; b < P.jobs + kJoinExtra; b += gridDim.x) {
+        __syncthreads();  // the previous job's LDS reads are done
+        join_job<true>(P, b);
+    }
 }
 
 // result[0] += matches; result[3], result[4] += probe / total ticks of the join workgroups
@@ -3933,6 +3969,7 @@ void launch_join(const JoinParams& p0, uint32_t jobs, uint32_t* job_surv, hipStr
     k_join_split<<<(jobs + 255) / 256, 256, 0, st>>>(p.item_start, job_surv, p.log2NSUB, jobs, split,
                                                      p.nparts, p.extra, p.nextra, p.jsum);
     k_join<<<jobs + kJoinExtra, kJoinThreads, 0, st>>>(p);
+    k_join_mixed<<<std::min<uint32_t>(jobs + kJoinExtra, 1024u), kJoinThreads, 0, st>>>(p);
     k_join_sum<<<1, kJoinSumSlots, 0, st>>>(p.jsum, p.result);
 }
 
