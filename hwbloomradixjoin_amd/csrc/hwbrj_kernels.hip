@@ -1744,6 +1744,8 @@ constexpr int kAblProbe = HWBRJ_ABL_PROBE;
 #define HWBRJ_PCO_AUX 0
 #endif
 constexpr int kPco = HWBRJ_PCO < kPC ? HWBRJ_PCO : kPC;
+// without slices (PRO, the global-bitmap fallback) the stage can hold a whole item: kPC stores
+template <int KIND> constexpr int probe_pco() { return KIND == KIND_PASS ? kPC : kPco; }
 
 __device__ __forceinline__ uint32_t find_q(const uint32_t* item_start, uint32_t F, uint32_t it) {
     uint32_t lo = 0, hi = F - 1;
@@ -1838,14 +1840,14 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
                                // region holds round_up(total, 4) words, more than these bytes)
             const auto rp3 = buf_rsrc(prev_out, (prev_total + 3u) / 4u * 12u);
 #pragma unroll
-            for (int k = 0; k < kPco; k++) {
+            for (int k = 0; k < probe_pco<KIND>(); k++) {
                 const uint32_t i = tid + k * NT;
                 const v4u      v = src[min(i, scap / 4 - 1)];
                 __builtin_amdgcn_raw_buffer_store_b96(pack3x4(v, g.hash_shift), rp3, i * 12, 0, HWBRJ_PCO_AUX);
             }
         } else {
 #pragma unroll
-        for (int k = 0; k < kPco; k++) {
+        for (int k = 0; k < probe_pco<KIND>(); k++) {
             const uint32_t i = tid + k * NT;
             const v4u      v = src[min(i, scap / 4 - 1)];  // reads past the stage are never stored
             __builtin_amdgcn_raw_buffer_store_b128(v, ro, i * 16, 0, HWBRJ_PCO_AUX);
@@ -3940,7 +3942,7 @@ size_t probe_lds_bytes(const Geometry& g, uint32_t* stage_cap, bool pay) {
     // 2 buffers of cap words + 64 dummy slots each, in what the 512-byte static table leaves
     // (pay: codes and positions, half a buffer each)
     size_t cap = std::min<size_t>(kProbeCH * 32, (163840 - 512 - base) / 8 - 64) & ~(size_t) 7;
-    if (!pay) cap = std::min<size_t>(cap, (size_t) kPco * 4096);  // what the copy-out's stores cover
+    if (!pay) cap = std::min<size_t>(cap, (size_t) (slices ? kPco : kPC) * 4096);  // what the copy-out's stores cover
     if (stage_cap) *stage_cap = (uint32_t) cap;
     return base + 2 * (cap + 64) * 4;
 }
