@@ -16,7 +16,7 @@ from collections import defaultdict
 
 # kernel -> phase (hwbrj_engine.cpp Engine::enqueue)
 PHASE_OF = {"k_build_global": "build", "k_build": "build", "k_probe_global": "probe",
-            "k_probe": "probe", "k_join_split": "join", "k_join": "join", "k_join_sum": "join", "k_plan": "index",
+            "k_probe": "probe", "k_join_split": "join", "k_join": "join", "k_join_mixed": "join", "k_join_sum": "join", "k_plan": "index",
             "k_list_fill": "index", "k_mat_build": "materialize", "k_mat_probe": "materialize"}
 
 
