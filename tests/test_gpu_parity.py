@@ -478,3 +478,32 @@ def test_join_skew_split_forced(hw, cuda, orc, gen3, split, hook):
             st = hw.join_device(to_dev(cuda, R), to_dev(cuda, S), args)
             res, filt, _ = orc.bpro(R, S, 8, 1 if args else 0, 1 << 24, 1, 1024, args is not None)
             assert (st.filtered, st.matches) == (filt, res)
+
+
+def test_join_key_formats_across_launches(hw, cuda, orc):
+    """3-byte join keys (pack3): a probe item whose survivors overflow its LDS stage
+    keeps 32-bit survivor runs, so a launch can hold both formats (k_join_mixed), and the Engine
+    stops packing after a join that had such items (pack3_hint_). At the north star's filter size
+    (stage of 2592 words per 12288-tuple item), S with ~21 % members puts some items over the
+    stage and some under. The sequence low, low (packed), mid (mixed launch), mid (32-bit), low
+    (32-bit), low (packed again) must count what the oracle counts every time."""
+    rng = np.random.default_rng(23)
+    nR, nS = 1 << 20, 1 << 24
+    Rk = rng.permutation(nR).astype(np.int64) + 1
+    outside = lambda n: rng.integers(2 * nR, INT_MAX, size=n)  # never in R
+    S_lo = np.concatenate([rng.integers(1, nR + 1, size=nS // 100), outside(nS - nS // 100)])
+    S_mid = np.concatenate([rng.integers(1, nR + 1, size=nS * 21 // 100), outside(nS - nS * 21 // 100)])
+    rng.shuffle(S_lo)
+    rng.shuffle(S_mid)
+    args = hw.BloomFilterArgs(hw.BLOCKED, 1 << 30, 1, 1024)
+    want = {}
+    for name, Sk in (("lo", S_lo), ("mid", S_mid)):
+        R = np.stack([Rk.astype(np.int32), np.arange(nR, dtype=np.int32)], 1)
+        S = np.stack([Sk.astype(np.int32), np.arange(nS, dtype=np.int32)], 1)
+        res, filt, _ = orc.bpro(R, S, 8, args.variant, args.m, args.k, args.B)
+        assert res == int(np.isin(Sk, Rk).sum())
+        want[name] = (filt, res, to_dev(cuda, R), to_dev(cuda, S))
+    for name in ("lo", "lo", "mid", "mid", "lo", "lo"):
+        filt, res, dR, dS = want[name]
+        st = hw.join_device(dR, dS, args)
+        assert (st.filtered, st.matches) == (filt, res), (name, st)
