@@ -2502,7 +2502,6 @@ __device__ __forceinline__ void join_job(const JoinParams& P, const uint32_t blk
         const uint64_t off = offw & 0x7FFFFFFFu;
         return (offw >> 31) ? kPk | (e0 * 4u + off * 3u) : (e0 + off) * 4u;
     };
-    auto body = [&]() {
     auto ldv = [&](auto side_c, uint64_t tb, uint32_t o) -> uint32_t {
         constexpr int SIDE = decltype(side_c)::value;
         uint32_t      st   = kst;
@@ -2824,8 +2823,6 @@ __device__ __forceinline__ void join_job(const JoinParams& P, const uint32_t blk
             }
         }
     }
-    };
-    body();
     cnt = wave_sum_u64(cnt);
     if (lane == 0) wsum[wave] = cnt;
     __syncthreads();
