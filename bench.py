@@ -74,11 +74,13 @@ def parse():
     return ap.parse_args()
 
 
+JOIN_KEY_NAMES = {0: "32-bit codes", 1: "3-byte keys (pack3)", 2: "mixed (3-byte, unstaged items 32-bit)"}
+
+
 def join_key_bytes(st) -> float:
-    """Bytes per join key between build/probe and k_join: 3 when v = code >> hash_shift fits 24
-    bits (hash_shift = log2(F) + log2(subparts) >= 8 where the partition digit is a code digit, i.e.
-    not the slice-basic mode 2; hwbrj_kernels.h join_pack3), else 4."""
-    return 3.0 if st.mode != 2 and st.partitions * st.subparts >= 256 else 4.0
+    """Bytes per join key between build/probe and k_join, as the join ran them (hwbrj_stats_t
+    join_keys): 3 for 3-byte keys (the mixed format's unstaged runs are a small share), else 4."""
+    return 3.0 if st.join_keys in (1, 2) else 4.0
 
 
 def modeled_bytes(nR: int, nS: int, filtered: int, m: int, word_bytes: float, key_bytes: float = 4.0) -> dict:
@@ -264,7 +266,10 @@ def main():
                 "algorithmic_bytes": alg_bytes, "launch": "one full join (every kernel of BPRO)",
                 "launch_ms": round(dev_ms, 4),
                 "modeled_bytes": modeled_bytes(nR, nS, st.filtered, a.bloom_size if args else 0,
-                                               word_bytes, join_key_bytes(st)),
+                                               word_bytes, join_key_bytes(last)),
+                "join_keys": {"format": JOIN_KEY_NAMES.get(last.join_keys), "unstaged_items": last.unstaged_items,
+                              "what": "the key format the timed joins handed to k_join (the last one's "
+                                      "hwbrj_stats_t.join_keys)"},
                 "pmc_source": os.path.relpath(a.pmc_json, ROOT) if pm else None,
                 "pmc_library": pm.get("library") if pm else None,
                 "traffic_note": pmc_note,

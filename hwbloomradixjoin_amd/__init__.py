@@ -58,7 +58,11 @@ class _Stats(ctypes.Structure):  # include/hwbrj.h hwbrj_stats_t
                 ("subparts", ctypes.c_uint32), ("slice_segments", ctypes.c_uint32)] + [
                     (n, ctypes.c_double) for n in (
                         "ms_total", "ms_r_scatter", "ms_r_index", "ms_build", "ms_s_scatter",
-                        "ms_s_index", "ms_probe", "ms_surv", "ms_join", "ms_join_probe")]
+                        "ms_s_index", "ms_probe", "ms_surv", "ms_join", "ms_join_probe")] + [
+                    ("join_keys", ctypes.c_int), ("unstaged_items", ctypes.c_uint32)]
+
+# hwbrj_stats_t.join_keys (include/hwbrj.h): the key format between the build / probe and the join
+JOIN_KEYS_32, JOIN_KEYS_PACKED, JOIN_KEYS_MIXED = 0, 1, 2
 
 
 _LIB = None
@@ -315,6 +319,8 @@ class Stats:
     ms_surv: float
     ms_join: float
     ms_join_probe: float
+    join_keys: int = 0       # JOIN_KEYS_32 / _PACKED / _MIXED
+    unstaged_items: int = 0  # probe items whose survivors overflowed the LDS stage
 
 
 class Relation:

@@ -7,6 +7,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -31,13 +32,25 @@ const char* hwbrj_last_error(void) { return g_last_error.c_str(); }
 #ifndef HWBRJ_SRC_SHA
 #define HWBRJ_SRC_SHA "dev"
 #endif
+// Test hooks that are set (hwbrj_set_test_hook) are named too, so a bench line or a PMC stamp of a
+// process that set one shows it.
 const char* hwbrj_version(void) {
-    static const std::string v = [] {
+    static const std::string base = [] {
         std::string k = kernel_build_knobs();
         const std::string d = dev_knobs_string();
         if (!d.empty()) k += (k.empty() ? "" : " ") + d;
-        return std::string("hwbloomradixjoin_amd 0.4 (gfx950) src " HWBRJ_SRC_SHA) + (k.empty() ? "" : " knobs: " + k);
+        return k;
     }();
+    static std::mutex  mu;
+    static std::string v;
+    std::lock_guard<std::mutex> lk(mu);
+    std::string        k = base;
+    const TestHooks&   h = test_hooks();
+    auto add = [&](const std::string& w) { k += (k.empty() ? "" : " ") + w; };
+    if (h.join_split) add("HWBRJ_HOOK_JOIN_SPLIT=" + std::to_string(h.join_split));
+    if (h.pj_fail_rank >= 0) add("HWBRJ_HOOK_PJ_FAIL_RANK=" + std::to_string(h.pj_fail_rank));
+    if (h.bcast_nonroot) add("HWBRJ_HOOK_BCAST_NONROOT=" + std::to_string(h.bcast_nonroot));
+    v = std::string("hwbloomradixjoin_amd 0.5 (gfx950) src " HWBRJ_SRC_SHA) + (k.empty() ? "" : " knobs: " + k);
     return v.c_str();
 }
 

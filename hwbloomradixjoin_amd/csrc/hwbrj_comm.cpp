@@ -223,9 +223,9 @@ int rccl_broadcast(void* comm, void* buf, size_t bytes, int root, hipStream_t st
 // collective. Returns rc (this rank's own failure), 22 if another rank failed, 30/31 on RCCL errors.
 int rccl_agree_status(void* comm, int world, int rank, int rc, hipStream_t stream, DevBuf* tmp) {
     if (int e = need_rccl()) return rc ? rc : e;
-    if (!tmp->ensure((size_t) world * 8)) {
+    if (!tmp->ensure((size_t) world * 8)) {  // (allocated by comm_init: this does not allocate)
         set_last_error("hipMalloc failed (status agreement)");
-        rc = rc ? rc : 4;  // (still take part: the peers wait for this rank's word)
+        rc = rc ? rc : 4;
     }
     std::vector<uint64_t> st(world, 0);
     st[rank] = (uint64_t) (uint32_t) rc;
@@ -264,6 +264,13 @@ int Engine::comm_init(const uint8_t* unique_id, int world, int rank) {
     comm_       = c;
     comm_world_ = world;
     comm_rank_  = rank;
+    // the status agreement's words, allocated here: an agreement never allocates, so a
+    // rank whose big allocations just failed still takes part in it
+    if (!agree_.ensure((size_t) world * 8)) {
+        (void) comm_destroy();
+        set_last_error("hipMalloc failed (status agreement words)");
+        return 4;
+    }
     return 0;
 }
 

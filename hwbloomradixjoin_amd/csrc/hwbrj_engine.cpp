@@ -592,7 +592,7 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     // the broadcast: rank 0 builds the slices, the other ranks only sub-partition R for the join
     // and receive them over RCCL (HWBRJ_HOOK_BCAST_NONROOT: this rank takes the non-root side, for
     // tests at world 1; value 2 zeroes the slices first, so the counts show whether k_build wrote any)
-    const int nonroot_hook = bcast ? test_hooks().bcast_nonroot : 0;
+    const int nonroot_hook = bcast && comm_world_ == 1 ? test_hooks().bcast_nonroot : 0;  // (tests only: world 1)
     bp.no_slices = bcast && (comm_rank_ != 0 || nonroot_hook) ? 1u : 0u;
     if (nonroot_hook == 2) HWBRJ_CHECK(hipMemsetAsync(slices.p, 0, slices.bytes, stream));
     launch_build(bp, F, stream);
@@ -696,6 +696,7 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     jp.split_surv      = test_hooks().join_split;  // (tests: force the skew split)
     jp.r_pack3         = pack3 ? 1u : 0u;
     jp.fmt_cnt         = pp.fmt_cnt;
+    jp.timing          = phase_ev_ ? 1u : 0u;  // (back-to-back joins: counts only)
     if (mat) {
         // (k_join_split, which leaves job_surv zero for the next join, does not run here)
         HWBRJ_CHECK(hipMemsetAsync(jparts.as<uint32_t>() + NJ, 0, (size_t) NJ * 4, stream));
@@ -735,6 +736,7 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     pending_ev_   = phase_ev_;
     pending_sfirst_ = s_first;
     pending_fmt_    = pp.fmt_cnt != nullptr;
+    pending_pack3_  = pack3;
     pending_stream_ = stream;
     have_filter_  = args != nullptr;
     last_g_       = g;
@@ -1004,6 +1006,7 @@ int Engine::enqueue_basic_kk(const uint2* dR, uint64_t nR, const uint2* dS, uint
     jp.nextra          = jparts.as<uint32_t>() + 2 * NJ;
     jp.jkind           = (uint32_t) jkind;
     jp.split_surv      = test_hooks().join_split;
+    jp.timing          = phase_ev_ ? 1u : 0u;
     launch_join(jp, NJ, jparts.as<uint32_t>() + NJ, stream);
     HWBRJ_CHECK(hipEventRecord(ev_[8], stream));
     HWBRJ_CHECK(hipGetLastError());
@@ -1014,6 +1017,7 @@ int Engine::enqueue_basic_kk(const uint2* dR, uint64_t nR, const uint2* dS, uint
     pending_ev_   = phase_ev_;
     pending_sfirst_ = false;
     pending_fmt_    = false;
+    pending_pack3_  = false;
     pending_stream_ = stream;
     have_filter_  = true;
     last_g_       = g;
@@ -1073,6 +1077,9 @@ int Engine::wait(hwbrj_stats_t* st) {
         st->ms_join      = ms[8];
         // the probe share of the join's workgroup time (k_join's wall_clock64 sections)
         st->ms_join_probe = small_h[4] ? ms[8] * (double) small_h[3] / (double) small_h[4] : 0.0;
+        st->unstaged_items = pending_fmt_ ? (uint32_t) small_h[5] : 0u;
+        st->join_keys      = !pending_pack3_ ? HWBRJ_JOIN_KEYS_32
+                             : st->unstaged_items ? HWBRJ_JOIN_KEYS_MIXED : HWBRJ_JOIN_KEYS_PACKED;
     }
     return 0;
 }

@@ -119,6 +119,7 @@ class Engine {
     hipStream_t  pending_stream_ = nullptr;
     bool         pending_sfirst_ = false;  // the pending join ran its S pass first (phase boundaries)
     bool         pending_fmt_    = false;  // the pending join counted its unstaged probe items
+    bool         pending_pack3_  = false;  // the pending join packed its join keys
     bool         pack3_hint_     = true;   // the last waited join had none: 3-byte join keys pay
     int          pending_rc_     = 0;   // nonzero: the pending join failed after enqueuing kernels
     std::string  pending_err_;

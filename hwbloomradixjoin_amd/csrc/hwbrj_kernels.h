@@ -106,7 +106,8 @@ struct JoinParams {
     uint32_t        slot;         // r_codes words per build sweep
     uint32_t        bitmap;       // 1: keys fit the direct-address bitmap (32 - hash_shift <= 18)
     uint64_t*       result;
-    uint64_t*       jsum;         // kJoinSumSlots partial sums, one per 128-byte line (zeroed by k_join_split)
+    uint64_t*       jsum;         // kJoinSumSlots partial sums, one per 128-byte line (word 3: the
+                                  // slot's workgroup ticket), zeroed by k_join_split
     uint32_t        jobs;         // F * NSUB (set by launch_join)
     uint32_t*       nparts;       // [jobs] parts of each job (k_join_split)
     uint2*          extra;        // [join_extra_tasks()] {job, part} of the further parts
@@ -120,6 +121,8 @@ struct JoinParams {
     uint32_t        r_pack3;      // 1: r_codes hold 3-byte join keys (BuildParams::pack3); survivor
                                   // runs say so per item (bit 31 of surv_off)
     const uint32_t* fmt_cnt;      // ProbeParams::fmt_cnt (the launch's survivor-run formats), or nullptr
+    uint32_t        timing;       // 1: accumulate the probe / total ticks (result[3], result[4]) for
+                                  // ms_join_probe (synchronous joins; 0: one count add per workgroup)
 };
 
 // The materializing join (k_join_mat): R codes + payloads of the build sweeps, survivors + their
@@ -217,7 +220,7 @@ void   launch_pj_gather(const uint32_t* pool, const uint32_t* list, uint32_t n, 
                         hipStream_t st);
 // the native transport's per-destination counts message (k_pj_counts), built on the device
 void   launch_pj_counts(const uint32_t* starts, const uint64_t* bound, uint32_t W, uint32_t QL, uint32_t NC,
-                        uint64_t status, uint64_t extra, uint64_t* out, hipStream_t st);
+                        uint64_t status, uint64_t extra, uint64_t extra2, uint64_t* out, hipStream_t st);
 void   launch_pj_relist(const uint32_t* rent, const int64_t* tab, uint32_t pairs, uint32_t* list,
                         hipStream_t st);
 void   launch_pj_surv_pack(const uint32_t* surv, const uint64_t* region, const uint32_t* tot,

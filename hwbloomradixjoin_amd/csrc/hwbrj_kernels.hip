@@ -2386,8 +2386,8 @@ constexpr uint32_t kJoinTaskSurv = 1u << 17;
 constexpr uint32_t kJoinExtra    = 2048;
 
 // Match counts: every join workgroup adds its count to one of kJoinSumSlots partial sums (each in
-// its own 128-byte line, so the ~16K adds are not serialised on one address); k_join_sum adds them
-// into the result.
+// its own 128-byte line, so the adds are not serialised on one address); the last workgroup of the
+// launch adds them into the result.
 constexpr uint32_t kJoinSumSlots = 64;
 constexpr uint32_t kJoinSumStride = 16;  // u64 words per slot (128 bytes)
 
@@ -2397,8 +2397,8 @@ __global__ __launch_bounds__(256) void k_join_split(const uint32_t* __restrict__
                                                      uint32_t* __restrict__ nparts,
                                                      uint2* __restrict__ extra, uint32_t* nextra,
                                                      uint64_t* __restrict__ jsum) {
-    if (blockIdx.x == 0 && threadIdx.x < kJoinSumSlots)
-        for (int w = 0; w < 3; w++) jsum[threadIdx.x * kJoinSumStride + w] = 0;
+    if (blockIdx.x == 0 && threadIdx.x < kJoinSumSlots)  // (word 3: k_join's ticket of the slot)
+        for (int w = 0; w < 4; w++) jsum[threadIdx.x * kJoinSumStride + w] = 0;
     const uint32_t job = blockIdx.x * blockDim.x + threadIdx.x;  // one thread per job
     if (job >= NJ) return;
     const uint32_t q = job >> log2NSUB, items = item_start[q + 1] - item_start[q];
@@ -2416,54 +2416,128 @@ __global__ __launch_bounds__(256) void k_join_split(const uint32_t* __restrict__
     nparts[job] = np;
 }
 
-// One (job, part) of the join on workgroup slot blk; MIXED: survivor runs of both formats (below).
-template <bool MIXED>
-__device__ __forceinline__ void join_job(const JoinParams& P, const uint32_t blk) {
-    __shared__ __attribute__((aligned(16))) uint32_t tab[kJoinWords];  // bitmap or hash table
-    __shared__ uint64_t dbase[kJoinDesc];  // run starts (byte offsets) of a batch: S survivor runs
-    __shared__ uint32_t dcnt[kJoinDesc];
-    __shared__ uint64_t rbase[kJoinDesc];  // R runs (one per build sweep of q)
-    __shared__ uint32_t rcnt[kJoinDesc];
-    __shared__ uint32_t pend[kJoinDesc + 1];  // hash path: piece boundaries inside an R batch
-    __shared__ uint64_t wsum[kJoinWaves];
-    __shared__ uint32_t dupflag, npieces;
-    const uint32_t NSUB = 1u << P.log2NSUB;
-    uint32_t       job = blk, part = 0;  // workgroup j < jobs: part 0 of job j
+// One workgroup per work item: items [0, jobs) are part 0 of job map(item), the rest the further
+// parts of skewed jobs (k_join_split's table). A job is a chain of memory latencies (its descriptors,
+// its R and survivor runs). On the fused path every lane loads the descriptors of its wave's runs
+// (read back uniformly with readlane, no LDS staging), the R runs and the first survivor runs are
+// in flight together, and the further survivor runs are issued as soon as the R keys are in the
+// bitmap, so they arrive while the workgroup counts the bitmap and tests the first ones. Only
+// validity bits stay live past a load. Counts go to kJoinSumSlots partial sums; the last workgroup
+// of each slot's group adds its sum into the result (no separate sum launch).
 #ifndef HWBRJ_JXCD
 #define HWBRJ_JXCD 1
 #endif
+#ifndef HWBRJ_JFR
+#define HWBRJ_JFR 8  // fused path: R runs per wave
+#define HWBRJ_JFW 5  // fused path: R words per lane per run (runs average slot / NSUB words)
+#endif
+#ifndef HWBRJ_JRR
+#define HWBRJ_JRR 4
+#define HWBRJ_JRW 4
+#define HWBRJ_JSR 8
+#define HWBRJ_JSW 2
+#endif
+#ifndef HWBRJ_JFS
+#define HWBRJ_JFS HWBRJ_JSR  // fused path: survivor runs per wave loaded with the R runs
+#endif
+#ifndef HWBRJ_JFS2
+#define HWBRJ_JFS2 16  // fused path: survivor runs per wave issued once the R keys are set
+#endif
+
+// Uniform facts of one work item (scalar registers).
+struct JobInfo {
+    uint32_t job, s, w0, w1, qi0, qi1, i0, i1, lq0, npc;
+};
+
+// This lane's run descriptors of a job, for the fused path: lane l of wave v holds R run and
+// survivor run d = v + kJoinWaves * l (the wave's run l), read back uniformly with readlane.
+struct JobDesc {
+    uint32_t rc, ro;  // R run: keys, offset in its sweep slot
+    uint32_t sc, so;  // survivor run: keys, surv_off entry (bit 31: 3-byte keys)
+    uint64_t se;      // survivor run: element base of its item region
+};
+
+// LDS of a join workgroup (one instance per kernel, shared by both format instantiations)
+struct JoinLds {
+    uint32_t tab[kJoinWords] __attribute__((aligned(16)));  // bitmap or hash table
+    uint64_t dbase[kJoinDesc];  // general path: survivor run starts (tagged byte offsets) of a batch
+    uint32_t dcnt[kJoinDesc];
+    uint64_t rbase[kJoinDesc];  // R runs (one per build sweep of q)
+    uint32_t rcnt[kJoinDesc];
+    uint32_t pend[kJoinDesc + 1];  // hash path: piece boundaries inside an R batch
+    uint32_t dupflag, npieces, rkw[kJoinWaves];
+    uint64_t wsum[kJoinWaves];
+};
+
+template <bool MIXED>
+__device__ __forceinline__ void join_one(const JoinParams& P, JoinLds& L, uint64_t& cnt, uint64_t& t_probe) {
+    uint32_t* const tab = L.tab;
+    uint64_t* const dbase = L.dbase;
+    uint32_t* const dcnt = L.dcnt;
+    uint64_t* const rbase = L.rbase;
+    uint32_t* const rcnt = L.rcnt;
+    uint32_t* const pend = L.pend;
+    uint32_t& dupflag = L.dupflag;
+    uint32_t& npieces = L.npieces;
+    uint32_t* const rkw = L.rkw;
+    const uint32_t NSUB = 1u << P.log2NSUB;
+    const uint32_t blk  = blockIdx.x;
+    const uint32_t W    = P.jobs + min(*P.nextra, kJoinExtra);  // work items of this launch
+    const int      tid = threadIdx.x, lane = tid & 63;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane((uint32_t) tid >> 6);
+    const bool     rpk  = P.r_pack3 != 0;
+    const uint32_t sh   = P.hash_shift;
     // XCD-aware job order: blocks b, b + 8, ... share an XCD (dealt round-robin), so they take
     // consecutive jobs -- the 16 subs of a partition run on one XCD, where the lines their runs
     // share (adjacent sub runs in every sweep slot and item region) are fetched into its L2 once
-    if (HWBRJ_JXCD && blk < P.jobs && (P.jobs & 7u) == 0) job = (blk & 7u) * (P.jobs >> 3) + (blk >> 3);
-    if (blk >= P.jobs) {                 // extra workgroups: further parts of skewed jobs
-        const uint32_t e = blk - P.jobs;
-        if (e >= min(*P.nextra, kJoinExtra)) return;
-        const uint2 x = P.extra[e];
-        job           = x.x;
-        part          = x.y;
-    }
-    const uint32_t q = job >> P.log2NSUB, s = job & (NSUB - 1u);
-    const uint32_t w0 = P.r_sweep_start[q], w1 = P.r_sweep_start[q + 1];
-    const uint32_t qi0 = P.item_start[q], qi1 = P.item_start[q + 1];  // q's items (segment-major)
-    const uint32_t np  = P.nparts[job];
-    const bool     rpk = P.r_pack3 != 0;
-    const uint32_t i0  = qi0 + (uint32_t) ((uint64_t) (qi1 - qi0) * part / np);
-    const uint32_t i1  = qi0 + (uint32_t) ((uint64_t) (qi1 - qi0) * (part + 1) / np);
-    if (w1 == w0 || i1 == i0) return;
-    const uint32_t lq0 = P.item_base ? 0u : P.list_start[q];
-    const uint32_t npc = (qi1 - qi0) / P.nseg;  // probe pieces of q
-    const uint32_t sh  = P.hash_shift;
-    const int      tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    uint64_t       cnt = 0;
-    // probe share of the join (the reference's per-thread probe timers, :289-321): thread 0 sums
-    // the 100 MHz ticks of the survivor-probing sections of this workgroup
-    const uint64_t t_start = wall_clock64();
-    uint64_t       t_probe = 0, t_mark = 0;
-    auto probe_begin = [&]() { t_mark = wall_clock64(); };
-    auto probe_end   = [&]() { t_probe += wall_clock64() - t_mark; };
+    const bool xcd = HWBRJ_JXCD && (P.jobs & 7u) == 0;
+    auto info = [&](uint32_t w) -> JobInfo {
+        JobInfo J;
+        uint32_t part = 0;
+        if (w < P.jobs) {
+            J.job = xcd ? (w & 7u) * (P.jobs >> 3) + (w >> 3) : w;
+        } else {  // a further part of a skewed job
+            const uint2 x = P.extra[w - P.jobs];
+            J.job         = x.x;
+            part          = x.y;
+        }
+        const uint32_t q = J.job >> P.log2NSUB, np = P.nparts[J.job];
+        J.s   = J.job & (NSUB - 1u);
+        J.w0  = P.r_sweep_start[q];
+        J.w1  = P.r_sweep_start[q + 1];
+        J.qi0 = P.item_start[q];  // q's items (segment-major)
+        J.qi1 = P.item_start[q + 1];
+        J.i0  = J.qi0 + (uint32_t) ((uint64_t) (J.qi1 - J.qi0) * part / np);
+        J.i1  = J.qi0 + (uint32_t) ((uint64_t) (J.qi1 - J.qi0) * (part + 1) / np);
+        J.lq0 = P.item_base ? 0u : P.list_start[q];
+        J.npc = (J.qi1 - J.qi0) / P.nseg;  // probe pieces of q
+        return J;
+    };
+    // element base of item it's survivor region
+    auto item_e0 = [&](const JobInfo& J, uint32_t it) -> uint64_t {
+        if (P.item_base) return P.item_base[it];  // (the partitioned multi-GPU join)
+        const uint32_t local = it - J.qi0, seg = local / J.npc, piece = local - seg * J.npc;
+        return (uint64_t) seg * P.surv_seg_stride + (uint64_t) (J.lq0 + piece * P.CH) * 32;
+    };
+    constexpr int FR = HWBRJ_JFR, FW = HWBRJ_JFW;
+    auto descs = [&](const JobInfo& J) -> JobDesc {
+        JobDesc        X{0, 0, 0, 0, 0};
+        const uint32_t d = wave + kJoinWaves * (uint32_t) lane;
+        if (lane < FR && d < J.w1 - J.w0) {
+            const uint64_t r = (uint64_t) (J.w0 + d) * NSUB + J.s;
+            X.rc             = P.r_cnt[r];
+            X.ro             = P.r_off[r];
+        }
+        if (d < J.i1 - J.i0) {
+            const uint32_t it = J.i0 + d;
+            X.sc              = P.surv_cnt[(uint64_t) it * NSUB + J.s];
+            X.so              = P.surv_off[(uint64_t) it * NSUB + J.s];
+            X.se              = item_e0(J, it);
+        }
+        return X;
+    };
     // dev-only phase stamps of wave 0 (build with -DHWBRJ_STAMPS, run with HWBRJ_DBG): fused path
-    // 0 descriptors, 1 R loads + bit sets, 2 popcount, 3 first survivor runs, 4 further runs, 5 sum
+    // 0 descriptors + zeroing, 1 R loads + bit sets, 2 popcount, 3 first survivor runs, 4 further runs
     uint64_t tph[6] = {0, 0, 0, 0, 0, 0}, tlast = __builtin_amdgcn_s_memtime();
     (void) tlast;
     (void) tph;
@@ -2478,15 +2552,23 @@ __device__ __forceinline__ void join_job(const JoinParams& P, const uint32_t blk
         (void) k;
 #endif
     };
+    // probe share of the join (the reference's per-thread probe timers, :289-321), synchronous joins
+    // only (P.timing): the 100 MHz ticks of the survivor-probing sections of this workgroup
+    uint64_t t_mark = 0;
+    auto probe_begin = [&]() {
+        if (P.timing) t_mark = wall_clock64();
+    };
+    auto probe_end = [&]() {
+        if (P.timing) t_probe += wall_clock64() - t_mark;
+    };
     // Run formats. A run is addressed by a tagged byte offset tb from its array's base: bit 63 set =
     // 3-byte keys (pack3), key o the low 24 bits of the unaligned dword at tb + 3 o; else 32-bit
     // codes at tb + 4 o, key = code >> sh. R runs share one format (the build's); survivor runs are
     // packed when their probe item was staged (bit 31 of surv_off). P.fmt_cnt counts the unstaged
     // items: with none (or no pack3 at all) every run of the launch has one format, whose stride,
-    // shift and mask are uniform (k_join); otherwise the survivor runs are mixed and read with a
-    // per-run format (k_join_mixed: only where probe items overflow their stage), R runs packed.
-    // Loads stay raw until used (key()): ALU work on a conditionally loaded value would make the
-    // wave wait for it at once.
+    // shift and mask are uniform; otherwise (MIXED: only where probe items overflow their stage)
+    // the survivor runs are read with a per-run format, R runs packed. Loads stay raw until used
+    // (key()): ALU work on a conditionally loaded value would make the wave wait for it at once.
     constexpr uint64_t kPk = 1ull << 63;
     const uint32_t kst = rpk ? 3u : 4u, ksh = rpk ? 0u : sh, kmk = rpk ? 0xFFFFFFu : 0xFFFFFFFFu;
     const uint8_t* const r8 = (const uint8_t*) P.r_codes;
@@ -2529,8 +2611,8 @@ __device__ __forceinline__ void join_job(const JoinParams& P, const uint32_t blk
                 if (o + 64u * u < n) op(key(side_c, v[u], (bb & kPk) != 0));
         }
     };
-    // Every word of runs [da, db) of a descriptor batch through op(word): a wave per run, RUNS runs
-    // in flight per wave with WPL words per lane each; longer runs finish in a tail loop.
+    // Every word of runs [da, db) of a descriptor batch in LDS through op(word): a wave per run,
+    // RUNS runs in flight per wave with WPL words per lane each; longer runs finish in a tail loop.
     auto walk = [&](auto runs_c, auto wpl_c, auto side_c, const uint32_t* nc,
                     const uint64_t* nb, uint32_t da, uint32_t db, auto&& op) {
         constexpr int RUNS = decltype(runs_c)::value, WPL = decltype(wpl_c)::value;
@@ -2560,313 +2642,327 @@ __device__ __forceinline__ void join_job(const JoinParams& P, const uint32_t blk
             }
         }
     };
-#ifndef HWBRJ_JRR
-#define HWBRJ_JRR 4
-#define HWBRJ_JRW 4
-#define HWBRJ_JSR 8
-#define HWBRJ_JSW 2
-#endif
     using RR = std::integral_constant<int, HWBRJ_JRR>;  // R runs in flight per wave
     using RW = std::integral_constant<int, HWBRJ_JRW>;  // R words per lane per run
     using SR = std::integral_constant<int, HWBRJ_JSR>;  // survivor runs in flight per wave
     using SW = std::integral_constant<int, HWBRJ_JSW>;
-    // the survivors of (q, s), batch by batch, against the table: bitmap (BM) or hash table
-    auto probe_survivors = [&](auto&& op) {
-        probe_begin();
-        for (uint32_t d0 = i0; d0 < i1; d0 += kJoinDesc) {
-            const uint32_t nd = min(kJoinDesc, i1 - d0);
-            __syncthreads();  // previous descriptors consumed
-            if ((uint32_t) tid < nd) {
-                const uint32_t it    = d0 + tid;
-                const uint32_t local = it - qi0;
-                const uint32_t seg   = local / npc;
-                const uint32_t piece = local - seg * npc;
-                dcnt[tid]  = P.surv_cnt[(uint64_t) it * NSUB + s];
-                dbase[tid] = stag(P.item_base ? P.item_base[it]  // (the partitioned multi-GPU join)
-                                              : (uint64_t) seg * P.surv_seg_stride + (uint64_t) (lq0 + piece * P.CH) * 32,
-                                  P.surv_off[(uint64_t) it * NSUB + s]);
-            }
-            __syncthreads();
-            walk(SR{}, SW{}, SideS{}, dcnt, dbase, 0, nd, op);
-        }
-        probe_end();
+    constexpr int FS = HWBRJ_JFS, FS2 = HWBRJ_JFS2, FSW = HWBRJ_JSW;
+    auto rl64 = [](uint64_t x, uint32_t l) -> uint64_t {
+        return (uint64_t) __builtin_amdgcn_readlane((uint32_t) x, l) |
+               (uint64_t) __builtin_amdgcn_readlane((uint32_t) (x >> 32), l) << 32;
     };
-    // R run descriptors of a batch
-    auto load_r = [&](uint32_t d0, uint32_t nd) {
-        __syncthreads();  // previous R descriptors consumed
-        uint32_t c = 0;
-        if ((uint32_t) tid < nd) {
-            const uint64_t r = (uint64_t) (d0 + tid) * NSUB + s;
-            c                = P.r_cnt[r];
-            rcnt[tid]        = c;
-            rbase[tid]       = rtag(d0 + tid, P.r_off[r]);
-        }
-        (void) c;
-        __syncthreads();
+    // survivor run r of this wave (run d = wave + kJoinWaves r of the job), from the lanes' descriptors
+    auto srun = [&](const JobDesc& X, uint32_t r, uint32_t nSd, uint32_t& n) -> uint64_t {
+        r &= 63u;  // (lanes past the wave's runs are never used: n = 0)
+        n = wave + kJoinWaves * r < nSd ? __builtin_amdgcn_readlane(X.sc, r) : 0u;
+        return stag(rl64(X.se, r), __builtin_amdgcn_readlane(X.so, r));
     };
-    // PRH / PRHO (P.jkind 1 / 2): the histogram join of every job, below
-    bool hashed = !P.bitmap || P.jkind != 0;
-    bool done   = false;
-#ifndef HWBRJ_JFR
-#define HWBRJ_JFR 8  // fused path: R runs per wave
-#define HWBRJ_JFW 5  // fused path: R words per lane per run (runs average slot / NSUB words)
-#endif
-    constexpr int FR = HWBRJ_JFR, FW = HWBRJ_JFW;
-    const uint32_t nRd = w1 - w0, nSd = i1 - i0;
-    if (!hashed && nRd <= (uint32_t) (kJoinWaves * FR) && nSd <= kJoinDesc) {
-        // Fused bitmap path (every job of the north star): both descriptor sets in one phase, then
-        // the loads of all R runs and of the first survivor runs are issued before any is used, so
-        // a job costs two memory latencies (descriptors, data) instead of one per batch.
-        for (uint32_t i = tid; i < kJoinWords / 4; i += kJoinThreads) ((uint4*) tab)[i] = make_uint4(0, 0, 0, 0);
-        if (tid == 0) dupflag = 0;
-        uint32_t rc = 0;
-        if ((uint32_t) tid < nRd) {
-            const uint64_t r = (uint64_t) (w0 + tid) * NSUB + s;
-            rcnt[tid]        = P.r_cnt[r];
-            rbase[tid]       = rtag(w0 + tid, P.r_off[r]);
-            rc = rcnt[tid];
-        }
-        stamp(0);
-        if (wave == 0) {  // the job's R keys (nRd <= 64: every R descriptor is in wave 0)
-            const uint32_t t = __builtin_amdgcn_readlane(wave_incl_scan_dpp(rc), 63);
-            if (lane == 0) npieces = t;
-        }
-        if ((uint32_t) tid < nSd) {
-            const uint32_t it    = i0 + tid;
-            const uint32_t local = it - qi0;
-            const uint32_t seg   = local / npc;
-            const uint32_t piece = local - seg * npc;
-            dcnt[tid]  = P.surv_cnt[(uint64_t) it * NSUB + s];
-            dbase[tid] = stag(P.item_base ? P.item_base[it]  // (the partitioned multi-GPU join)
-                                          : (uint64_t) seg * P.surv_seg_stride + (uint64_t) (lq0 + piece * P.CH) * 32,
-                              P.surv_off[(uint64_t) it * NSUB + s]);
-        }
-        __syncthreads();
-#ifndef HWBRJ_JFS
-#define HWBRJ_JFS HWBRJ_JSR
-#endif
-        constexpr int FS = HWBRJ_JFS, FSW = HWBRJ_JSW;  // survivor runs per wave loaded with R's
-        uint32_t rv[FR][FW], rn[FR], sv[FS][FSW], sn[FS], spk = 0;  // spk bit r: survivor run r packed
+    // Survivor runs [r0, r0 + N) of this wave into registers (N runs in flight, FSW words per lane).
+    // Past the loads only bits stay live: vm bit r FSW + j = slot j of run r holds a key, tl bit r =
+    // run r is longer than its registers, pk bit r = run r holds 3-byte keys (MIXED)
+    auto sload = [&](auto n_c, const JobDesc& X, uint32_t r0, uint32_t nSd, uint32_t (&v)[decltype(n_c)::value][FSW],
+                     uint32_t& vm, uint32_t& tl, uint32_t& pk) {
+        constexpr int N = decltype(n_c)::value;
+        static_assert(N * FSW <= 32, "validity bits");
+        vm = tl = pk = 0;
 #pragma unroll
-        for (int r = 0; r < FR; r++) {
-            const uint32_t dd = wave + r * kJoinWaves;
-            rn[r]             = dd < nRd ? rcnt[dd] : 0u;
-#ifdef HWBRJ_ABL_JNOR
-            rn[r] = 0;  // dev ablation (results invalid)
-#endif
-            const uint64_t bb = dd < nRd ? rbase[dd] : 0ull;
-#pragma unroll
-            for (int j = 0; j < FW; j++) {
-                const uint32_t o = lane + 64u * j;
-                rv[r][j]         = o < rn[r] ? ldv(SideR{}, bb, o) : 0u;
-            }
-        }
-#pragma unroll
-        for (int r = 0; r < FS; r++) {
-            const uint32_t dd = wave + r * kJoinWaves;
-            sn[r]             = dd < nSd ? dcnt[dd] : 0u;
+        for (int r = 0; r < N; r++) {
+            uint32_t       n;
+            const uint64_t bb = srun(X, r0 + r, nSd, n);
 #ifdef HWBRJ_ABL_JNOS
-            sn[r] = 0;  // dev ablation (results invalid)
+            n = 0;  // dev ablation (results invalid)
 #endif
-            const uint64_t bb = dd < nSd ? dbase[dd] : 0ull;
-            spk |= (uint32_t) (bb >> 63) << r;
+            tl |= (uint32_t) (n > 64u * FSW) << r;
+            pk |= (uint32_t) (bb >> 63) << r;
 #pragma unroll
             for (int j = 0; j < FSW; j++) {
-                const uint32_t o = lane + 64u * j;
-                sv[r][j]         = o < sn[r] ? ldv(SideS{}, bb, o) : 0u;
+                const uint32_t o  = lane + 64u * j;
+                const bool     ok = o < n;
+                vm |= (uint32_t) ok << (r * FSW + j);
+                v[r][j] = ok ? ldv(SideS{}, bb, o) : 0u;
             }
         }
-        // bits set without returns (no wave waits on them); a duplicate R key shows as fewer set
-        // bits than the job's R keys (popcount after the barrier)
-        auto set = [&](uint32_t x) { __hip_atomic_fetch_or(&tab[x >> 5], 1u << (x & 31u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); };
+    };
+    auto stest = [&](auto n_c, const JobDesc& X, uint32_t r0, uint32_t nSd, const uint32_t (&v)[decltype(n_c)::value][FSW],
+                     uint32_t vm, uint32_t tl, uint32_t pk, auto&& test) {
+        constexpr int N = decltype(n_c)::value;
 #pragma unroll
-        for (int r = 0; r < FR; r++) {
+        for (int r = 0; r < N; r++)
 #pragma unroll
-            for (int j = 0; j < FW; j++)
-                if (lane + 64u * j < rn[r]) set(key(SideR{}, rv[r][j], rpk));
-            if (rn[r] > 64u * FW) {  // (rare) longer run
-                const uint64_t bb = rbase[wave + r * kJoinWaves];
-                tail_run(SideR{}, bb, 64u * FW, rn[r], set);
-            }
+            for (int j = 0; j < FSW; j++)
+                if ((vm >> (r * FSW + j)) & 1u) test(key(SideS{}, v[r][j], (pk >> r) & 1u));
+        while (tl) {  // (rare) runs longer than their registers
+            const uint32_t r = __builtin_ctz(tl);
+            tl &= tl - 1u;
+            uint32_t       n;
+            const uint64_t bb = srun(X, r0 + r, nSd, n);
+            tail_run(SideS{}, bb, 64u * FSW, n, test);
         }
-        __syncthreads();
-        stamp(1);
-        {
-            uint32_t pc = 0;
-            for (uint32_t i = tid; i < kJoinWords / 4; i += kJoinThreads) {
-                const uint4 v = ((const uint4*) tab)[i];
-                pc += __builtin_popcount(v.x) + __builtin_popcount(v.y) + __builtin_popcount(v.z) + __builtin_popcount(v.w);
-            }
-            pc = __builtin_amdgcn_readlane(wave_incl_scan_dpp(pc), 63);
-            if (lane == 0 && pc) atomicAdd(&dupflag, pc);  // (dupflag: the set bits)
-        }
-        __syncthreads();
-        hashed = dupflag != npieces;  // uniform
-        stamp(2);
-        if (!hashed) {
-            probe_begin();
-            auto test = [&](uint32_t x) { cnt += (tab[x >> 5] >> (x & 31u)) & 1u; };
+    };
+
+    if (blk >= W) return;
+    const JobInfo J = info(blk);
+    if (J.w1 == J.w0 || J.i1 == J.i0) return;
+    const uint32_t nRd = J.w1 - J.w0, nSd = J.i1 - J.i0;
+    {
+        const uint32_t s = J.s, i0 = J.i0, i1 = J.i1, w0 = J.w0, w1 = J.w1;
+        // PRH / PRHO (P.jkind 1 / 2): the histogram join of every job, below
+        bool hashed = !P.bitmap || P.jkind != 0;
+        bool done   = false;
+        if (!hashed && nRd <= (uint32_t) (kJoinWaves * FR) && nSd <= (uint32_t) (kJoinWaves * 64)) {
+            // Fused bitmap path (every job of the north star): the descriptors, then the R runs and
+            // the first survivor runs loaded before any is used; the bitmap is zeroed while they are
+            // in flight.
+            const JobDesc X = descs(J);
+            static_assert(FR * FW <= 64, "R validity bits");
+            uint32_t rv[FR][FW], rtl = 0, rk = 0;  // rtl bit r: R run r is longer than its registers
+            uint64_t rvm = 0;                      // bit r FW + j: R slot j of run r holds a key
 #pragma unroll
-            for (int r = 0; r < FS; r++) {
-#pragma unroll
-                for (int j = 0; j < FSW; j++)
-                    if (lane + 64u * j < sn[r]) test(key(SideS{}, sv[r][j], (spk >> r) & 1u));
-                if (sn[r] > 64u * FSW) {
-                    const uint64_t bb = dbase[wave + r * kJoinWaves];
-                    tail_run(SideS{}, bb, 64u * FSW, sn[r], test);
-                }
-            }
-            stamp(3);
-#ifndef HWBRJ_ABL_JNOS
-            walk(SR{}, SW{}, SideS{}, dcnt, dbase, (uint32_t) (kJoinWaves * FS), nSd, test);
+            for (int r = 0; r < FR; r++) {
+                uint32_t n = wave + kJoinWaves * r < nRd ? __builtin_amdgcn_readlane(X.rc, r) : 0u;
+#ifdef HWBRJ_ABL_JNOR
+                n = 0;  // dev ablation (results invalid)
 #endif
-            stamp(4);
-            probe_end();
-            done = true;
-        }
-    }
-    if (!hashed && !done) {  // every R key sets bit v; a bit already set means a duplicate key
-        for (uint32_t i = tid; i < kJoinWords / 4; i += kJoinThreads) ((uint4*) tab)[i] = make_uint4(0, 0, 0, 0);
-        if (tid == 0) dupflag = 0;
-        uint32_t dup = 0;
-        for (uint32_t d0 = w0; d0 < w1; d0 += kJoinDesc) {
-            const uint32_t nd = min(kJoinDesc, w1 - d0);
-            load_r(d0, nd);
-            walk(RR{}, RW{}, SideR{}, rcnt, rbase, 0, nd, [&](uint32_t x) {
-                const uint32_t bit = 1u << (x & 31u);
-                dup |= atomicOr(&tab[x >> 5], bit) & bit;
-            });
-        }
-        if (dup) dupflag = 1;
-        __syncthreads();
-        hashed = dupflag != 0;  // uniform
-        if (!hashed) probe_survivors([&](uint32_t x) { cnt += (tab[x >> 5] >> (x & 31u)) & 1u; });
-    }
-    if (hashed) {  // duplicate R keys (or keys too wide for the bitmap): counting hash table over
-                   // pieces of consecutive R runs holding <= kJoinPiece keys (a run has <= slot)
-        for (uint32_t d0 = w0; d0 < w1; d0 += kJoinDesc) {
-            const uint32_t nd = min(kJoinDesc, w1 - d0);
-            load_r(d0, nd);
-            if (tid == 0) {
-                uint32_t np = 0, acc = 0;
-                pend[0] = 0;
-                for (uint32_t d = 0; d < nd; d++) {
-                    if (acc + rcnt[d] > kJoinPiece && acc > 0) {
-                        pend[++np] = d;
-                        acc        = 0;
-                    }
-                    acc += rcnt[d];
+                rk += n;
+                rtl |= (uint32_t) (n > 64u * FW) << r;
+                const uint64_t bb = rtag(w0 + wave + kJoinWaves * r, __builtin_amdgcn_readlane(X.ro, r));
+#pragma unroll
+                for (int j = 0; j < FW; j++) {
+                    const uint32_t o  = lane + 64u * j;
+                    const bool     ok = o < n;
+                    rvm |= (uint64_t) ok << (r * FW + j);
+                    rv[r][j] = ok ? ldv(SideR{}, bb, o) : 0u;
                 }
-                pend[++np] = nd;
-                npieces    = np;
+            }
+            uint32_t sv[FS][FSW], svm, stl, spk;
+            sload(std::integral_constant<int, FS>{}, X, 0, nSd, sv, svm, stl, spk);
+            for (uint32_t i = tid; i < kJoinWords / 4; i += kJoinThreads) ((uint4*) tab)[i] = make_uint4(0, 0, 0, 0);
+            if (tid == 0) dupflag = 0;
+            if (lane == 0) rkw[wave] = rk;
+            stamp(0);
+            __syncthreads();
+            // bits set without returns (no wave waits on them); a duplicate R key shows as fewer set
+            // bits than the job's R keys (popcount after the barrier)
+            auto set = [&](uint32_t x) { __hip_atomic_fetch_or(&tab[x >> 5], 1u << (x & 31u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); };
+#pragma unroll
+            for (int r = 0; r < FR; r++)
+#pragma unroll
+                for (int j = 0; j < FW; j++)
+                    if ((rvm >> (r * FW + j)) & 1u) set(key(SideR{}, rv[r][j], rpk));
+            while (rtl) {  // (rare) R runs longer than their registers
+                const uint32_t r = __builtin_ctz(rtl);
+                rtl &= rtl - 1u;
+                const uint32_t n = __builtin_amdgcn_readlane(X.rc, r);
+                tail_run(SideR{}, rtag(w0 + wave + kJoinWaves * r, __builtin_amdgcn_readlane(X.ro, r)), 64u * FW, n, set);
+            }
+            // the further survivor runs, into the registers the R runs leave
+            uint32_t sv2[FS2][FSW], svm2, stl2, spk2;
+            sload(std::integral_constant<int, FS2>{}, X, FS, nSd, sv2, svm2, stl2, spk2);
+            __syncthreads();
+            stamp(1);
+            {
+                uint32_t pc = 0;
+                for (uint32_t i = tid; i < kJoinWords / 4; i += kJoinThreads) {
+                    const uint4 v = ((const uint4*) tab)[i];
+                    pc += __builtin_popcount(v.x) + __builtin_popcount(v.y) + __builtin_popcount(v.z) + __builtin_popcount(v.w);
+                }
+                pc = __builtin_amdgcn_readlane(wave_incl_scan_dpp(pc), 63);
+                if (lane == 0 && pc) atomicAdd(&dupflag, pc);  // (dupflag: the set bits)
             }
             __syncthreads();
-            const uint32_t np = npieces;
-            for (uint32_t pc = 0; pc < np; pc++) {
-                const uint32_t da = pend[pc], db = pend[pc + 1];
-                __syncthreads();
-                if (P.jkind == 0) {  // counting hash table (bucket_chaining_join's role)
-                    for (uint32_t i = tid; i < kJoinT / 4; i += kJoinThreads)
-                        ((uint4*) tab)[i] = make_uint4(kEmpty, kEmpty, kEmpty, kEmpty);
-                    __syncthreads();
-                    walk(RR{}, RW{}, SideR{}, rcnt, rbase, da, db, [&](uint32_t x) { join_insert(tab, x); });
-                    probe_survivors([&](uint32_t x) { cnt += join_count(tab, x); });  // (starts with a barrier)
-                    continue;
+            uint32_t rkt = 0;
+#pragma unroll
+            for (int v = 0; v < kJoinWaves; v++) rkt += rkw[v];
+            hashed = dupflag != rkt;  // uniform
+            stamp(2);
+            if (!hashed) {
+                probe_begin();
+                auto test = [&](uint32_t x) { cnt += (tab[x >> 5] >> (x & 31u)) & 1u; };
+                stest(std::integral_constant<int, FS>{}, X, 0, nSd, sv, svm, stl, spk, test);
+                stest(std::integral_constant<int, FS2>{}, X, FS, nSd, sv2, svm2, stl2, spk2, test);
+                stamp(3);
+                // runs beyond the first FS + FS2 of this wave (more than 4 (FS + FS2) probe items)
+                for (uint32_t r0 = FS + FS2; wave + kJoinWaves * r0 < nSd; r0 += SR::value) {
+                    uint32_t v3[SR::value][FSW], vm3, tl3, pk3;
+                    sload(SR{}, X, r0, nSd, v3, vm3, tl3, pk3);
+                    stest(SR{}, X, r0, nSd, v3, vm3, tl3, pk3, test);
                 }
-                // Histogram join of Kim et al. (histogram_join / histogram_optimized_join,
-                // src/parallel_radix_join_bloom.c:350-419, :441-555): a histogram of the piece's R
-                // keys over NH = max(4, next_pow2(n) / 4) buckets, its prefix sum, the keys
-                // reordered by bucket (keys = tab[0, kJoinPiece), hist = tab[kJoinPiece, +NH + 2));
-                // every survivor compares the keys of its bucket -- one by one (PRH), or 4 per
-                // 16-byte LDS read (PRHO, the reference's SIMD compare).
-                uint32_t n = 0;
-                for (uint32_t d = da; d < db; d++) n += rcnt[d];
-                uint32_t NH = 4;
-                while (NH * 4 < n) NH <<= 1;
-                uint32_t* keys = tab;
-                uint32_t* hist = tab + kJoinPiece;
-                for (uint32_t i = tid; i < NH + 2; i += kJoinThreads) hist[i] = 0;
-                __syncthreads();
-                walk(RR{}, RW{}, SideR{}, rcnt, rbase, da, db, [&](uint32_t x) { atomicAdd(&hist[(x & (NH - 1u)) + 2], 1u); });
-                __syncthreads();
-                if (wave == 0) {  // inclusive prefix sum of hist[2, NH + 2): 16 buckets per lane
-                    const uint32_t per = (NH + 63) / 64, b0 = 2 + lane * per;
-                    uint32_t       loc = 0;
-                    for (uint32_t i = 0; i < per; i++)
-                        if (b0 + i < NH + 2) loc += hist[b0 + i];
-                    uint32_t run = wave_incl_scan(loc) - loc;
-                    for (uint32_t i = 0; i < per; i++)
-                        if (b0 + i < NH + 2) {
-                            run += hist[b0 + i];
-                            hist[b0 + i] = run;
-                        }
+                stamp(4);
+                probe_end();
+                done = true;
+            }
+        }
+        // the general path: descriptors in LDS batches (jobs with more runs than the lanes hold,
+        // duplicate R keys, the hash and histogram joins)
+        auto probe_survivors = [&](auto&& op) {
+            probe_begin();
+            for (uint32_t d0 = i0; d0 < i1; d0 += kJoinDesc) {
+                const uint32_t nd = min(kJoinDesc, i1 - d0);
+                __syncthreads();  // previous descriptors consumed
+                if ((uint32_t) tid < nd) {
+                    const uint32_t it = d0 + tid;
+                    dcnt[tid]         = P.surv_cnt[(uint64_t) it * NSUB + s];
+                    dbase[tid]        = stag(item_e0(J, it), P.surv_off[(uint64_t) it * NSUB + s]);
                 }
                 __syncthreads();
-                walk(RR{}, RW{}, SideR{}, rcnt, rbase, da, db, [&](uint32_t x) {
-                    keys[atomicAdd(&hist[(x & (NH - 1u)) + 1], 1u)] = x;  // bucket b: [hist[b], hist[b + 1])
+                walk(SR{}, SW{}, SideS{}, dcnt, dbase, 0, nd, op);
+            }
+            probe_end();
+        };
+        auto load_r = [&](uint32_t d0, uint32_t nd) {  // R run descriptors of a batch
+            __syncthreads();  // previous R descriptors consumed
+            if ((uint32_t) tid < nd) {
+                const uint64_t r = (uint64_t) (d0 + tid) * NSUB + s;
+                rcnt[tid]        = P.r_cnt[r];
+                rbase[tid]       = rtag(d0 + tid, P.r_off[r]);
+            }
+            __syncthreads();
+        };
+        if (!hashed && !done) {  // every R key sets bit v; a bit already set means a duplicate key
+            __syncthreads();
+            for (uint32_t i = tid; i < kJoinWords / 4; i += kJoinThreads) ((uint4*) tab)[i] = make_uint4(0, 0, 0, 0);
+            if (tid == 0) dupflag = 0;
+            uint32_t dup = 0;
+            for (uint32_t d0 = w0; d0 < w1; d0 += kJoinDesc) {
+                const uint32_t nd = min(kJoinDesc, w1 - d0);
+                load_r(d0, nd);
+                walk(RR{}, RW{}, SideR{}, rcnt, rbase, 0, nd, [&](uint32_t x) {
+                    const uint32_t bit = 1u << (x & 31u);
+                    dup |= atomicOr(&tab[x >> 5], bit) & bit;
                 });
-                if (P.jkind == 1) {
-                    probe_survivors([&](uint32_t x) {
-                        const uint32_t b = x & (NH - 1u);
-                        for (uint32_t j = hist[b], e = hist[b + 1]; j < e; j++) cnt += keys[j] == x;
-                    });
-                } else {
-                    probe_survivors([&](uint32_t x) {
-                        const uint32_t b = x & (NH - 1u), j0 = hist[b], e = hist[b + 1];
-                        for (uint32_t j = j0 & ~3u; j < e; j += 4) {
-                            const uint4 k = *(const uint4*) &keys[j];
-                            cnt += (k.x == x && j >= j0) + (k.y == x && j + 1 >= j0 && j + 1 < e) +
-                                   (k.z == x && j + 2 >= j0 && j + 2 < e) + (k.w == x && j + 3 < e);
+            }
+            if (dup) dupflag = 1;
+            __syncthreads();
+            hashed = dupflag != 0;  // uniform
+            if (!hashed) probe_survivors([&](uint32_t x) { cnt += (tab[x >> 5] >> (x & 31u)) & 1u; });
+        }
+        if (hashed) {  // duplicate R keys (or keys too wide for the bitmap): counting hash table over
+                       // pieces of consecutive R runs holding <= kJoinPiece keys (a run has <= slot)
+            for (uint32_t d0 = w0; d0 < w1; d0 += kJoinDesc) {
+                const uint32_t nd = min(kJoinDesc, w1 - d0);
+                load_r(d0, nd);
+                if (tid == 0) {
+                    uint32_t np = 0, acc = 0;
+                    pend[0] = 0;
+                    for (uint32_t d = 0; d < nd; d++) {
+                        if (acc + rcnt[d] > kJoinPiece && acc > 0) {
+                            pend[++np] = d;
+                            acc        = 0;
                         }
+                        acc += rcnt[d];
+                    }
+                    pend[++np] = nd;
+                    npieces    = np;
+                }
+                __syncthreads();
+                const uint32_t np = npieces;
+                for (uint32_t pc = 0; pc < np; pc++) {
+                    const uint32_t da = pend[pc], db = pend[pc + 1];
+                    __syncthreads();
+                    if (P.jkind == 0) {  // counting hash table (bucket_chaining_join's role)
+                        for (uint32_t i = tid; i < kJoinT / 4; i += kJoinThreads)
+                            ((uint4*) tab)[i] = make_uint4(kEmpty, kEmpty, kEmpty, kEmpty);
+                        __syncthreads();
+                        walk(RR{}, RW{}, SideR{}, rcnt, rbase, da, db, [&](uint32_t x) { join_insert(tab, x); });
+                        probe_survivors([&](uint32_t x) { cnt += join_count(tab, x); });  // (starts with a barrier)
+                        continue;
+                    }
+                    // Histogram join of Kim et al. (histogram_join / histogram_optimized_join,
+                    // src/parallel_radix_join_bloom.c:350-419, :441-555): a histogram of the piece's R
+                    // keys over NH = max(4, next_pow2(n) / 4) buckets, its prefix sum, the keys
+                    // reordered by bucket (keys = tab[0, kJoinPiece), hist = tab[kJoinPiece, +NH + 2));
+                    // every survivor compares the keys of its bucket -- one by one (PRH), or 4 per
+                    // 16-byte LDS read (PRHO, the reference's SIMD compare).
+                    uint32_t n = 0;
+                    for (uint32_t d = da; d < db; d++) n += rcnt[d];
+                    uint32_t NH = 4;
+                    while (NH * 4 < n) NH <<= 1;
+                    uint32_t* keys = tab;
+                    uint32_t* hist = tab + kJoinPiece;
+                    for (uint32_t i = tid; i < NH + 2; i += kJoinThreads) hist[i] = 0;
+                    __syncthreads();
+                    walk(RR{}, RW{}, SideR{}, rcnt, rbase, da, db, [&](uint32_t x) { atomicAdd(&hist[(x & (NH - 1u)) + 2], 1u); });
+                    __syncthreads();
+                    if (wave == 0) {  // inclusive prefix sum of hist[2, NH + 2): 16 buckets per lane
+                        const uint32_t per = (NH + 63) / 64, b0 = 2 + lane * per;
+                        uint32_t       loc = 0;
+                        for (uint32_t i = 0; i < per; i++)
+                            if (b0 + i < NH + 2) loc += hist[b0 + i];
+                        uint32_t run = wave_incl_scan(loc) - loc;
+                        for (uint32_t i = 0; i < per; i++)
+                            if (b0 + i < NH + 2) {
+                                run += hist[b0 + i];
+                                hist[b0 + i] = run;
+                            }
+                    }
+                    __syncthreads();
+                    walk(RR{}, RW{}, SideR{}, rcnt, rbase, da, db, [&](uint32_t x) {
+                        keys[atomicAdd(&hist[(x & (NH - 1u)) + 1], 1u)] = x;  // bucket b: [hist[b], hist[b + 1])
                     });
+                    if (P.jkind == 1) {
+                        probe_survivors([&](uint32_t x) {
+                            const uint32_t b = x & (NH - 1u);
+                            for (uint32_t j = hist[b], e = hist[b + 1]; j < e; j++) cnt += keys[j] == x;
+                        });
+                    } else {
+                        probe_survivors([&](uint32_t x) {
+                            const uint32_t b = x & (NH - 1u), j0 = hist[b], e = hist[b + 1];
+                            for (uint32_t j = j0 & ~3u; j < e; j += 4) {
+                                const uint4 k = *(const uint4*) &keys[j];
+                                cnt += (k.x == x && j >= j0) + (k.y == x && j + 1 >= j0 && j + 1 < e) +
+                                       (k.z == x && j + 2 >= j0 && j + 2 < e) + (k.w == x && j + 3 < e);
+                            }
+                        });
+                    }
                 }
             }
         }
     }
-    cnt = wave_sum_u64(cnt);
-    if (lane == 0) wsum[wave] = cnt;
-    __syncthreads();
-    if (tid == 0) {
-        uint64_t t = 0;
-        for (int w = 0; w < kJoinWaves; w++) t += wsum[w];
-        uint64_t* slot = &P.jsum[(blk % kJoinSumSlots) * kJoinSumStride];
-        if (t) atomicAdd((unsigned long long*) slot, (unsigned long long) t);
-        atomicAdd((unsigned long long*) (slot + 1), (unsigned long long) t_probe);
-        atomicAdd((unsigned long long*) (slot + 2), (unsigned long long) (wall_clock64() - t_start));
-    }
-    stamp(5);
 #ifdef HWBRJ_STAMPS
     if (P.dbg && tid == 0)
         for (int k = 0; k < 6; k++) atomicAdd((unsigned long long*) &P.dbg[(blk & 1023u) * 8 + k], (unsigned long long) tph[k]);
 #endif
 }
 
-// The uniform-format join (every launch without unstaged probe items, the north star's) and the
-// mixed one; both are launched, the one whose case this is not returns at once. The mixed one runs
-// on a small grid of persistent workgroups (an empty launch of it costs ~1 us, a full grid ~14 us);
-// it is rare: the Engine stops packing after a join that had unstaged items (pack3_hint_).
+// The join: one workgroup per work item. Survivor runs have one format unless some probe item
+// overflowed its stage (P.fmt_cnt, read once: MIXED, rare, since the Engine stops packing after a
+// join that had such items). A workgroup adds its count to partial sum blk % kJoinSumSlots (each in
+// its own 128-byte line) and takes a ticket of that slot (word 3); the slot's last workgroup adds
+// the slot into the result. k_join_split zeroes the slots.
 __global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
-    if (P.r_pack3 && P.fmt_cnt && *P.fmt_cnt) return;
-    join_job<false>(P, blockIdx.x);
-}
-
-__global__ __launch_bounds__(kJoinThreads) void k_join_mixed(JoinParams P) {
-    if (!(P.r_pack3 && P.fmt_cnt && *P.fmt_cnt)) return;
-    for (uint32_t b = blockIdx.x; b < P.jobs + kJoinExtra; b += gridDim.x) {
-        __syncthreads();  // the previous job's LDS reads are done
-        join_job<true>(P, b);
+    __shared__ JoinLds L;
+    const uint64_t t_start = P.timing ? wall_clock64() : 0;
+    uint64_t       cnt = 0, t_probe = 0;
+    if (P.r_pack3 && P.fmt_cnt && *P.fmt_cnt)
+        join_one<true>(P, L, cnt, t_probe);
+    else
+        join_one<false>(P, L, cnt, t_probe);
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    cnt = wave_sum_u64(cnt);
+    __syncthreads();  // (a workgroup that returned early from join_one meets the others here)
+    if (lane == 0) L.wsum[wave] = cnt;
+    __syncthreads();
+    if (tid != 0) return;
+    uint64_t t = 0;
+    for (int v = 0; v < kJoinWaves; v++) t += L.wsum[v];
+    const uint32_t i    = blockIdx.x % kJoinSumSlots;
+    uint64_t*      slot = &P.jsum[i * kJoinSumStride];
+    if (t) atomicAdd((unsigned long long*) slot, (unsigned long long) t);
+    if (P.timing) {
+        atomicAdd((unsigned long long*) (slot + 1), (unsigned long long) t_probe);
+        atomicAdd((unsigned long long*) (slot + 2), (unsigned long long) (wall_clock64() - t_start));
     }
-}
-
-// result[0] += matches; result[3], result[4] += probe / total ticks of the join workgroups
-__global__ __launch_bounds__(64) void k_join_sum(const uint64_t* __restrict__ jsum, uint64_t* result) {
-    const uint64_t v  = wave_sum_u64(jsum[threadIdx.x * kJoinSumStride]);
-    const uint64_t tp = wave_sum_u64(jsum[threadIdx.x * kJoinSumStride + 1]);
-    const uint64_t tt = wave_sum_u64(jsum[threadIdx.x * kJoinSumStride + 2]);
-    if (threadIdx.x == 0) {
-        if (v) atomicAdd((unsigned long long*) result, (unsigned long long) v);
-        atomicAdd((unsigned long long*) (result + 3), (unsigned long long) tp);
-        atomicAdd((unsigned long long*) (result + 4), (unsigned long long) tt);
+    __threadfence();
+    const uint32_t group = (gridDim.x - i + kJoinSumSlots - 1) / kJoinSumSlots;  // workgroups of slot i
+    if (atomicAdd((unsigned long long*) (slot + 3), 1ull) != group - 1u) return;
+    __threadfence();  // the slot's last workgroup: every add of its group is visible
+    const uint64_t v = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (v) atomicAdd((unsigned long long*) P.result, (unsigned long long) v);  // result[0] += matches
+    if (P.timing) {  // result[3], result[4] += probe / total ticks
+        atomicAdd((unsigned long long*) (P.result + 3),
+                  (unsigned long long) __hip_atomic_load(slot + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        atomicAdd((unsigned long long*) (P.result + 4),
+                  (unsigned long long) __hip_atomic_load(slot + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     }
 }
 
@@ -3702,7 +3798,8 @@ void launch_pj_item_tables(const uint32_t* tab, uint32_t pairs, uint32_t W, cons
 // from starts[], then words = bound[(j + 1) QL] - bound[j QL] when bound is given (survivors), else
 // starts[j QL] (the position of j's first chunk), then this rank's status and `extra`.
 __global__ void k_pj_counts(const uint32_t* __restrict__ starts, const uint64_t* __restrict__ bound, uint32_t W,
-                            uint32_t QL, uint32_t NC, uint64_t status, uint64_t extra, uint64_t* __restrict__ out) {
+                            uint32_t QL, uint32_t NC, uint64_t status, uint64_t extra, uint64_t extra2,
+                            uint64_t* __restrict__ out) {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= W * NC) return;
     const uint32_t j = t / NC, i = t % NC;
@@ -3710,13 +3807,14 @@ __global__ void k_pj_counts(const uint32_t* __restrict__ starts, const uint64_t*
     if (i < QL) v = starts[j * QL + i + 1] - starts[j * QL + i];
     else if (i == QL) v = bound ? bound[(j + 1) * QL] - bound[j * QL] : starts[j * QL];
     else if (i == QL + 1) v = status;
-    else v = extra;
+    else if (i == QL + 2) v = extra;
+    else v = extra2;
     out[t] = v;
 }
 
 void launch_pj_counts(const uint32_t* starts, const uint64_t* bound, uint32_t W, uint32_t QL, uint32_t NC,
-                      uint64_t status, uint64_t extra, uint64_t* out, hipStream_t st) {
-    k_pj_counts<<<(W * NC + 255) / 256, 256, 0, st>>>(starts, bound, W, QL, NC, status, extra, out);
+                      uint64_t status, uint64_t extra, uint64_t extra2, uint64_t* out, hipStream_t st) {
+    k_pj_counts<<<(W * NC + 255) / 256, 256, 0, st>>>(starts, bound, W, QL, NC, status, extra, extra2, out);
 }
 
 void launch_pj_gather(const uint32_t* pool, const uint32_t* list, uint32_t n, void* out, uint32_t* ent,
@@ -3968,8 +4066,6 @@ void launch_join(const JoinParams& p0, uint32_t jobs, uint32_t* job_surv, hipStr
     k_join_split<<<(jobs + 255) / 256, 256, 0, st>>>(p.item_start, job_surv, p.log2NSUB, jobs, split,
                                                      p.nparts, p.extra, p.nextra, p.jsum);
     k_join<<<jobs + kJoinExtra, kJoinThreads, 0, st>>>(p);
-    k_join_mixed<<<std::min<uint32_t>(jobs + kJoinExtra, 1024u), kJoinThreads, 0, st>>>(p);
-    k_join_sum<<<1, kJoinSumSlots, 0, st>>>(p.jsum, p.result);
 }
 
 uint32_t join_extra_tasks() { return kJoinExtra; }

@@ -149,8 +149,8 @@ int Engine::join_partitioned(const hwbrj_exchange_t* x, int rank, int world, con
         }
         return peers(r.data(), 1, rc);
     };
-    // counts exchanges: QL partition counts, a total, the status, this rank's |S| shard
-    const uint32_t NC = QL + 3;
+    // counts exchanges: QL partition counts, a total, the status, this rank's |S| and |R| shards
+    const uint32_t NC = QL + 4;
     std::vector<double> ms(8, 0.0);
     auto lap = [&, t = std::chrono::steady_clock::now()](int k) mutable {
         const auto n = std::chrono::steady_clock::now();
@@ -185,7 +185,7 @@ int Engine::join_partitioned(const hwbrj_exchange_t* x, int rank, int world, con
         uint64_t*      ds = xcnt()->as<uint64_t>();
         uint64_t*      dr = ds + n;
         if (rc_local == 0) {
-            launch_pj_counts(d_starts, d_bound, W, QL, NC, 0, extra, ds, stream);
+            launch_pj_counts(d_starts, d_bound, W, QL, NC, 0, extra, nR, ds, stream);
         } else {
             hstat.assign(n, 0);
             for (uint32_t j = 0; j < W; j++) hstat[(uint64_t) j * NC + QL + 1] = (uint64_t) (uint32_t) rc_local;
@@ -293,14 +293,29 @@ int Engine::join_partitioned(const hwbrj_exchange_t* x, int rank, int world, con
             for (uint32_t i = 0; i < QL; i++) scnt[j * NC + i] = ls[j * QL + i + 1] - ls[j * QL + i];
             scnt[j * NC + QL]     = ls[j * QL];
             scnt[j * NC + QL + 2] = nS;
+            scnt[j * NC + QL + 3] = nR;
         }
         return drain();
     }();
     lap(0);
     // ------------------------------------------------------------- 2. R exchange
+    // Every rank learns every R shard's size with the R counts: the receive bounds come from the
+    // caller's nR_total, so shards that sum to more fail on every rank alike, before any
+    // rank enters the R all-to-all.
+    auto check_r_total = [&]() -> int {
+        uint64_t sum = 0;
+        for (uint32_t j = 0; j < W; j++) sum += rcnt[(uint64_t) j * NC + QL + 3];
+        if (sum > nR_total) {
+            set_last_error("partitioned join: the R shards hold " + std::to_string(sum) + " tuples, nR_total is " +
+                           std::to_string(nR_total));
+            return 2;
+        }
+        return 0;
+    };
     if (native) {
         if (const int rc = native_counts(lstartR.as<uint32_t>(), nullptr, rc1, nS, ls.data(), nullptr)) return rc;
         if (const int rc = peers(rcnt.data() + QL + 1, NC, rc1)) return rc;
+        if (const int rc = check_r_total()) return rc;
         PJ_STAGE("R scatter");
         launch_pj_gather(poolR.as<uint32_t>(), listR.as<uint32_t>(), ls[F], sendC, sendE, stream);
         PJ_STAGE("k_pj_gather");
@@ -308,6 +323,7 @@ int Engine::join_partitioned(const hwbrj_exchange_t* x, int rank, int world, con
         for (uint32_t j = 0; j < W; j++) scnt[j * NC + QL + 1] = (uint64_t) (uint32_t) rc1;
         PJ_XCHG(x->alltoall_u64(x->ctx, scnt.data(), rcnt.data(), NC), "R chunk counts");
         if (const int rc = peers(rcnt.data() + QL + 1, NC, rc1)) return rc;
+        if (const int rc = check_r_total()) return rc;
     }
     const int rc2 = [&]() -> int {
         for (uint32_t j = 0; j < W; j++) {
@@ -319,7 +335,8 @@ int Engine::join_partitioned(const hwbrj_exchange_t* x, int rank, int world, con
             rbytes[j] = c * 128;
             RC += c;
         }
-        if (native) {  // (allocated at RCmax before the counts step)
+        if (native) {  // (allocated at RCmax before the counts step; with the R shards summing to at
+                       // most nR_total, RC cannot exceed it: a bug guard)
             if (RC > RCmax) {
                 set_last_error("partitioned join: received R chunks above their bound");
                 return 21;
@@ -579,7 +596,8 @@ int Engine::join_partitioned(const hwbrj_exchange_t* x, int rank, int world, con
             RI += c;
             RW += rwords[j];
         }
-        if (native) {  // (allocated at RImax / RWmax before the counts step)
+        if (native) {  // (allocated at RImax / RWmax before the counts step, from every shard's exact
+                       // |S|, so no input can exceed them: a bug guard)
             if (RI > RImax || RW > RWmax) {
                 set_last_error("partitioned join: received survivors above their bound");
                 return 21;
@@ -713,6 +731,7 @@ int Engine::join_partitioned(const hwbrj_exchange_t* x, int rank, int world, con
     jp.nextra          = jparts.as<uint32_t>() + 2 * F * NSUB;
     jp.item_base       = pjIbase.as<uint64_t>();
     jp.split_surv      = test_hooks().join_split;
+    jp.timing          = 1;
     launch_join(jp, NJ, pjJobs.as<uint32_t>(), stream);
     PJ_STAGE("k_join");
     PJ_CHECK(hipGetLastError());

@@ -135,8 +135,15 @@ typedef struct hwbrj_stats_t {
     double   ms_surv;       /* survivor sub-partitioning: fused into the probe (k_probe), ~0 */
     double   ms_join;
     double   ms_join_probe; /* the survivor-probing share of ms_join (k_join's probe sections),
-                               printed as PROBE-TIME-USECS */
+                               printed as PROBE-TIME-USECS; synchronous joins only (0 for async) */
+    /* The key format between the build / probe and the join ("Join keys"):
+     * HWBRJ_JOIN_KEYS_32 32-bit codes, _PACKED 3-byte keys, _MIXED 3-byte keys with the survivor
+     * runs of unstaged probe items in 32-bit codes. It follows the last waited join on the device
+     * (after a join with unstaged items the next one does not pack). */
+    int      join_keys;
+    uint32_t unstaged_items; /* probe items whose survivors overflowed the probe's LDS stage */
 } hwbrj_stats_t;
+enum { HWBRJ_JOIN_KEYS_32 = 0, HWBRJ_JOIN_KEYS_PACKED = 1, HWBRJ_JOIN_KEYS_MIXED = 2 };
 
 /* Join device-resident tuple arrays (tuple_t layout). args == NULL runs PRO (no filter).
  * stream: a hipStream_t (NULL = the library's own stream). The call is synchronous. */
@@ -317,7 +324,8 @@ int          hwbrj_set_device(int device);
 void         hwbrj_release(void); /* free all device buffers */
 const char * hwbrj_last_error(void);
 /* "hwbloomradixjoin_amd <version> (gfx950)"; a build whose kernels were compiled with any
- * non-default switch (tuning A/Bs, dev ablations) appends " knobs: NAME=value ..." naming them. */
+ * non-default switch (tuning A/Bs, dev ablations) appends " knobs: NAME=value ..." naming them,
+ * and so does every test hook that is set (hwbrj_set_test_hook). */
 const char * hwbrj_version(void);
 
 /* Test hooks (no reference counterpart): process-wide settings that force rarely taken paths or
@@ -331,7 +339,9 @@ const char * hwbrj_version(void);
  *                             join's non-root side (k_build writes no filter slices; they come
  *                             from ncclBroadcast, which at world 1 leaves the buffer as it is).
  *                             1 = as is, 2 = the slice buffer zeroed first (the filter is then
- *                             empty unless something writes it: the counts must drop).
+ *                             empty unless something writes it: the counts must drop). Honoured
+ *                             only on a communicator of world 1 (a test setting; ignored by a
+ *                             real multi-rank broadcast).
  * Returns 0, or 2 for an unknown hook or a value out of range. */
 enum { HWBRJ_HOOK_JOIN_SPLIT = 1, HWBRJ_HOOK_PJ_FAIL_RANK = 2, HWBRJ_HOOK_BCAST_NONROOT = 3 };
 int          hwbrj_set_test_hook(int hook, int64_t value);

@@ -48,6 +48,26 @@ def test_struct_layouts_match_reference(hw):
     assert ctypes.sizeof(hw._ThreadResult) == 24
 
 
+def test_stats_layout_matches_header(hw, tmp_path):
+    """hwbrj_stats_t as the C compiler lays it out (include/hwbrj.h) equals the ctypes mirror,
+    including the join key format fields at its end."""
+    import ctypes
+    src = tmp_path / "st.c"
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "hwbrj.h"\nint main(void) {\n'
+                   '  printf("%zu %zu %zu %zu %d %d %d\\n", sizeof(hwbrj_stats_t), offsetof(hwbrj_stats_t, '
+                   'ms_join_probe), offsetof(hwbrj_stats_t, join_keys), offsetof(hwbrj_stats_t, '
+                   'unstaged_items), HWBRJ_JOIN_KEYS_32, HWBRJ_JOIN_KEYS_PACKED, HWBRJ_JOIN_KEYS_MIXED);\n'
+                   '  return 0;\n}\n')
+    exe = tmp_path / "st"
+    subprocess.run(["gcc", "-std=gnu11", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"),
+                    "-o", str(exe), str(src)], check=True)
+    got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True,
+                                          check=True).stdout.split()]
+    S = hw._Stats
+    assert got == [ctypes.sizeof(S), S.ms_join_probe.offset, S.join_keys.offset,
+                   S.unstaged_items.offset, hw.JOIN_KEYS_32, hw.JOIN_KEYS_PACKED, hw.JOIN_KEYS_MIXED]
+
+
 def test_host_hashes_match_reference_kats(hw):
     for row in KATS["kats"]:
         assert hw.hash_crc(42, row["key"]) == row["crc32c"]
@@ -181,18 +201,16 @@ def test_bench_uses_pmc_traffic_only_for_the_profiled_library(tmp_path, hw):
 
 
 def test_bench_modeled_join_key_bytes():
-    """modeled_bytes prices the join's runs at 3 bytes per key exactly where the engine stores
-    3-byte keys (hwbrj_kernels.h join_pack3: hash_shift = log2 F + log2 subparts >= 8, code-digit
-    partitions), else 4."""
+    """modeled_bytes prices the join's runs at the key format the join reported
+    (hwbrj_stats_t.join_keys): 3 bytes per key for packed and mixed runs, else 4."""
     import importlib.util
     from types import SimpleNamespace as NS
     spec = importlib.util.spec_from_file_location("bench", os.path.join(ROOT, "bench.py"))
     bench = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(bench)
-    assert bench.join_key_bytes(NS(mode=1, partitions=1024, subparts=16)) == 3.0  # north star
-    assert bench.join_key_bytes(NS(mode=0, partitions=1024, subparts=16)) == 3.0  # PRO
-    assert bench.join_key_bytes(NS(mode=1, partitions=16, subparts=8)) == 4.0     # hash_shift 7
-    assert bench.join_key_bytes(NS(mode=2, partitions=1024, subparts=64)) == 4.0  # slice-basic: mixed keys
+    assert bench.join_key_bytes(NS(join_keys=1)) == 3.0  # packed (the north star)
+    assert bench.join_key_bytes(NS(join_keys=2)) == 3.0  # mixed
+    assert bench.join_key_bytes(NS(join_keys=0)) == 4.0  # 32-bit codes
     mb = bench.modeled_bytes(10, 20, 5, 0, 4.0, 3.0)
     assert mb["join_codes_R"] == 60.0 and mb["survivors"] == 30.0
 

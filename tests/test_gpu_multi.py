@@ -210,6 +210,21 @@ def test_partitioned_rccl_failure_world1(hw, cuda, orc, rccl1, hook):
     assert (st.filtered, st.matches) == (g["rows"]["1024"][0], g["results"])
 
 
+def test_partitioned_rccl_understated_r_total(hw, cuda, orc, rccl1):
+    """the receive bounds of the native transport come from the caller's nR_total. Every
+    rank's |R| shard travels with the R counts, so shards that sum to more than nR_total fail on every
+    rank alike before the R all-to-all (code 2), and the next join is correct."""
+    g = GOLD["F3_grid"]
+    R = hw.generate_host(g["r"], 2, g["r"], g["r"], 1.0, 1)
+    S = hw.generate_host(g["s"], 2, INT_MAX, g["r"], g["q"], 2)
+    dR, dS = to_dev(cuda, R), to_dev(cuda, S)
+    args = hw.BloomFilterArgs(hw.BLOCKED, g["m"], 1, 1024)
+    with pytest.raises(RuntimeError, match="R shards hold"):
+        rccl1.join_partitioned_rccl(dR, dS, g["r"] // 2, args)
+    st = rccl1.join_partitioned_rccl(dR, dS, g["r"], args)
+    assert (st.filtered, st.matches) == (g["rows"]["1024"][0], g["results"])
+
+
 @pytest.mark.parametrize("a", [("blocked", 1 << 24, 1, 1024), ("sectorized", 1 << 24, 2, 1024),
                                ("basic", 1 << 24, 1, 1024), ("blocked", 1 << 31, 2, 512)], ids=str)
 def test_filter_broadcast_nonroot_world1(hw, cuda, orc, rccl1, hook, a):

@@ -486,7 +486,8 @@ def test_join_key_formats_across_launches(hw, cuda, orc):
     stops packing after a join that had such items (pack3_hint_). At the north star's filter size
     (stage of 2592 words per 12288-tuple item), S with ~21 % members puts some items over the
     stage and some under. The sequence low, low (packed), mid (mixed launch), mid (32-bit), low
-    (32-bit), low (packed again) must count what the oracle counts every time."""
+    (32-bit), low (packed again) must count what the oracle counts every time, and the path each
+    join took (hwbrj_stats_t.join_keys, unstaged_items) must be that sequence."""
     rng = np.random.default_rng(23)
     nR, nS = 1 << 20, 1 << 24
     Rk = rng.permutation(nR).astype(np.int64) + 1
@@ -503,7 +504,13 @@ def test_join_key_formats_across_launches(hw, cuda, orc):
         res, filt, _ = orc.bpro(R, S, 8, args.variant, args.m, args.k, args.B)
         assert res == int(np.isin(Sk, Rk).sum())
         want[name] = (filt, res, to_dev(cuda, R), to_dev(cuda, S))
-    for name in ("lo", "lo", "mid", "mid", "lo", "lo"):
+    seq = [("lo", hw.JOIN_KEYS_PACKED), ("lo", hw.JOIN_KEYS_PACKED), ("mid", hw.JOIN_KEYS_MIXED),
+           ("mid", hw.JOIN_KEYS_32), ("lo", hw.JOIN_KEYS_32), ("lo", hw.JOIN_KEYS_PACKED)]
+    hw.join_device(want["lo"][2], want["lo"][3], args)  # (a packing join before the sequence)
+    for name, keys in seq:
         filt, res, dR, dS = want[name]
         st = hw.join_device(dR, dS, args)
         assert (st.filtered, st.matches) == (filt, res), (name, st)
+        assert st.join_keys == keys, (name, st)
+        # unstaged items: some in every mid join (packed or not), none in a lo join
+        assert (st.unstaged_items > 0) == (name == "mid"), (name, st)
