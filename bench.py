@@ -64,6 +64,10 @@ def parse():
     ap.add_argument("--filter-bcast", action="store_true",
                     help="replicated design: rank 0 builds the filter, ncclBroadcast sends it to "
                          "every rank (the north_star's bitmap broadcast) instead of a rebuild per rank")
+    ap.add_argument("--no-alt-designs", action="store_true",
+                    help="N > 1 (or any process group): skip the extra legs that time the other "
+                         "multi-GPU designs on the same ranks after the headline (alt_designs)")
+    ap.add_argument("--alt-steps", type=int, default=5, help="timed joins per alt_designs leg")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the PCIe-inclusive end-to-end time")
     ap.add_argument("--cpu-sample", type=int, default=0,
@@ -239,6 +243,10 @@ def main():
         t = torch.tensor([elapsed, dev_ms], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, dev_ms = (float(x) for x in t.tolist())
+    # the other multi-GPU designs on the same ranks, after the headline (never its value)
+    alt = None
+    if dist and not a.no_alt_designs and not a.filter_bcast:
+        alt = alt_designs(a, hw, torch, dist, rank, world, local, dR, dS, args, shared)
 
     if rank != 0:
         if dist:
@@ -334,12 +342,114 @@ def main():
                  "backend": dist.get_backend() if dist else None,
                  "shared_gpu_rehearsal": shared},
         "phase_ms": {k[3:]: round(v, 4) for k, v in mean.items()},
+        "alt_designs": alt,
         "published_ref": {"value": 3.98e8, "config": "blocked B=512 k=1 m=2^30, 2x Xeon Gold 6226 "
                           "48 threads (thesis data, BASELINE.md)"},
     }
     print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()
+
+
+def alt_designs(a, hw, torch, dist, rank, world, local, dR, dS, args, shared):
+    """The designs the headline does not run, timed on the same ranks and shards right after it, so
+    one multi-GPU run decides between them:
+      bcast        the replicated design with the north_star's bitmap broadcast: rank 0 builds the
+                   filter slices, ncclBroadcast sends them (hwbrj_set_filter_broadcast); K joins
+                   enqueued back to back, HIP events, max over ranks (one GPU per rank: RCCL);
+      partitioned  R range-sharded too, partitions owned by ranks: the R chunk and survivor
+                   all-to-alls and the slice all-gather (hwbrj_join_partitioned_rccl; the torch
+                   callback transport when ranks share a GPU); host-synchronous, so timed by wall
+                   clock between barriers, max over ranks.
+    Each leg reports its ms per join, the probe-tuples/s that gives, and every rank's own
+    (filtered, matches), whose sums must be the headline's counts. A failing leg is reported, and
+    never stops the headline line."""
+    from hwbloomradixjoin_amd import pjoin
+    nR, nS_total = a.r_size, a.s_size
+    K = max(1, min(a.steps, a.alt_steps))
+    cdev = "cpu" if shared else "cuda"
+    out = {"steps": K, "what": "the other multi-GPU designs on the same ranks and shards after the "
+                               "headline's timed region (DESIGN.md s6); value = |S| / the slowest rank"}
+
+    def gather_counts(st):
+        c = torch.tensor([st.filtered, st.matches], dtype=torch.int64, device=cdev)
+        g = [torch.empty_like(c) for _ in range(world)]
+        dist.all_gather(g, c)
+        per = [[int(x) for x in t.tolist()] for t in g]
+        return per, [sum(col) for col in zip(*per)]
+
+    def slowest(x):
+        t = torch.tensor([x], dtype=torch.float64, device=cdev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def leg(name, run):
+        try:
+            ms, per, tot = run()
+            out[name] = {"ms": round(ms, 4), "value": round(nS_total / (ms * 1e-3), 1),
+                         "per_rank": per, "sum": tot}
+        except Exception as e:  # (reported; the headline stands)
+            out[name] = {"failed": str(e)[:300]}
+
+    native = not shared
+    if native:
+        pjoin.comm_init()
+    slice_filter = args is not None and not (args.variant == hw.BASIC and args.k > 1)
+
+    def bcast():
+        pjoin.set_filter_broadcast(True)
+        try:
+            per, tot = gather_counts(hw.join_device(dR, dS, args))
+            stream = torch.cuda.Stream()
+            hw.join_device_async(dR, dS, args, stream=stream)
+            hw.join_wait()
+            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            dist.barrier()
+            torch.cuda.synchronize()
+            ev0.record(stream)
+            for _ in range(K):
+                hw.join_device_async(dR, dS, args, stream=stream)
+            ev1.record(stream)
+            hw.join_wait()
+            torch.cuda.synchronize()
+            dist.barrier()
+            return slowest(ev0.elapsed_time(ev1) / K), per, tot
+        finally:
+            pjoin.set_filter_broadcast(False)
+
+    def partitioned():
+        rlo, rhi = hw.shard_range(nR, rank, world)
+        dRs = dR[rlo:rhi]
+        if native:
+            def join():
+                return pjoin.join_partitioned_rccl(dRs, dS, nR, args)
+        else:
+            x = pjoin.TorchExchange(torch.device("cuda", local))
+
+            def join():
+                return pjoin.join_partitioned(dRs, dS, nR, args, x)
+        per, tot = gather_counts(join())
+        join()
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(K):
+            join()
+        torch.cuda.synchronize()
+        dist.barrier()
+        return slowest((time.perf_counter() - t0) / K * 1e3), per, tot
+
+    if native and slice_filter:
+        leg("bcast", bcast)
+    else:
+        out["bcast"] = {"skipped": "needs one GPU per rank (RCCL) and a slice filter"}
+    if args is None or slice_filter:
+        leg("partitioned", partitioned)
+    else:
+        out["partitioned"] = {"skipped": "basic k > 1 has no partition slices"}
+    if native:
+        pjoin.comm_destroy()
+    return out
 
 
 def run_partitioned(a, hw, torch, dist, rank, world, local, dR, dS, args, shared):

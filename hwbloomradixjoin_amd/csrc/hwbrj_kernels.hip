@@ -2441,7 +2441,10 @@ __global__ __launch_bounds__(256) void k_join_split(const uint32_t* __restrict__
 #define HWBRJ_JFS HWBRJ_JSR  // fused path: survivor runs per wave loaded with the R runs
 #endif
 #ifndef HWBRJ_JFS2
-#define HWBRJ_JFS2 16  // fused path: survivor runs per wave issued once the R keys are set
+#define HWBRJ_JFS2 16  // fused path: further survivor runs per wave (issued once the R keys are set)
+#endif
+#ifndef HWBRJ_JS2E
+#define HWBRJ_JS2E 0  // 1: the further survivor runs issued with the R runs instead (A/B)
 #endif
 
 // Uniform facts of one work item (scalar registers).
@@ -2736,6 +2739,8 @@ __device__ __forceinline__ void join_one(const JoinParams& P, JoinLds& L, uint64
             }
             uint32_t sv[FS][FSW], svm, stl, spk;
             sload(std::integral_constant<int, FS>{}, X, 0, nSd, sv, svm, stl, spk);
+            uint32_t sv2[FS2][FSW], svm2, stl2, spk2;
+            if (HWBRJ_JS2E) sload(std::integral_constant<int, FS2>{}, X, FS, nSd, sv2, svm2, stl2, spk2);
             for (uint32_t i = tid; i < kJoinWords / 4; i += kJoinThreads) ((uint4*) tab)[i] = make_uint4(0, 0, 0, 0);
             if (tid == 0) dupflag = 0;
             if (lane == 0) rkw[wave] = rk;
@@ -2756,8 +2761,7 @@ __device__ __forceinline__ void join_one(const JoinParams& P, JoinLds& L, uint64
                 tail_run(SideR{}, rtag(w0 + wave + kJoinWaves * r, __builtin_amdgcn_readlane(X.ro, r)), 64u * FW, n, set);
             }
             // the further survivor runs, into the registers the R runs leave
-            uint32_t sv2[FS2][FSW], svm2, stl2, spk2;
-            sload(std::integral_constant<int, FS2>{}, X, FS, nSd, sv2, svm2, stl2, spk2);
+            if (!HWBRJ_JS2E) sload(std::integral_constant<int, FS2>{}, X, FS, nSd, sv2, svm2, stl2, spk2);
             __syncthreads();
             stamp(1);
             {
@@ -4118,6 +4122,8 @@ const char* kernel_build_knobs() {
         num("HWBRJ_JSW", HWBRJ_JSW, 2);
         num("HWBRJ_JFR", HWBRJ_JFR, 8);
         num("HWBRJ_JFW", HWBRJ_JFW, 5);
+        num("HWBRJ_JFS2", HWBRJ_JFS2, 16);
+        num("HWBRJ_JS2E", HWBRJ_JS2E, 0);
         num("HWBRJ_ABL_PROBE", HWBRJ_ABL_PROBE, 0);
         num("HWBRJ_PCO", HWBRJ_PCO, 1);
         num("HWBRJ_PCO_AUX", HWBRJ_PCO_AUX, 0);

@@ -243,19 +243,19 @@ def test_write_result_relation_reference_order(hw, tmp_path):
 
 def test_prof_summary_phase_labels():
     """tools/prof_summary.py (the per-phase PMC traffic bench.py's roofline.traffic comes from)
-    takes the last join between two k_join_sum dispatches and labels plan / list-fill kernels by
-    the side of the scatter before them, whichever side the Engine runs first."""
+    takes the last join between two k_join dispatches (a join's last kernel) and labels plan /
+    list-fill kernels by the side of the scatter before them, whichever side the Engine runs first."""
     import importlib.util
     spec = importlib.util.spec_from_file_location("prof_summary", os.path.join(ROOT, "tools", "prof_summary.py"))
     ps = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(ps)
     one = ["k_scatter_s", "k_plan", "k_list_fill", "k_scatter_r", "k_plan", "k_list_fill", "k_build",
-           "k_probe", "k_join_split", "k_join", "k_join_mixed", "k_join_sum"]
+           "k_probe", "k_join_split", "k_join"]
     names = ["k_gen"] + one + ["__amd_rocclr_copyBuffer"] + one + ["k_copy_bw"]
     idx = ps.last_join(names)
     assert [names[i] for i in idx] == ["__amd_rocclr_copyBuffer"] + one
     assert ps.label(names, idx) == ["other", "s_scatter", "s_index", "s_index", "r_scatter", "r_index",
-                                    "r_index", "build", "probe", "join", "join", "join", "join"]
+                                    "r_index", "build", "probe", "join", "join"]
     r_first = ["k_scatter_r", "k_plan", "k_list_fill", "k_build", "k_scatter_s", "k_plan", "k_list_fill"]
     assert ps.label(r_first, range(len(r_first))) == ["r_scatter", "r_index", "r_index", "build",
                                                       "s_scatter", "s_index", "s_index"]

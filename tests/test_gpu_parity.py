@@ -388,6 +388,13 @@ def test_bench_two_ranks(hw):
     assert (line["parity"]["filtered"], line["parity"]["matches"]) == (g["rows"]["1024"][0], g["results"])
     per = line["parity"]["per_rank"]  # two S shards: their counts sum to the golden
     assert len(per) == 2 and [sum(c) for c in zip(*per)] == [g["rows"]["1024"][0], g["results"]]
+    # the other designs on the same ranks: the broadcast needs a GPU per rank,
+    # the partitioned join runs over the torch transport; its per-rank counts sum to the golden
+    alt = line["alt_designs"]
+    assert "skipped" in alt["bcast"]
+    part = alt["partitioned"]
+    assert len(part["per_rank"]) == 2 and part["sum"] == [g["rows"]["1024"][0], g["results"]], part
+    assert part["ms"] > 0
 
 
 def test_bench_rccl_process_group(hw):
@@ -412,6 +419,11 @@ def test_bench_rccl_process_group(hw):
     assert (line["parity"]["filtered"], line["parity"]["matches"]) == (g["rows"]["1024"][0], g["results"])
     assert line["scaling"] == "strong" and line["dist"] == {"world_size_seen": 1, "backend": "nccl",
                                                             "shared_gpu_rehearsal": False}
+    # the other designs on the same rank over the library's RCCL communicator
+    for name in ("bcast", "partitioned"):
+        leg = line["alt_designs"][name]
+        assert leg.get("sum") == [g["rows"]["1024"][0], g["results"]] and leg["ms"] > 0, (name, leg)
+        assert leg["per_rank"] == [leg["sum"]]
 
 
 def _sorted_pairs(p):
@@ -482,18 +494,21 @@ def test_join_skew_split_forced(hw, cuda, orc, gen3, split, hook):
 
 def test_join_key_formats_across_launches(hw, cuda, orc):
     """3-byte join keys (pack3): a probe item whose survivors overflow its LDS stage
-    keeps 32-bit survivor runs, so a launch can hold both formats (k_join_mixed), and the Engine
-    stops packing after a join that had such items (pack3_hint_). At the north star's filter size
-    (stage of 2592 words per 12288-tuple item), S with ~21 % members puts some items over the
-    stage and some under. The sequence low, low (packed), mid (mixed launch), mid (32-bit), low
-    (32-bit), low (packed again) must count what the oracle counts every time, and the path each
-    join took (hwbrj_stats_t.join_keys, unstaged_items) must be that sequence."""
+    keeps 32-bit survivor runs, so a launch can hold both formats (the mixed join), and the Engine
+    stops packing after a join that had such items (pack3_hint_). At the north star's filter size the
+    stage holds 2592 survivors. Here |S| = 2^24 over 1024 partitions and 256 scatter regions: a
+    partition has ~640 chunks (~26 words each), i.e. a full 384-chunk probe item of ~9800 words and
+    a last one of ~6600. With 32 % members the full items overflow the stage and the last ones do
+    not (a mixed launch); with 1 % none overflows. The sequence low, low (packed), mid (mixed
+    launch), mid (32-bit), low (32-bit), low (packed again) must count what the oracle counts every
+    time, and the path each join took (hwbrj_stats_t.join_keys, unstaged_items) must be that
+    sequence (round 4's 21 % members never overflowed a stage)."""
     rng = np.random.default_rng(23)
     nR, nS = 1 << 20, 1 << 24
     Rk = rng.permutation(nR).astype(np.int64) + 1
     outside = lambda n: rng.integers(2 * nR, INT_MAX, size=n)  # never in R
     S_lo = np.concatenate([rng.integers(1, nR + 1, size=nS // 100), outside(nS - nS // 100)])
-    S_mid = np.concatenate([rng.integers(1, nR + 1, size=nS * 21 // 100), outside(nS - nS * 21 // 100)])
+    S_mid = np.concatenate([rng.integers(1, nR + 1, size=nS * 32 // 100), outside(nS - nS * 32 // 100)])
     rng.shuffle(S_lo)
     rng.shuffle(S_mid)
     args = hw.BloomFilterArgs(hw.BLOCKED, 1 << 30, 1, 1024)

@@ -16,7 +16,7 @@ from collections import defaultdict
 
 # kernel -> phase (hwbrj_engine.cpp Engine::enqueue)
 PHASE_OF = {"k_build_global": "build", "k_build": "build", "k_probe_global": "probe",
-            "k_probe": "probe", "k_join_split": "join", "k_join": "join", "k_join_mixed": "join", "k_join_sum": "join", "k_plan": "index",
+            "k_probe": "probe", "k_join_split": "join", "k_join": "join", "k_plan": "index",
             "k_list_fill": "index", "k_mat_build": "materialize", "k_mat_probe": "materialize"}
 
 
@@ -28,10 +28,11 @@ def one(path_glob):
 
 
 def last_join(names):
-    """Indices of the dispatches of the last join: after the previous join's final count reduction
-    (k_join_sum) up to its own, so kernels the bench runs after the joins (its copy-rate
-    measurement) are not counted. The S pass may come first (Engine::enqueue) or the R side."""
-    ends = [i for i, n in enumerate(names) if n == "k_join_sum"]
+    """Indices of the dispatches of the last join: after the previous join's last kernel (k_join,
+    which also reduces the counts) up to its own, so kernels the bench runs after the joins (its
+    copy-rate measurement) are not counted. The S pass may come first (Engine::enqueue) or the R
+    side."""
+    ends = [i for i, n in enumerate(names) if n == "k_join"]
     if not ends:
         return list(range(len(names)))
     b = ends[-2] + 1 if len(ends) > 1 else 0
