@@ -685,8 +685,7 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     jp.CH              = CH;
     jp.log2NSUB        = g.log2NSUB;
     jp.hash_shift      = g.hash_shift;
-    jp.bitmap          = (g.sub_shift > 0 && 32 - g.hash_shift <= 18) ? 1u : 0u;
-    jp.result          = d_result;
+    jp.bitmap          = (g.sub_shift > 0 && 32 - g.hash_shift <= join_bitmap_log2()) ? 1u : 0u;
     jp.jsum            = (uint64_t*) ((char*) small.p + 128);  // 64 partial sums, one per 128-B line
     jp.dbg             = dbg_on ? dbgJ.as<uint64_t>() : nullptr;
     jp.nparts          = jparts.as<uint32_t>();
@@ -737,6 +736,7 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     pending_sfirst_ = s_first;
     pending_fmt_    = pp.fmt_cnt != nullptr;
     pending_pack3_  = pack3;
+    pending_slots_  = !mat;
     pending_stream_ = stream;
     have_filter_  = args != nullptr;
     last_g_       = g;
@@ -839,7 +839,6 @@ int Engine::enqueue_basic_kk(const uint2* dR, uint64_t nR, const uint2* dS, uint
         return 4;
     }
     if (alloc_only_) return 0;
-    uint64_t* d_result   = small.as<uint64_t>();
     uint64_t* d_filtered = small.as<uint64_t>() + 2;
     uint64_t* cnt        = kkcnt.as<uint64_t>();  // [j]: candidates after pass j (j < k - 1); [NC - 1]: dummy
     uint32_t* wgc[2]     = {(uint32_t*) (cnt + NC), (uint32_t*) (cnt + NC) + G};  // per-workgroup counts
@@ -998,8 +997,7 @@ int Engine::enqueue_basic_kk(const uint2* dR, uint64_t nR, const uint2* dS, uint
     jp.CH              = CH;
     jp.log2NSUB        = gj.log2NSUB;
     jp.hash_shift      = gj.hash_shift;
-    jp.bitmap          = (gj.sub_shift > 0 && 32 - gj.hash_shift <= 18) ? 1u : 0u;
-    jp.result          = d_result;
+    jp.bitmap          = (gj.sub_shift > 0 && 32 - gj.hash_shift <= join_bitmap_log2()) ? 1u : 0u;
     jp.jsum            = (uint64_t*) ((char*) small.p + 128);
     jp.nparts          = jparts.as<uint32_t>();
     jp.extra           = jtask.as<uint2>();
@@ -1018,9 +1016,28 @@ int Engine::enqueue_basic_kk(const uint2* dR, uint64_t nR, const uint2* dS, uint
     pending_sfirst_ = false;
     pending_fmt_    = false;
     pending_pack3_  = false;
+    pending_slots_  = true;
     pending_stream_ = stream;
     have_filter_  = true;
     last_g_       = g;
+    return 0;
+}
+
+int read_join_counts(const void* small, bool slots, hipStream_t stream, uint64_t h[6]) {
+    const size_t          S = join_sum_slots(), W = join_sum_stride();
+    std::vector<uint64_t> buf(16 + (slots ? S * W : 0));  // 128 bytes of result words, then the slots
+    if (hipMemcpyAsync(buf.data(), small, buf.size() * 8, hipMemcpyDeviceToHost, stream) != hipSuccess ||
+        hipStreamSynchronize(stream) != hipSuccess) {
+        set_last_error("reading the join's counts failed");
+        return 1;
+    }
+    for (int i = 0; i < 6; i++) h[i] = buf[i];
+    if (slots)
+        for (size_t j = 0; j < S; j++) {
+            h[0] += buf[16 + j * W];
+            h[3] += buf[16 + j * W + 1];
+            h[4] += buf[16 + j * W + 2];
+        }
     return 0;
 }
 
@@ -1041,7 +1058,7 @@ int Engine::wait(hwbrj_stats_t* st) {
     const uint64_t* d_result   = small.as<uint64_t>();      // (see enqueue)
     const uint64_t* d_filtered = small.as<uint64_t>() + 2;
     uint64_t small_h[6] = {0, 0, 0, 0, 0, 0};  // matches, dcount, filtered, probe ticks, join ticks, unstaged items
-    HWBRJ_CHECK(hipMemcpy(small_h, d_result, sizeof small_h, hipMemcpyDeviceToHost));
+    if (const int rc = read_join_counts(d_result, pending_slots_, own_stream_, small_h)) return rc;
     if (pending_fmt_) pack3_hint_ = (uint32_t) small_h[5] == 0;  // (k_probe's count, ProbeParams::fmt_cnt)
     (void) d_filtered;
     const uint64_t matches = small_h[0], filtered = small_h[2];

@@ -120,6 +120,7 @@ class Engine {
     bool         pending_sfirst_ = false;  // the pending join ran its S pass first (phase boundaries)
     bool         pending_fmt_    = false;  // the pending join counted its unstaged probe items
     bool         pending_pack3_  = false;  // the pending join packed its join keys
+    bool         pending_slots_  = false;  // the pending join's matches are in k_join's partial sums
     bool         pack3_hint_     = true;   // the last waited join had none: 3-byte join keys pay
     int          pending_rc_     = 0;   // nonzero: the pending join failed after enqueuing kernels
     std::string  pending_err_;
@@ -158,6 +159,10 @@ void    set_last_error(const std::string& s);
 // RCCL entry points used by the engine (hwbrj_comm.cpp; librccl is bound at first use). Return 0 or
 // an error code with the message in set_last_error.
 int rccl_broadcast(void* comm, void* buf, size_t bytes, int root, hipStream_t stream);
+// The counts a join leaves in the small buffer (`small`: result words, then k_join's partial-sum
+// slots), read in one copy: h[0] matches, h[1] dense count, h[2] filtered, h[3] probe ticks,
+// h[4] join ticks, h[5] unstaged probe items; with slots, their sums are added to h[0], h[3], h[4].
+int read_join_counts(const void* small, bool slots, hipStream_t stream, uint64_t h[6]);
 int rccl_agree_status(void* comm, int world, int rank, int rc, hipStream_t stream, DevBuf* tmp);
 class Engine;
 int rccl_alltoall_u64_dev(Engine* e, const uint64_t* d_send, uint64_t* d_recv, uint64_t n);

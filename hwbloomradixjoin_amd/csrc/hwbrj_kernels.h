@@ -105,9 +105,8 @@ struct JoinParams {
     uint32_t        nseg, CH, log2NSUB, hash_shift;
     uint32_t        slot;         // r_codes words per build sweep
     uint32_t        bitmap;       // 1: keys fit the direct-address bitmap (32 - hash_shift <= 18)
-    uint64_t*       result;
-    uint64_t*       jsum;         // kJoinSumSlots partial sums, one per 128-byte line (word 3: the
-                                  // slot's workgroup ticket), zeroed by k_join_split
+    uint64_t*       jsum;         // kJoinSumSlots partial sums, one per 128-byte line (zeroed by
+                                  // k_join_split, summed by the host)
     uint32_t        jobs;         // F * NSUB (set by launch_join)
     uint32_t*       nparts;       // [jobs] parts of each job (k_join_split)
     uint2*          extra;        // [join_extra_tasks()] {job, part} of the further parts
@@ -192,6 +191,11 @@ void   launch_probe_bitj(const ProbeParams& p, uint32_t grid, hipStream_t st);
 // splits skewed jobs (job_surv: survivors per job from k_probe, cleared here) and runs the join
 void   launch_join(const JoinParams& p, uint32_t jobs, uint32_t* job_surv, hipStream_t st);
 uint32_t join_extra_tasks();
+// k_join's partial sums (JoinParams::jsum): join_sum_slots() slots of join_sum_stride() u64 words,
+// word 0 matches, 1 probe ticks, 2 total ticks (P.timing); the host adds them up
+uint32_t join_sum_slots();
+uint32_t join_sum_stride();
+uint32_t join_bitmap_log2();  // k_join's bitmap path: job keys v < 2^join_bitmap_log2()
 void   launch_join_mat(const MatJoinParams& p, uint32_t jobs, hipStream_t st);
 // result materialization (K12): R table build, S probe writing (R.payload, S.payload) pairs
 void   launch_mat_build(const uint2* R, uint64_t n, unsigned long long* tab, uint64_t mask,

@@ -2333,9 +2333,12 @@ void launch_probe_bitj(const ProbeParams& p, uint32_t grid, hipStream_t st) {
 #endif
 constexpr int      kJoinThreads = HWBRJ_JT;
 constexpr int      kJoinWaves   = kJoinThreads / 64;
-constexpr uint32_t kJoinBmLog2  = 18;                  // bitmap path: v < 2^18
+#ifndef HWBRJ_JBM
+#define HWBRJ_JBM 18  // bitmap path: keys v < 2^HWBRJ_JBM (17: half the LDS, with 32 subs; dev A/B)
+#endif
+constexpr uint32_t kJoinBmLog2  = HWBRJ_JBM;           // bitmap path: v < 2^18
 constexpr uint32_t kJoinWords   = 1u << (kJoinBmLog2 - 5);  // 8192 LDS words (32 KiB)
-constexpr uint32_t kJoinLog2T   = 13;                  // hash path: 8192 slots in the same words
+constexpr uint32_t kJoinLog2T   = kJoinBmLog2 - 5;     // hash path: 8192 slots in the same words
 constexpr uint32_t kJoinT       = 1u << kJoinLog2T;
 constexpr uint32_t kJoinPiece   = kJoinT / 2;
 constexpr uint32_t kJoinDesc    = 256;                 // run descriptors per batch
@@ -2386,8 +2389,7 @@ constexpr uint32_t kJoinTaskSurv = 1u << 17;
 constexpr uint32_t kJoinExtra    = 2048;
 
 // Match counts: every join workgroup adds its count to one of kJoinSumSlots partial sums (each in
-// its own 128-byte line, so the adds are not serialised on one address); the last workgroup of the
-// launch adds them into the result.
+// its own 128-byte line, so the adds are not serialised on one address); the host sums them.
 constexpr uint32_t kJoinSumSlots = 64;
 constexpr uint32_t kJoinSumStride = 16;  // u64 words per slot (128 bytes)
 
@@ -2397,8 +2399,8 @@ __global__ __launch_bounds__(256) void k_join_split(const uint32_t* __restrict__
                                                      uint32_t* __restrict__ nparts,
                                                      uint2* __restrict__ extra, uint32_t* nextra,
                                                      uint64_t* __restrict__ jsum) {
-    if (blockIdx.x == 0 && threadIdx.x < kJoinSumSlots)  // (word 3: k_join's ticket of the slot)
-        for (int w = 0; w < 4; w++) jsum[threadIdx.x * kJoinSumStride + w] = 0;
+    if (blockIdx.x == 0 && threadIdx.x < kJoinSumSlots)
+        for (int w = 0; w < 3; w++) jsum[threadIdx.x * kJoinSumStride + w] = 0;
     const uint32_t job = blockIdx.x * blockDim.x + threadIdx.x;  // one thread per job
     if (job >= NJ) return;
     const uint32_t q = job >> log2NSUB, items = item_start[q + 1] - item_start[q];
@@ -2416,131 +2418,57 @@ __global__ __launch_bounds__(256) void k_join_split(const uint32_t* __restrict__
     nparts[job] = np;
 }
 
-// One workgroup per work item: items [0, jobs) are part 0 of job map(item), the rest the further
-// parts of skewed jobs (k_join_split's table). A job is a chain of memory latencies (its descriptors,
-// its R and survivor runs). On the fused path every lane loads the descriptors of its wave's runs
-// (read back uniformly with readlane, no LDS staging), the R runs and the first survivor runs are
-// in flight together, and the further survivor runs are issued as soon as the R keys are in the
-// bitmap, so they arrive while the workgroup counts the bitmap and tests the first ones. Only
-// validity bits stay live past a load. Counts go to kJoinSumSlots partial sums; the last workgroup
-// of each slot's group adds its sum into the result (no separate sum launch).
+// One (job, part) of the join on workgroup slot blk; MIXED: survivor runs of both formats (below).
+// Adds this thread's matches to cnt_acc and (P.timing) the workgroup's probe ticks to tp_acc.
+template <bool MIXED>
+__device__ __forceinline__ void join_job(const JoinParams& P, const uint32_t blk, uint64_t& cnt_acc, uint64_t& tp_acc) {
+    __shared__ __attribute__((aligned(16))) uint32_t tab[kJoinWords];  // bitmap or hash table
+    __shared__ uint64_t dbase[kJoinDesc];  // run starts (byte offsets) of a batch: S survivor runs
+    __shared__ uint32_t dcnt[kJoinDesc];
+    __shared__ uint64_t rbase[kJoinDesc];  // R runs (one per build sweep of q)
+    __shared__ uint32_t rcnt[kJoinDesc];
+    __shared__ uint32_t pend[kJoinDesc + 1];  // hash path: piece boundaries inside an R batch
+    __shared__ uint32_t dupflag, npieces;
+    const uint32_t NSUB = 1u << P.log2NSUB;
+    uint32_t       job = blk, part = 0;  // workgroup j < jobs: part 0 of job j
 #ifndef HWBRJ_JXCD
 #define HWBRJ_JXCD 1
 #endif
-#ifndef HWBRJ_JFR
-#define HWBRJ_JFR 8  // fused path: R runs per wave
-#define HWBRJ_JFW 5  // fused path: R words per lane per run (runs average slot / NSUB words)
-#endif
-#ifndef HWBRJ_JRR
-#define HWBRJ_JRR 4
-#define HWBRJ_JRW 4
-#define HWBRJ_JSR 8
-#define HWBRJ_JSW 2
-#endif
-#ifndef HWBRJ_JFS
-#define HWBRJ_JFS HWBRJ_JSR  // fused path: survivor runs per wave loaded with the R runs
-#endif
-#ifndef HWBRJ_JFS2
-#define HWBRJ_JFS2 16  // fused path: further survivor runs per wave (issued once the R keys are set)
-#endif
-#ifndef HWBRJ_JS2E
-#define HWBRJ_JS2E 0  // 1: the further survivor runs issued with the R runs instead (A/B)
-#endif
-
-// Uniform facts of one work item (scalar registers).
-struct JobInfo {
-    uint32_t job, s, w0, w1, qi0, qi1, i0, i1, lq0, npc;
-};
-
-// This lane's run descriptors of a job, for the fused path: lane l of wave v holds R run and
-// survivor run d = v + kJoinWaves * l (the wave's run l), read back uniformly with readlane.
-struct JobDesc {
-    uint32_t rc, ro;  // R run: keys, offset in its sweep slot
-    uint32_t sc, so;  // survivor run: keys, surv_off entry (bit 31: 3-byte keys)
-    uint64_t se;      // survivor run: element base of its item region
-};
-
-// LDS of a join workgroup (one instance per kernel, shared by both format instantiations)
-struct JoinLds {
-    uint32_t tab[kJoinWords] __attribute__((aligned(16)));  // bitmap or hash table
-    uint64_t dbase[kJoinDesc];  // general path: survivor run starts (tagged byte offsets) of a batch
-    uint32_t dcnt[kJoinDesc];
-    uint64_t rbase[kJoinDesc];  // R runs (one per build sweep of q)
-    uint32_t rcnt[kJoinDesc];
-    uint32_t pend[kJoinDesc + 1];  // hash path: piece boundaries inside an R batch
-    uint32_t dupflag, npieces, rkw[kJoinWaves];
-    uint64_t wsum[kJoinWaves];
-};
-
-template <bool MIXED>
-__device__ __forceinline__ void join_one(const JoinParams& P, JoinLds& L, uint64_t& cnt, uint64_t& t_probe) {
-    uint32_t* const tab = L.tab;
-    uint64_t* const dbase = L.dbase;
-    uint32_t* const dcnt = L.dcnt;
-    uint64_t* const rbase = L.rbase;
-    uint32_t* const rcnt = L.rcnt;
-    uint32_t* const pend = L.pend;
-    uint32_t& dupflag = L.dupflag;
-    uint32_t& npieces = L.npieces;
-    uint32_t* const rkw = L.rkw;
-    const uint32_t NSUB = 1u << P.log2NSUB;
-    const uint32_t blk  = blockIdx.x;
-    const uint32_t W    = P.jobs + min(*P.nextra, kJoinExtra);  // work items of this launch
-    const int      tid = threadIdx.x, lane = tid & 63;
-    const uint32_t wave = __builtin_amdgcn_readfirstlane((uint32_t) tid >> 6);
-    const bool     rpk  = P.r_pack3 != 0;
-    const uint32_t sh   = P.hash_shift;
     // XCD-aware job order: blocks b, b + 8, ... share an XCD (dealt round-robin), so they take
     // consecutive jobs -- the 16 subs of a partition run on one XCD, where the lines their runs
     // share (adjacent sub runs in every sweep slot and item region) are fetched into its L2 once
-    const bool xcd = HWBRJ_JXCD && (P.jobs & 7u) == 0;
-    auto info = [&](uint32_t w) -> JobInfo {
-        JobInfo J;
-        uint32_t part = 0;
-        if (w < P.jobs) {
-            J.job = xcd ? (w & 7u) * (P.jobs >> 3) + (w >> 3) : w;
-        } else {  // a further part of a skewed job
-            const uint2 x = P.extra[w - P.jobs];
-            J.job         = x.x;
-            part          = x.y;
-        }
-        const uint32_t q = J.job >> P.log2NSUB, np = P.nparts[J.job];
-        J.s   = J.job & (NSUB - 1u);
-        J.w0  = P.r_sweep_start[q];
-        J.w1  = P.r_sweep_start[q + 1];
-        J.qi0 = P.item_start[q];  // q's items (segment-major)
-        J.qi1 = P.item_start[q + 1];
-        J.i0  = J.qi0 + (uint32_t) ((uint64_t) (J.qi1 - J.qi0) * part / np);
-        J.i1  = J.qi0 + (uint32_t) ((uint64_t) (J.qi1 - J.qi0) * (part + 1) / np);
-        J.lq0 = P.item_base ? 0u : P.list_start[q];
-        J.npc = (J.qi1 - J.qi0) / P.nseg;  // probe pieces of q
-        return J;
+    if (HWBRJ_JXCD && blk < P.jobs && (P.jobs & 7u) == 0) job = (blk & 7u) * (P.jobs >> 3) + (blk >> 3);
+    if (blk >= P.jobs) {                 // extra workgroups: further parts of skewed jobs
+        const uint32_t e = blk - P.jobs;
+        if (e >= min(*P.nextra, kJoinExtra)) return;
+        const uint2 x = P.extra[e];
+        job           = x.x;
+        part          = x.y;
+    }
+    const uint32_t q = job >> P.log2NSUB, s = job & (NSUB - 1u);
+    const uint32_t w0 = P.r_sweep_start[q], w1 = P.r_sweep_start[q + 1];
+    const uint32_t qi0 = P.item_start[q], qi1 = P.item_start[q + 1];  // q's items (segment-major)
+    const uint32_t np  = P.nparts[job];
+    const bool     rpk = P.r_pack3 != 0;
+    const uint32_t i0  = qi0 + (uint32_t) ((uint64_t) (qi1 - qi0) * part / np);
+    const uint32_t i1  = qi0 + (uint32_t) ((uint64_t) (qi1 - qi0) * (part + 1) / np);
+    if (w1 == w0 || i1 == i0) return;
+    const uint32_t lq0 = P.item_base ? 0u : P.list_start[q];
+    const uint32_t npc = (qi1 - qi0) / P.nseg;  // probe pieces of q
+    const uint32_t sh  = P.hash_shift;
+    const int      tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    uint64_t       cnt = 0;
+    // probe share of the join (the reference's per-thread probe timers, :289-321): the 100 MHz
+    // ticks of the survivor-probing sections of this workgroup (synchronous joins only, P.timing)
+    uint64_t t_probe = 0, t_mark = 0;
+    auto probe_begin = [&]() {
+        if (P.timing) t_mark = wall_clock64();
     };
-    // element base of item it's survivor region
-    auto item_e0 = [&](const JobInfo& J, uint32_t it) -> uint64_t {
-        if (P.item_base) return P.item_base[it];  // (the partitioned multi-GPU join)
-        const uint32_t local = it - J.qi0, seg = local / J.npc, piece = local - seg * J.npc;
-        return (uint64_t) seg * P.surv_seg_stride + (uint64_t) (J.lq0 + piece * P.CH) * 32;
-    };
-    constexpr int FR = HWBRJ_JFR, FW = HWBRJ_JFW;
-    auto descs = [&](const JobInfo& J) -> JobDesc {
-        JobDesc        X{0, 0, 0, 0, 0};
-        const uint32_t d = wave + kJoinWaves * (uint32_t) lane;
-        if (lane < FR && d < J.w1 - J.w0) {
-            const uint64_t r = (uint64_t) (J.w0 + d) * NSUB + J.s;
-            X.rc             = P.r_cnt[r];
-            X.ro             = P.r_off[r];
-        }
-        if (d < J.i1 - J.i0) {
-            const uint32_t it = J.i0 + d;
-            X.sc              = P.surv_cnt[(uint64_t) it * NSUB + J.s];
-            X.so              = P.surv_off[(uint64_t) it * NSUB + J.s];
-            X.se              = item_e0(J, it);
-        }
-        return X;
+    auto probe_end = [&]() {
+        if (P.timing) t_probe += wall_clock64() - t_mark;
     };
     // dev-only phase stamps of wave 0 (build with -DHWBRJ_STAMPS, run with HWBRJ_DBG): fused path
-    // 0 descriptors + zeroing, 1 R loads + bit sets, 2 popcount, 3 first survivor runs, 4 further runs
+    // 0 descriptors, 1 R loads + bit sets, 2 popcount, 3 first survivor runs, 4 further runs, 5 sum
     uint64_t tph[6] = {0, 0, 0, 0, 0, 0}, tlast = __builtin_amdgcn_s_memtime();
     (void) tlast;
     (void) tph;
@@ -2555,23 +2483,15 @@ __device__ __forceinline__ void join_one(const JoinParams& P, JoinLds& L, uint64
         (void) k;
 #endif
     };
-    // probe share of the join (the reference's per-thread probe timers, :289-321), synchronous joins
-    // only (P.timing): the 100 MHz ticks of the survivor-probing sections of this workgroup
-    uint64_t t_mark = 0;
-    auto probe_begin = [&]() {
-        if (P.timing) t_mark = wall_clock64();
-    };
-    auto probe_end = [&]() {
-        if (P.timing) t_probe += wall_clock64() - t_mark;
-    };
     // Run formats. A run is addressed by a tagged byte offset tb from its array's base: bit 63 set =
     // 3-byte keys (pack3), key o the low 24 bits of the unaligned dword at tb + 3 o; else 32-bit
     // codes at tb + 4 o, key = code >> sh. R runs share one format (the build's); survivor runs are
     // packed when their probe item was staged (bit 31 of surv_off). P.fmt_cnt counts the unstaged
     // items: with none (or no pack3 at all) every run of the launch has one format, whose stride,
-    // shift and mask are uniform; otherwise (MIXED: only where probe items overflow their stage)
-    // the survivor runs are read with a per-run format, R runs packed. Loads stay raw until used
-    // (key()): ALU work on a conditionally loaded value would make the wave wait for it at once.
+    // shift and mask are uniform (k_join); otherwise the survivor runs are mixed and read with a
+    // per-run format (k_join_mixed: only where probe items overflow their stage), R runs packed.
+    // Loads stay raw until used (key()): ALU work on a conditionally loaded value would make the
+    // wave wait for it at once.
     constexpr uint64_t kPk = 1ull << 63;
     const uint32_t kst = rpk ? 3u : 4u, ksh = rpk ? 0u : sh, kmk = rpk ? 0xFFFFFFu : 0xFFFFFFFFu;
     const uint8_t* const r8 = (const uint8_t*) P.r_codes;
@@ -2614,8 +2534,8 @@ __device__ __forceinline__ void join_one(const JoinParams& P, JoinLds& L, uint64
                 if (o + 64u * u < n) op(key(side_c, v[u], (bb & kPk) != 0));
         }
     };
-    // Every word of runs [da, db) of a descriptor batch in LDS through op(word): a wave per run,
-    // RUNS runs in flight per wave with WPL words per lane each; longer runs finish in a tail loop.
+    // Every word of runs [da, db) of a descriptor batch through op(word): a wave per run, RUNS runs
+    // in flight per wave with WPL words per lane each; longer runs finish in a tail loop.
     auto walk = [&](auto runs_c, auto wpl_c, auto side_c, const uint32_t* nc,
                     const uint64_t* nb, uint32_t da, uint32_t db, auto&& op) {
         constexpr int RUNS = decltype(runs_c)::value, WPL = decltype(wpl_c)::value;
@@ -2645,123 +2565,156 @@ __device__ __forceinline__ void join_one(const JoinParams& P, JoinLds& L, uint64
             }
         }
     };
+#ifndef HWBRJ_JRR
+#define HWBRJ_JRR 4
+#define HWBRJ_JRW 4
+#define HWBRJ_JSR 8
+#define HWBRJ_JSW 2
+#endif
     using RR = std::integral_constant<int, HWBRJ_JRR>;  // R runs in flight per wave
     using RW = std::integral_constant<int, HWBRJ_JRW>;  // R words per lane per run
     using SR = std::integral_constant<int, HWBRJ_JSR>;  // survivor runs in flight per wave
     using SW = std::integral_constant<int, HWBRJ_JSW>;
-    constexpr int FS = HWBRJ_JFS, FS2 = HWBRJ_JFS2, FSW = HWBRJ_JSW;
-    auto rl64 = [](uint64_t x, uint32_t l) -> uint64_t {
-        return (uint64_t) __builtin_amdgcn_readlane((uint32_t) x, l) |
-               (uint64_t) __builtin_amdgcn_readlane((uint32_t) (x >> 32), l) << 32;
-    };
-    // survivor run r of this wave (run d = wave + kJoinWaves r of the job), from the lanes' descriptors
-    auto srun = [&](const JobDesc& X, uint32_t r, uint32_t nSd, uint32_t& n) -> uint64_t {
-        r &= 63u;  // (lanes past the wave's runs are never used: n = 0)
-        n = wave + kJoinWaves * r < nSd ? __builtin_amdgcn_readlane(X.sc, r) : 0u;
-        return stag(rl64(X.se, r), __builtin_amdgcn_readlane(X.so, r));
-    };
-    // Survivor runs [r0, r0 + N) of this wave into registers (N runs in flight, FSW words per lane).
-    // Past the loads only bits stay live: vm bit r FSW + j = slot j of run r holds a key, tl bit r =
-    // run r is longer than its registers, pk bit r = run r holds 3-byte keys (MIXED)
-    auto sload = [&](auto n_c, const JobDesc& X, uint32_t r0, uint32_t nSd, uint32_t (&v)[decltype(n_c)::value][FSW],
-                     uint32_t& vm, uint32_t& tl, uint32_t& pk) {
-        constexpr int N = decltype(n_c)::value;
-        static_assert(N * FSW <= 32, "validity bits");
-        vm = tl = pk = 0;
-#pragma unroll
-        for (int r = 0; r < N; r++) {
-            uint32_t       n;
-            const uint64_t bb = srun(X, r0 + r, nSd, n);
-#ifdef HWBRJ_ABL_JNOS
-            n = 0;  // dev ablation (results invalid)
-#endif
-            tl |= (uint32_t) (n > 64u * FSW) << r;
-            pk |= (uint32_t) (bb >> 63) << r;
-#pragma unroll
-            for (int j = 0; j < FSW; j++) {
-                const uint32_t o  = lane + 64u * j;
-                const bool     ok = o < n;
-                vm |= (uint32_t) ok << (r * FSW + j);
-                v[r][j] = ok ? ldv(SideS{}, bb, o) : 0u;
+    // the survivors of (q, s), batch by batch, against the table: bitmap (BM) or hash table
+    auto probe_survivors = [&](auto&& op) {
+        probe_begin();
+        for (uint32_t d0 = i0; d0 < i1; d0 += kJoinDesc) {
+            const uint32_t nd = min(kJoinDesc, i1 - d0);
+            __syncthreads();  // previous descriptors consumed
+            if ((uint32_t) tid < nd) {
+                const uint32_t it    = d0 + tid;
+                const uint32_t local = it - qi0;
+                const uint32_t seg   = local / npc;
+                const uint32_t piece = local - seg * npc;
+                dcnt[tid]  = P.surv_cnt[(uint64_t) it * NSUB + s];
+                dbase[tid] = stag(P.item_base ? P.item_base[it]  // (the partitioned multi-GPU join)
+                                              : (uint64_t) seg * P.surv_seg_stride + (uint64_t) (lq0 + piece * P.CH) * 32,
+                                  P.surv_off[(uint64_t) it * NSUB + s]);
             }
+            __syncthreads();
+            walk(SR{}, SW{}, SideS{}, dcnt, dbase, 0, nd, op);
         }
+        probe_end();
     };
-    auto stest = [&](auto n_c, const JobDesc& X, uint32_t r0, uint32_t nSd, const uint32_t (&v)[decltype(n_c)::value][FSW],
-                     uint32_t vm, uint32_t tl, uint32_t pk, auto&& test) {
-        constexpr int N = decltype(n_c)::value;
-#pragma unroll
-        for (int r = 0; r < N; r++)
-#pragma unroll
-            for (int j = 0; j < FSW; j++)
-                if ((vm >> (r * FSW + j)) & 1u) test(key(SideS{}, v[r][j], (pk >> r) & 1u));
-        while (tl) {  // (rare) runs longer than their registers
-            const uint32_t r = __builtin_ctz(tl);
-            tl &= tl - 1u;
-            uint32_t       n;
-            const uint64_t bb = srun(X, r0 + r, nSd, n);
-            tail_run(SideS{}, bb, 64u * FSW, n, test);
+    // R run descriptors of a batch
+    auto load_r = [&](uint32_t d0, uint32_t nd) {
+        __syncthreads();  // previous R descriptors consumed
+        uint32_t c = 0;
+        if ((uint32_t) tid < nd) {
+            const uint64_t r = (uint64_t) (d0 + tid) * NSUB + s;
+            c                = P.r_cnt[r];
+            rcnt[tid]        = c;
+            rbase[tid]       = rtag(d0 + tid, P.r_off[r]);
         }
+        (void) c;
+        __syncthreads();
     };
-
-    if (blk >= W) return;
-    const JobInfo J = info(blk);
-    if (J.w1 == J.w0 || J.i1 == J.i0) return;
-    const uint32_t nRd = J.w1 - J.w0, nSd = J.i1 - J.i0;
-    {
-        const uint32_t s = J.s, i0 = J.i0, i1 = J.i1, w0 = J.w0, w1 = J.w1;
-        // PRH / PRHO (P.jkind 1 / 2): the histogram join of every job, below
-        bool hashed = !P.bitmap || P.jkind != 0;
-        bool done   = false;
-        if (!hashed && nRd <= (uint32_t) (kJoinWaves * FR) && nSd <= (uint32_t) (kJoinWaves * 64)) {
-            // Fused bitmap path (every job of the north star): the descriptors, then the R runs and
-            // the first survivor runs loaded before any is used; the bitmap is zeroed while they are
-            // in flight.
-            const JobDesc X = descs(J);
-            static_assert(FR * FW <= 64, "R validity bits");
-            uint32_t rv[FR][FW], rtl = 0, rk = 0;  // rtl bit r: R run r is longer than its registers
-            uint64_t rvm = 0;                      // bit r FW + j: R slot j of run r holds a key
+    // PRH / PRHO (P.jkind 1 / 2): the histogram join of every job, below
+    bool hashed = !P.bitmap || P.jkind != 0;
+    bool done   = false;
+#ifndef HWBRJ_JFR
+#define HWBRJ_JFR 8  // fused path: R runs per wave
+#define HWBRJ_JFW 5  // fused path: R words per lane per run (runs average slot / NSUB words)
+#endif
+    constexpr int FR = HWBRJ_JFR, FW = HWBRJ_JFW;
+    const uint32_t nRd = w1 - w0, nSd = i1 - i0;
+    if (!hashed && nRd <= (uint32_t) (kJoinWaves * FR) && nSd <= kJoinDesc) {
+        // Fused bitmap path (every job of the north star): both descriptor sets in one phase, then
+        // the loads of all R runs and of the first survivor runs are issued before any is used, so
+        // a job costs two memory latencies (descriptors, data) instead of one per batch.
+        for (uint32_t i = tid; i < kJoinWords / 4; i += kJoinThreads) ((uint4*) tab)[i] = make_uint4(0, 0, 0, 0);
+        if (tid == 0) dupflag = 0;
+        uint32_t rc = 0;
+        if ((uint32_t) tid < nRd) {
+            const uint64_t r = (uint64_t) (w0 + tid) * NSUB + s;
+            rcnt[tid]        = P.r_cnt[r];
+            rbase[tid]       = rtag(w0 + tid, P.r_off[r]);
+            rc = rcnt[tid];
+        }
+        stamp(0);
+        if (wave == 0) {  // the job's R keys (nRd <= 64: every R descriptor is in wave 0)
+            const uint32_t t = __builtin_amdgcn_readlane(wave_incl_scan_dpp(rc), 63);
+            if (lane == 0) npieces = t;
+        }
+        if ((uint32_t) tid < nSd) {
+            const uint32_t it    = i0 + tid;
+            const uint32_t local = it - qi0;
+            const uint32_t seg   = local / npc;
+            const uint32_t piece = local - seg * npc;
+            dcnt[tid]  = P.surv_cnt[(uint64_t) it * NSUB + s];
+            dbase[tid] = stag(P.item_base ? P.item_base[it]  // (the partitioned multi-GPU join)
+                                          : (uint64_t) seg * P.surv_seg_stride + (uint64_t) (lq0 + piece * P.CH) * 32,
+                              P.surv_off[(uint64_t) it * NSUB + s]);
+        }
+        __syncthreads();
+#ifndef HWBRJ_JFS
+#define HWBRJ_JFS HWBRJ_JSR
+#endif
+#ifndef HWBRJ_JS2
+#define HWBRJ_JS2 0  // survivor runs per wave issued behind the R bit sets (0: none)
+#endif
+        constexpr int FS = HWBRJ_JFS, FSW = HWBRJ_JSW;  // survivor runs per wave loaded with R's
+#ifndef HWBRJ_JG12
+#define HWBRJ_JG12 0  // packed launches: keys loaded as aligned 12-byte groups of 4 (A/B: 0)
+#endif
+        if (HWBRJ_JG12 && !MIXED && rpk) {
+            // Every run of a packed launch holds 3-byte keys, 4 per 12-byte group from its slot's or
+            // region's (4-byte aligned) start, so a lane loads whole groups with one aligned 12-byte
+            // load: R runs 2 groups per lane (512 keys), survivor runs 1 (256 keys), instead of one
+            // unaligned dword per key. A run at byte b0 starts at key r0 = (-b0) & 3 of its group.
+            struct alignas(4) U3 {
+                uint32_t x, y, z;
+            };
+            auto gkey = [](const U3& g, int j) -> uint32_t {  // key j of a group (pack3x4's layout)
+                return j == 0   ? g.x & 0xFFFFFFu
+                       : j == 1 ? __builtin_amdgcn_alignbit(g.y, g.x, 24) & 0xFFFFFFu
+                       : j == 2 ? __builtin_amdgcn_alignbit(g.z, g.y, 16) & 0xFFFFFFu
+                                : g.z >> 8;
+            };
+            U3       rg[FR][2], sg[FS];
+            uint32_t rn[FR], rr0[FR], sn[FS], sr0[FS];
 #pragma unroll
             for (int r = 0; r < FR; r++) {
-                uint32_t n = wave + kJoinWaves * r < nRd ? __builtin_amdgcn_readlane(X.rc, r) : 0u;
+                const uint32_t dd = wave + r * kJoinWaves;
+                rn[r]             = dd < nRd ? rcnt[dd] : 0u;
 #ifdef HWBRJ_ABL_JNOR
-                n = 0;  // dev ablation (results invalid)
+                rn[r] = 0;  // dev ablation (results invalid)
 #endif
-                rk += n;
-                rtl |= (uint32_t) (n > 64u * FW) << r;
-                const uint64_t bb = rtag(w0 + wave + kJoinWaves * r, __builtin_amdgcn_readlane(X.ro, r));
+                const uint64_t b0 = (dd < nRd ? rbase[dd] : 0ull) & ~kPk;
+                rr0[r]            = (0u - (uint32_t) b0) & 3u;
+                const uint8_t* gp = r8 + (b0 - 3u * rr0[r]);
+                const uint32_t ng = (rn[r] + rr0[r] + 3u) >> 2;
 #pragma unroll
-                for (int j = 0; j < FW; j++) {
-                    const uint32_t o  = lane + 64u * j;
-                    const bool     ok = o < n;
-                    rvm |= (uint64_t) ok << (r * FW + j);
-                    rv[r][j] = ok ? ldv(SideR{}, bb, o) : 0u;
+                for (int h = 0; h < 2; h++) {
+                    const uint32_t g = lane + 64u * h;
+                    rg[r][h]         = g < ng ? *(const U3*) (gp + 12u * g) : U3{0, 0, 0};
                 }
             }
-            uint32_t sv[FS][FSW], svm, stl, spk;
-            sload(std::integral_constant<int, FS>{}, X, 0, nSd, sv, svm, stl, spk);
-            uint32_t sv2[FS2][FSW], svm2, stl2, spk2;
-            if (HWBRJ_JS2E) sload(std::integral_constant<int, FS2>{}, X, FS, nSd, sv2, svm2, stl2, spk2);
-            for (uint32_t i = tid; i < kJoinWords / 4; i += kJoinThreads) ((uint4*) tab)[i] = make_uint4(0, 0, 0, 0);
-            if (tid == 0) dupflag = 0;
-            if (lane == 0) rkw[wave] = rk;
-            stamp(0);
-            __syncthreads();
-            // bits set without returns (no wave waits on them); a duplicate R key shows as fewer set
-            // bits than the job's R keys (popcount after the barrier)
+#pragma unroll
+            for (int r = 0; r < FS; r++) {
+                const uint32_t dd = wave + r * kJoinWaves;
+                sn[r]             = dd < nSd ? dcnt[dd] : 0u;
+#ifdef HWBRJ_ABL_JNOS
+                sn[r] = 0;  // dev ablation (results invalid)
+#endif
+                const uint64_t b0 = (dd < nSd ? dbase[dd] : 0ull) & ~kPk;
+                sr0[r]            = (0u - (uint32_t) b0) & 3u;
+                const uint8_t* gp = s8 + (b0 - 3u * sr0[r]);
+                sg[r]             = lane < ((sn[r] + sr0[r] + 3u) >> 2) ? *(const U3*) (gp + 12u * lane) : U3{0, 0, 0};
+            }
             auto set = [&](uint32_t x) { __hip_atomic_fetch_or(&tab[x >> 5], 1u << (x & 31u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); };
 #pragma unroll
-            for (int r = 0; r < FR; r++)
+            for (int r = 0; r < FR; r++) {
 #pragma unroll
-                for (int j = 0; j < FW; j++)
-                    if ((rvm >> (r * FW + j)) & 1u) set(key(SideR{}, rv[r][j], rpk));
-            while (rtl) {  // (rare) R runs longer than their registers
-                const uint32_t r = __builtin_ctz(rtl);
-                rtl &= rtl - 1u;
-                const uint32_t n = __builtin_amdgcn_readlane(X.rc, r);
-                tail_run(SideR{}, rtag(w0 + wave + kJoinWaves * r, __builtin_amdgcn_readlane(X.ro, r)), 64u * FW, n, set);
+                for (int h = 0; h < 2; h++)
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        const uint32_t k = 4u * (lane + 64u * h) + j;  // key k - r0 of the run
+                        if (k >= rr0[r] && k - rr0[r] < rn[r]) set(gkey(rg[r][h], j));
+                    }
+                if (rn[r] + rr0[r] > 512u)  // (rare) longer run
+                    tail_run(SideR{}, rbase[wave + r * kJoinWaves], 512u - rr0[r], rn[r], set);
             }
-            // the further survivor runs, into the registers the R runs leave
-            if (!HWBRJ_JS2E) sload(std::integral_constant<int, FS2>{}, X, FS, nSd, sv2, svm2, stl2, spk2);
             __syncthreads();
             stamp(1);
             {
@@ -2774,200 +2727,302 @@ __device__ __forceinline__ void join_one(const JoinParams& P, JoinLds& L, uint64
                 if (lane == 0 && pc) atomicAdd(&dupflag, pc);  // (dupflag: the set bits)
             }
             __syncthreads();
-            uint32_t rkt = 0;
-#pragma unroll
-            for (int v = 0; v < kJoinWaves; v++) rkt += rkw[v];
-            hashed = dupflag != rkt;  // uniform
+            hashed = dupflag != npieces;  // uniform
             stamp(2);
             if (!hashed) {
                 probe_begin();
                 auto test = [&](uint32_t x) { cnt += (tab[x >> 5] >> (x & 31u)) & 1u; };
-                stest(std::integral_constant<int, FS>{}, X, 0, nSd, sv, svm, stl, spk, test);
-                stest(std::integral_constant<int, FS2>{}, X, FS, nSd, sv2, svm2, stl2, spk2, test);
-                stamp(3);
-                // runs beyond the first FS + FS2 of this wave (more than 4 (FS + FS2) probe items)
-                for (uint32_t r0 = FS + FS2; wave + kJoinWaves * r0 < nSd; r0 += SR::value) {
-                    uint32_t v3[SR::value][FSW], vm3, tl3, pk3;
-                    sload(SR{}, X, r0, nSd, v3, vm3, tl3, pk3);
-                    stest(SR{}, X, r0, nSd, v3, vm3, tl3, pk3, test);
+#pragma unroll
+                for (int r = 0; r < FS; r++) {
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        const uint32_t k = 4u * lane + j;
+                        if (k >= sr0[r] && k - sr0[r] < sn[r]) test(gkey(sg[r], j));
+                    }
+                    if (sn[r] + sr0[r] > 256u) tail_run(SideS{}, dbase[wave + r * kJoinWaves], 256u - sr0[r], sn[r], test);
                 }
+                stamp(3);
+#ifndef HWBRJ_ABL_JNOS
+                walk(SR{}, SW{}, SideS{}, dcnt, dbase, (uint32_t) (kJoinWaves * FS), nSd, test);
+#endif
                 stamp(4);
                 probe_end();
                 done = true;
             }
+        } else {
+        uint32_t rv[FR][FW], rn[FR], sv[FS][FSW], sn[FS], spk = 0;  // spk bit r: survivor run r packed
+#pragma unroll
+        for (int r = 0; r < FR; r++) {
+            const uint32_t dd = wave + r * kJoinWaves;
+            rn[r]             = dd < nRd ? rcnt[dd] : 0u;
+#ifdef HWBRJ_ABL_JNOR
+            rn[r] = 0;  // dev ablation (results invalid)
+#endif
+            const uint64_t bb = dd < nRd ? rbase[dd] : 0ull;
+#pragma unroll
+            for (int j = 0; j < FW; j++) {
+                const uint32_t o = lane + 64u * j;
+                rv[r][j]         = o < rn[r] ? ldv(SideR{}, bb, o) : 0u;
+            }
         }
-        // the general path: descriptors in LDS batches (jobs with more runs than the lanes hold,
-        // duplicate R keys, the hash and histogram joins)
-        auto probe_survivors = [&](auto&& op) {
+#pragma unroll
+        for (int r = 0; r < FS; r++) {
+            const uint32_t dd = wave + r * kJoinWaves;
+            sn[r]             = dd < nSd ? dcnt[dd] : 0u;
+#ifdef HWBRJ_ABL_JNOS
+            sn[r] = 0;  // dev ablation (results invalid)
+#endif
+            const uint64_t bb = dd < nSd ? dbase[dd] : 0ull;
+            spk |= (uint32_t) (bb >> 63) << r;
+#pragma unroll
+            for (int j = 0; j < FSW; j++) {
+                const uint32_t o = lane + 64u * j;
+                sv[r][j]         = o < sn[r] ? ldv(SideS{}, bb, o) : 0u;
+            }
+        }
+        // bits set without returns (no wave waits on them); a duplicate R key shows as fewer set
+        // bits than the job's R keys (popcount after the barrier)
+        auto set = [&](uint32_t x) { __hip_atomic_fetch_or(&tab[x >> 5], 1u << (x & 31u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); };
+#pragma unroll
+        for (int r = 0; r < FR; r++) {
+#pragma unroll
+            for (int j = 0; j < FW; j++)
+                if (lane + 64u * j < rn[r]) set(key(SideR{}, rv[r][j], rpk));
+            if (rn[r] > 64u * FW) {  // (rare) longer run
+                const uint64_t bb = rbase[wave + r * kJoinWaves];
+                tail_run(SideR{}, bb, 64u * FW, rn[r], set);
+            }
+        }
+        // the next F2 survivor runs per wave, into the registers the R runs leave: they arrive
+        // during the popcount and the first runs' tests instead of one walk round later
+        constexpr int F2 = HWBRJ_JS2 > 0 ? HWBRJ_JS2 : 1;
+        uint32_t      s2v[F2][FSW], s2n[F2], s2pk = 0;
+        if (HWBRJ_JS2 > 0) {
+#pragma unroll
+            for (int r = 0; r < F2; r++) {
+                const uint32_t dd = wave + (FS + r) * kJoinWaves;
+                s2n[r]            = dd < nSd ? dcnt[dd] : 0u;
+#ifdef HWBRJ_ABL_JNOS
+                s2n[r] = 0;  // dev ablation (results invalid)
+#endif
+                const uint64_t bb = dd < nSd ? dbase[dd] : 0ull;
+                s2pk |= (uint32_t) (bb >> 63) << r;
+#pragma unroll
+                for (int j = 0; j < FSW; j++) {
+                    const uint32_t o = lane + 64u * j;
+                    s2v[r][j]        = o < s2n[r] ? ldv(SideS{}, bb, o) : 0u;
+                }
+            }
+        }
+        __syncthreads();
+        stamp(1);
+        {
+            uint32_t pc = 0;
+            for (uint32_t i = tid; i < kJoinWords / 4; i += kJoinThreads) {
+                const uint4 v = ((const uint4*) tab)[i];
+                pc += __builtin_popcount(v.x) + __builtin_popcount(v.y) + __builtin_popcount(v.z) + __builtin_popcount(v.w);
+            }
+            pc = __builtin_amdgcn_readlane(wave_incl_scan_dpp(pc), 63);
+            if (lane == 0 && pc) atomicAdd(&dupflag, pc);  // (dupflag: the set bits)
+        }
+        __syncthreads();
+        hashed = dupflag != npieces;  // uniform
+        stamp(2);
+        if (!hashed) {
             probe_begin();
-            for (uint32_t d0 = i0; d0 < i1; d0 += kJoinDesc) {
-                const uint32_t nd = min(kJoinDesc, i1 - d0);
-                __syncthreads();  // previous descriptors consumed
-                if ((uint32_t) tid < nd) {
-                    const uint32_t it = d0 + tid;
-                    dcnt[tid]         = P.surv_cnt[(uint64_t) it * NSUB + s];
-                    dbase[tid]        = stag(item_e0(J, it), P.surv_off[(uint64_t) it * NSUB + s]);
+            auto test = [&](uint32_t x) { cnt += (tab[x >> 5] >> (x & 31u)) & 1u; };
+#pragma unroll
+            for (int r = 0; r < FS; r++) {
+#pragma unroll
+                for (int j = 0; j < FSW; j++)
+                    if (lane + 64u * j < sn[r]) test(key(SideS{}, sv[r][j], (spk >> r) & 1u));
+                if (sn[r] > 64u * FSW) {
+                    const uint64_t bb = dbase[wave + r * kJoinWaves];
+                    tail_run(SideS{}, bb, 64u * FSW, sn[r], test);
                 }
-                __syncthreads();
-                walk(SR{}, SW{}, SideS{}, dcnt, dbase, 0, nd, op);
             }
+            if (HWBRJ_JS2 > 0) {
+#pragma unroll
+                for (int r = 0; r < F2; r++) {
+#pragma unroll
+                    for (int j = 0; j < FSW; j++)
+                        if (lane + 64u * j < s2n[r]) test(key(SideS{}, s2v[r][j], (s2pk >> r) & 1u));
+                    if (s2n[r] > 64u * FSW) {
+                        const uint64_t bb = dbase[wave + (FS + r) * kJoinWaves];
+                        tail_run(SideS{}, bb, 64u * FSW, s2n[r], test);
+                    }
+                }
+            }
+            stamp(3);
+#ifndef HWBRJ_ABL_JNOS
+            walk(SR{}, SW{}, SideS{}, dcnt, dbase, (uint32_t) (kJoinWaves * (FS + (HWBRJ_JS2 > 0 ? F2 : 0))), nSd, test);
+#endif
+            stamp(4);
             probe_end();
-        };
-        auto load_r = [&](uint32_t d0, uint32_t nd) {  // R run descriptors of a batch
-            __syncthreads();  // previous R descriptors consumed
-            if ((uint32_t) tid < nd) {
-                const uint64_t r = (uint64_t) (d0 + tid) * NSUB + s;
-                rcnt[tid]        = P.r_cnt[r];
-                rbase[tid]       = rtag(d0 + tid, P.r_off[r]);
-            }
-            __syncthreads();
-        };
-        if (!hashed && !done) {  // every R key sets bit v; a bit already set means a duplicate key
-            __syncthreads();
-            for (uint32_t i = tid; i < kJoinWords / 4; i += kJoinThreads) ((uint4*) tab)[i] = make_uint4(0, 0, 0, 0);
-            if (tid == 0) dupflag = 0;
-            uint32_t dup = 0;
-            for (uint32_t d0 = w0; d0 < w1; d0 += kJoinDesc) {
-                const uint32_t nd = min(kJoinDesc, w1 - d0);
-                load_r(d0, nd);
-                walk(RR{}, RW{}, SideR{}, rcnt, rbase, 0, nd, [&](uint32_t x) {
-                    const uint32_t bit = 1u << (x & 31u);
-                    dup |= atomicOr(&tab[x >> 5], bit) & bit;
-                });
-            }
-            if (dup) dupflag = 1;
-            __syncthreads();
-            hashed = dupflag != 0;  // uniform
-            if (!hashed) probe_survivors([&](uint32_t x) { cnt += (tab[x >> 5] >> (x & 31u)) & 1u; });
+            done = true;
         }
-        if (hashed) {  // duplicate R keys (or keys too wide for the bitmap): counting hash table over
-                       // pieces of consecutive R runs holding <= kJoinPiece keys (a run has <= slot)
-            for (uint32_t d0 = w0; d0 < w1; d0 += kJoinDesc) {
-                const uint32_t nd = min(kJoinDesc, w1 - d0);
-                load_r(d0, nd);
-                if (tid == 0) {
-                    uint32_t np = 0, acc = 0;
-                    pend[0] = 0;
-                    for (uint32_t d = 0; d < nd; d++) {
-                        if (acc + rcnt[d] > kJoinPiece && acc > 0) {
-                            pend[++np] = d;
-                            acc        = 0;
-                        }
-                        acc += rcnt[d];
+        }  // (the unpacked or mixed fused path)
+    }
+    if (!hashed && !done) {  // every R key sets bit v; a bit already set means a duplicate key
+        for (uint32_t i = tid; i < kJoinWords / 4; i += kJoinThreads) ((uint4*) tab)[i] = make_uint4(0, 0, 0, 0);
+        if (tid == 0) dupflag = 0;
+        uint32_t dup = 0;
+        for (uint32_t d0 = w0; d0 < w1; d0 += kJoinDesc) {
+            const uint32_t nd = min(kJoinDesc, w1 - d0);
+            load_r(d0, nd);
+            walk(RR{}, RW{}, SideR{}, rcnt, rbase, 0, nd, [&](uint32_t x) {
+                const uint32_t bit = 1u << (x & 31u);
+                dup |= atomicOr(&tab[x >> 5], bit) & bit;
+            });
+        }
+        if (dup) dupflag = 1;
+        __syncthreads();
+        hashed = dupflag != 0;  // uniform
+        if (!hashed) probe_survivors([&](uint32_t x) { cnt += (tab[x >> 5] >> (x & 31u)) & 1u; });
+    }
+    if (hashed) {  // duplicate R keys (or keys too wide for the bitmap): counting hash table over
+                   // pieces of consecutive R runs holding <= kJoinPiece keys (a run has <= slot)
+        for (uint32_t d0 = w0; d0 < w1; d0 += kJoinDesc) {
+            const uint32_t nd = min(kJoinDesc, w1 - d0);
+            load_r(d0, nd);
+            if (tid == 0) {
+                uint32_t np = 0, acc = 0;
+                pend[0] = 0;
+                for (uint32_t d = 0; d < nd; d++) {
+                    if (acc + rcnt[d] > kJoinPiece && acc > 0) {
+                        pend[++np] = d;
+                        acc        = 0;
                     }
-                    pend[++np] = nd;
-                    npieces    = np;
+                    acc += rcnt[d];
+                }
+                pend[++np] = nd;
+                npieces    = np;
+            }
+            __syncthreads();
+            const uint32_t np = npieces;
+            for (uint32_t pc = 0; pc < np; pc++) {
+                const uint32_t da = pend[pc], db = pend[pc + 1];
+                __syncthreads();
+                if (P.jkind == 0) {  // counting hash table (bucket_chaining_join's role)
+                    for (uint32_t i = tid; i < kJoinT / 4; i += kJoinThreads)
+                        ((uint4*) tab)[i] = make_uint4(kEmpty, kEmpty, kEmpty, kEmpty);
+                    __syncthreads();
+                    walk(RR{}, RW{}, SideR{}, rcnt, rbase, da, db, [&](uint32_t x) { join_insert(tab, x); });
+                    probe_survivors([&](uint32_t x) { cnt += join_count(tab, x); });  // (starts with a barrier)
+                    continue;
+                }
+                // Histogram join of Kim et al. (histogram_join / histogram_optimized_join,
+                // src/parallel_radix_join_bloom.c:350-419, :441-555): a histogram of the piece's R
+                // keys over NH = max(4, next_pow2(n) / 4) buckets, its prefix sum, the keys
+                // reordered by bucket (keys = tab[0, kJoinPiece), hist = tab[kJoinPiece, +NH + 2));
+                // every survivor compares the keys of its bucket -- one by one (PRH), or 4 per
+                // 16-byte LDS read (PRHO, the reference's SIMD compare).
+                uint32_t n = 0;
+                for (uint32_t d = da; d < db; d++) n += rcnt[d];
+                uint32_t NH = 4;
+                while (NH * 4 < n) NH <<= 1;
+                uint32_t* keys = tab;
+                uint32_t* hist = tab + kJoinPiece;
+                for (uint32_t i = tid; i < NH + 2; i += kJoinThreads) hist[i] = 0;
+                __syncthreads();
+                walk(RR{}, RW{}, SideR{}, rcnt, rbase, da, db, [&](uint32_t x) { atomicAdd(&hist[(x & (NH - 1u)) + 2], 1u); });
+                __syncthreads();
+                if (wave == 0) {  // inclusive prefix sum of hist[2, NH + 2): 16 buckets per lane
+                    const uint32_t per = (NH + 63) / 64, b0 = 2 + lane * per;
+                    uint32_t       loc = 0;
+                    for (uint32_t i = 0; i < per; i++)
+                        if (b0 + i < NH + 2) loc += hist[b0 + i];
+                    uint32_t run = wave_incl_scan(loc) - loc;
+                    for (uint32_t i = 0; i < per; i++)
+                        if (b0 + i < NH + 2) {
+                            run += hist[b0 + i];
+                            hist[b0 + i] = run;
+                        }
                 }
                 __syncthreads();
-                const uint32_t np = npieces;
-                for (uint32_t pc = 0; pc < np; pc++) {
-                    const uint32_t da = pend[pc], db = pend[pc + 1];
-                    __syncthreads();
-                    if (P.jkind == 0) {  // counting hash table (bucket_chaining_join's role)
-                        for (uint32_t i = tid; i < kJoinT / 4; i += kJoinThreads)
-                            ((uint4*) tab)[i] = make_uint4(kEmpty, kEmpty, kEmpty, kEmpty);
-                        __syncthreads();
-                        walk(RR{}, RW{}, SideR{}, rcnt, rbase, da, db, [&](uint32_t x) { join_insert(tab, x); });
-                        probe_survivors([&](uint32_t x) { cnt += join_count(tab, x); });  // (starts with a barrier)
-                        continue;
-                    }
-                    // Histogram join of Kim et al. (histogram_join / histogram_optimized_join,
-                    // src/parallel_radix_join_bloom.c:350-419, :441-555): a histogram of the piece's R
-                    // keys over NH = max(4, next_pow2(n) / 4) buckets, its prefix sum, the keys
-                    // reordered by bucket (keys = tab[0, kJoinPiece), hist = tab[kJoinPiece, +NH + 2));
-                    // every survivor compares the keys of its bucket -- one by one (PRH), or 4 per
-                    // 16-byte LDS read (PRHO, the reference's SIMD compare).
-                    uint32_t n = 0;
-                    for (uint32_t d = da; d < db; d++) n += rcnt[d];
-                    uint32_t NH = 4;
-                    while (NH * 4 < n) NH <<= 1;
-                    uint32_t* keys = tab;
-                    uint32_t* hist = tab + kJoinPiece;
-                    for (uint32_t i = tid; i < NH + 2; i += kJoinThreads) hist[i] = 0;
-                    __syncthreads();
-                    walk(RR{}, RW{}, SideR{}, rcnt, rbase, da, db, [&](uint32_t x) { atomicAdd(&hist[(x & (NH - 1u)) + 2], 1u); });
-                    __syncthreads();
-                    if (wave == 0) {  // inclusive prefix sum of hist[2, NH + 2): 16 buckets per lane
-                        const uint32_t per = (NH + 63) / 64, b0 = 2 + lane * per;
-                        uint32_t       loc = 0;
-                        for (uint32_t i = 0; i < per; i++)
-                            if (b0 + i < NH + 2) loc += hist[b0 + i];
-                        uint32_t run = wave_incl_scan(loc) - loc;
-                        for (uint32_t i = 0; i < per; i++)
-                            if (b0 + i < NH + 2) {
-                                run += hist[b0 + i];
-                                hist[b0 + i] = run;
-                            }
-                    }
-                    __syncthreads();
-                    walk(RR{}, RW{}, SideR{}, rcnt, rbase, da, db, [&](uint32_t x) {
-                        keys[atomicAdd(&hist[(x & (NH - 1u)) + 1], 1u)] = x;  // bucket b: [hist[b], hist[b + 1])
+                walk(RR{}, RW{}, SideR{}, rcnt, rbase, da, db, [&](uint32_t x) {
+                    keys[atomicAdd(&hist[(x & (NH - 1u)) + 1], 1u)] = x;  // bucket b: [hist[b], hist[b + 1])
+                });
+                if (P.jkind == 1) {
+                    probe_survivors([&](uint32_t x) {
+                        const uint32_t b = x & (NH - 1u);
+                        for (uint32_t j = hist[b], e = hist[b + 1]; j < e; j++) cnt += keys[j] == x;
                     });
-                    if (P.jkind == 1) {
-                        probe_survivors([&](uint32_t x) {
-                            const uint32_t b = x & (NH - 1u);
-                            for (uint32_t j = hist[b], e = hist[b + 1]; j < e; j++) cnt += keys[j] == x;
-                        });
-                    } else {
-                        probe_survivors([&](uint32_t x) {
-                            const uint32_t b = x & (NH - 1u), j0 = hist[b], e = hist[b + 1];
-                            for (uint32_t j = j0 & ~3u; j < e; j += 4) {
-                                const uint4 k = *(const uint4*) &keys[j];
-                                cnt += (k.x == x && j >= j0) + (k.y == x && j + 1 >= j0 && j + 1 < e) +
-                                       (k.z == x && j + 2 >= j0 && j + 2 < e) + (k.w == x && j + 3 < e);
-                            }
-                        });
-                    }
+                } else {
+                    probe_survivors([&](uint32_t x) {
+                        const uint32_t b = x & (NH - 1u), j0 = hist[b], e = hist[b + 1];
+                        for (uint32_t j = j0 & ~3u; j < e; j += 4) {
+                            const uint4 k = *(const uint4*) &keys[j];
+                            cnt += (k.x == x && j >= j0) + (k.y == x && j + 1 >= j0 && j + 1 < e) +
+                                   (k.z == x && j + 2 >= j0 && j + 2 < e) + (k.w == x && j + 3 < e);
+                        }
+                    });
                 }
             }
         }
     }
+    cnt_acc += cnt;
+    tp_acc += t_probe;
+    stamp(5);
 #ifdef HWBRJ_STAMPS
     if (P.dbg && tid == 0)
         for (int k = 0; k < 6; k++) atomicAdd((unsigned long long*) &P.dbg[(blk & 1023u) * 8 + k], (unsigned long long) tph[k]);
 #endif
 }
 
-// The join: one workgroup per work item. Survivor runs have one format unless some probe item
-// overflowed its stage (P.fmt_cnt, read once: MIXED, rare, since the Engine stops packing after a
-// join that had such items). A workgroup adds its count to partial sum blk % kJoinSumSlots (each in
-// its own 128-byte line) and takes a ticket of that slot (word 3); the slot's last workgroup adds
-// the slot into the result. k_join_split zeroes the slots.
-__global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
-    __shared__ JoinLds L;
-    const uint64_t t_start = P.timing ? wall_clock64() : 0;
-    uint64_t       cnt = 0, t_probe = 0;
-    if (P.r_pack3 && P.fmt_cnt && *P.fmt_cnt)
-        join_one<true>(P, L, cnt, t_probe);
-    else
-        join_one<false>(P, L, cnt, t_probe);
+// The uniform-format join (every launch without unstaged probe items, the north star's) and the
+// mixed one; both are launched, the one whose case this is not returns at once. The mixed one runs
+// on a small grid of persistent workgroups (an empty launch of it costs ~1 us, a full grid ~14 us);
+// it is rare: the Engine stops packing after a join that had unstaged items (pack3_hint_).
+#ifndef HWBRJ_JWPE
+#define HWBRJ_JWPE 0  // waves per SIMD the join is compiled for (0: the compiler's choice; dev A/B)
+#endif
+#if HWBRJ_JWPE
+#define HWBRJ_JOIN_ATTR __attribute__((amdgpu_waves_per_eu(HWBRJ_JWPE)))
+#else
+#define HWBRJ_JOIN_ATTR
+#endif
+// The end of a join workgroup: its matches go to partial sum blk % kJoinSumSlots (each in its own
+// 128-byte line, so the adds are not serialised on one address; with P.timing also its probe and
+// total ticks). No kernel sums the slots: the host reads them with the other counts when it waits
+// for the join (Engine::wait). (Summing them on the device was measured: a last-workgroup ticket
+// per slot costs as much as the launch it saves, and with a __threadfence() -- an agent-scope
+// release, which writes the XCD's L2 back -- the join took 0.84 instead of 0.29 ms.)
+__device__ __forceinline__ void join_finish(const JoinParams& P, uint64_t cnt, uint64_t t_probe, uint64_t t_start) {
+    __shared__ uint64_t wsum[kJoinWaves];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     cnt = wave_sum_u64(cnt);
-    __syncthreads();  // (a workgroup that returned early from join_one meets the others here)
-    if (lane == 0) L.wsum[wave] = cnt;
+    __syncthreads();  // (the previous job's LDS reads are done)
+    if (lane == 0) wsum[wave] = cnt;
     __syncthreads();
     if (tid != 0) return;
     uint64_t t = 0;
-    for (int v = 0; v < kJoinWaves; v++) t += L.wsum[v];
-    const uint32_t i    = blockIdx.x % kJoinSumSlots;
-    uint64_t*      slot = &P.jsum[i * kJoinSumStride];
+    for (int w = 0; w < kJoinWaves; w++) t += wsum[w];
+    uint64_t* slot = &P.jsum[(blockIdx.x % kJoinSumSlots) * kJoinSumStride];
     if (t) atomicAdd((unsigned long long*) slot, (unsigned long long) t);
     if (P.timing) {
-        atomicAdd((unsigned long long*) (slot + 1), (unsigned long long) t_probe);
+        if (t_probe) atomicAdd((unsigned long long*) (slot + 1), (unsigned long long) t_probe);
         atomicAdd((unsigned long long*) (slot + 2), (unsigned long long) (wall_clock64() - t_start));
     }
-    __threadfence();
-    const uint32_t group = (gridDim.x - i + kJoinSumSlots - 1) / kJoinSumSlots;  // workgroups of slot i
-    if (atomicAdd((unsigned long long*) (slot + 3), 1ull) != group - 1u) return;
-    __threadfence();  // the slot's last workgroup: every add of its group is visible
-    const uint64_t v = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (v) atomicAdd((unsigned long long*) P.result, (unsigned long long) v);  // result[0] += matches
-    if (P.timing) {  // result[3], result[4] += probe / total ticks
-        atomicAdd((unsigned long long*) (P.result + 3),
-                  (unsigned long long) __hip_atomic_load(slot + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-        atomicAdd((unsigned long long*) (P.result + 4),
-                  (unsigned long long) __hip_atomic_load(slot + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
+__global__ __launch_bounds__(kJoinThreads) HWBRJ_JOIN_ATTR void k_join(JoinParams P) {
+    if (P.r_pack3 && P.fmt_cnt && *P.fmt_cnt) return;
+    const uint64_t t_start = P.timing ? wall_clock64() : 0;
+    uint64_t       cnt = 0, t_probe = 0;
+    join_job<false>(P, blockIdx.x, cnt, t_probe);
+    join_finish(P, cnt, t_probe, t_start);
+}
+
+__global__ __launch_bounds__(kJoinThreads) void k_join_mixed(JoinParams P) {
+    if (!(P.r_pack3 && P.fmt_cnt && *P.fmt_cnt)) return;
+    const uint64_t t_start = P.timing ? wall_clock64() : 0;
+    uint64_t       cnt = 0, t_probe = 0;
+    for (uint32_t b = blockIdx.x; b < P.jobs + kJoinExtra; b += gridDim.x) {
+        __syncthreads();  // the previous job's LDS reads are done
+        join_job<true>(P, b, cnt, t_probe);
     }
+    join_finish(P, cnt, t_probe, t_start);
 }
 
 // ============================================================ K10m: the materializing join
@@ -4070,9 +4125,13 @@ void launch_join(const JoinParams& p0, uint32_t jobs, uint32_t* job_surv, hipStr
     k_join_split<<<(jobs + 255) / 256, 256, 0, st>>>(p.item_start, job_surv, p.log2NSUB, jobs, split,
                                                      p.nparts, p.extra, p.nextra, p.jsum);
     k_join<<<jobs + kJoinExtra, kJoinThreads, 0, st>>>(p);
+    k_join_mixed<<<std::min<uint32_t>(jobs + kJoinExtra, 1024u), kJoinThreads, 0, st>>>(p);
 }
 
 uint32_t join_extra_tasks() { return kJoinExtra; }
+uint32_t join_sum_slots() { return kJoinSumSlots; }
+uint32_t join_sum_stride() { return kJoinSumStride; }
+uint32_t join_bitmap_log2() { return kJoinBmLog2; }
 
 void launch_export(const uint32_t* slices, const Geometry& g, uint32_t* out, uint64_t nwords,
                    hipStream_t st) {
@@ -4122,8 +4181,10 @@ const char* kernel_build_knobs() {
         num("HWBRJ_JSW", HWBRJ_JSW, 2);
         num("HWBRJ_JFR", HWBRJ_JFR, 8);
         num("HWBRJ_JFW", HWBRJ_JFW, 5);
-        num("HWBRJ_JFS2", HWBRJ_JFS2, 16);
-        num("HWBRJ_JS2E", HWBRJ_JS2E, 0);
+        num("HWBRJ_JS2", HWBRJ_JS2, 0);
+        num("HWBRJ_JG12", HWBRJ_JG12, 0);
+        num("HWBRJ_JBM", HWBRJ_JBM, 18);
+        num("HWBRJ_JWPE", HWBRJ_JWPE, 0);
         num("HWBRJ_ABL_PROBE", HWBRJ_ABL_PROBE, 0);
         num("HWBRJ_PCO", HWBRJ_PCO, 1);
         num("HWBRJ_PCO_AUX", HWBRJ_PCO_AUX, 0);

@@ -723,8 +723,7 @@ int Engine::join_partitioned(const hwbrj_exchange_t* x, int rank, int world, con
     jp.CH              = CH;
     jp.log2NSUB        = g.log2NSUB;
     jp.hash_shift      = g.hash_shift;
-    jp.bitmap          = (g.sub_shift > 0 && 32 - g.hash_shift <= 18) ? 1u : 0u;
-    jp.result          = d_result;
+    jp.bitmap          = (g.sub_shift > 0 && 32 - g.hash_shift <= join_bitmap_log2()) ? 1u : 0u;
     jp.jsum            = (uint64_t*) ((char*) small.p + 128);
     jp.nparts          = jparts.as<uint32_t>();
     jp.extra           = jtask.as<uint2>();
@@ -735,9 +734,8 @@ int Engine::join_partitioned(const hwbrj_exchange_t* x, int rank, int world, con
     launch_join(jp, NJ, pjJobs.as<uint32_t>(), stream);
     PJ_STAGE("k_join");
     PJ_CHECK(hipGetLastError());
-    uint64_t small_h[5] = {0, 0, 0, 0, 0};
-    PJ_CHECK(hipMemcpyAsync(small_h, d_result, sizeof small_h, hipMemcpyDeviceToHost, stream));
-    PJ_CHECK(hipStreamSynchronize(stream));
+    uint64_t small_h[6] = {0, 0, 0, 0, 0, 0};
+    if (const int rc = read_join_counts(d_result, true, stream, small_h)) return rc;
     lap(6);
     pending_ = false;
     have_filter_ = false;  // (the slices live in the caller's exchange buffer)
