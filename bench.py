@@ -61,6 +61,9 @@ def parse():
                     help="--design partitioned: the library's own RCCL communicator (collectives on "
                          "the join stream), or torch.distributed callbacks (the only choice when "
                          "ranks share a GPU)")
+    ap.add_argument("--pj-sync", action="store_true",
+                    help="--design partitioned, native: the synchronous join (host waits on its two "
+                         "counts messages) instead of the async one (padded exchanges, joins back to back)")
     ap.add_argument("--filter-bcast", action="store_true",
                     help="replicated design: rank 0 builds the filter, ncclBroadcast sends it to "
                          "every rank (the north_star's bitmap broadcast) instead of a rebuild per rank")
@@ -351,6 +354,21 @@ def main():
         dist.destroy_process_group()
 
 
+def pj_async_steps(pjoin, dR, dS, nR, args, K, depth=8):
+    """K async partitioned joins (hwbrj_join_partitioned_rccl_async) back to back, at most `depth`
+    in flight: no host wait but the collection of the oldest. Their stats, in order."""
+    out, inflight = [], 0
+    for _ in range(K):
+        if inflight == depth:
+            out.append(pjoin.join_partitioned_wait())
+            inflight -= 1
+        pjoin.join_partitioned_rccl_async(dR, dS, nR, args)
+        inflight += 1
+    for _ in range(inflight):
+        out.append(pjoin.join_partitioned_wait())
+    return out
+
+
 def alt_designs(a, hw, torch, dist, rank, world, local, dR, dS, args, shared):
     """The designs the headline does not run, timed on the same ranks and shards right after it, so
     one multi-GPU run decides between them:
@@ -360,7 +378,10 @@ def alt_designs(a, hw, torch, dist, rank, world, local, dR, dS, args, shared):
       partitioned  R range-sharded too, partitions owned by ranks: the R chunk and survivor
                    all-to-alls and the slice all-gather (hwbrj_join_partitioned_rccl; the torch
                    callback transport when ranks share a GPU); host-synchronous, so timed by wall
-                   clock between barriers, max over ranks.
+                   clock between barriers, max over ranks;
+      partitioned_async  the same join with padded exchanges and no host wait
+                   (hwbrj_join_partitioned_rccl_async; one GPU per rank): K joins back to back,
+                   wall clock between barriers, max over ranks.
     Each leg reports its ms per join, the probe-tuples/s that gives, and every rank's own
     (filtered, matches), whose sums must be the headline's counts. A failing leg is reported, and
     never stops the headline line."""
@@ -439,12 +460,31 @@ def alt_designs(a, hw, torch, dist, rank, world, local, dR, dS, args, shared):
         dist.barrier()
         return slowest((time.perf_counter() - t0) / K * 1e3), per, tot
 
+    def partitioned_async():
+        rlo, rhi = hw.shard_range(nR, rank, world)
+        dRs = dR[rlo:rhi]
+        sts = pj_async_steps(pjoin, dRs, dS, nR, args, 2)  # (the plan join, then one async)
+        per, tot = gather_counts(sts[-1])
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        sts = pj_async_steps(pjoin, dRs, dS, nR, args, K)
+        torch.cuda.synchronize()
+        dist.barrier()
+        if any((s.filtered, s.matches) != (sts[0].filtered, sts[0].matches) for s in sts):
+            raise RuntimeError("async partitioned joins disagree")
+        return slowest((time.perf_counter() - t0) / K * 1e3), per, tot
+
     if native and slice_filter:
         leg("bcast", bcast)
     else:
         out["bcast"] = {"skipped": "needs one GPU per rank (RCCL) and a slice filter"}
     if args is None or slice_filter:
         leg("partitioned", partitioned)
+        if native:
+            leg("partitioned_async", partitioned_async)
+        else:
+            out["partitioned_async"] = {"skipped": "needs one GPU per rank (RCCL)"}
     else:
         out["partitioned"] = {"skipped": "basic k > 1 has no partition slices"}
     if native:
@@ -459,6 +499,7 @@ def run_partitioned(a, hw, torch, dist, rank, world, local, dR, dS, args, shared
     from hwbloomradixjoin_amd import pjoin
     nR, nS_total = a.r_size, a.s_size
     native = a.transport == "native" and not shared
+    use_async = native and not a.pj_sync
     if native:  # the library's own RCCL communicator, collectives on the join stream
         pjoin.comm_init()
 
@@ -471,27 +512,51 @@ def run_partitioned(a, hw, torch, dist, rank, world, local, dR, dS, args, shared
         def join():
             return pjoin.join_partitioned(dR, dS, nR, args, x)
     cdev = "cpu" if shared else "cuda"
-    st = join()
+    if use_async:  # (the first async join runs synchronously and makes the exchange plan)
+        st = pj_async_steps(pjoin, dR, dS, nR, args, 1)[0]
+    else:
+        st = join()
     counts = torch.tensor([st.filtered, st.matches], dtype=torch.int64, device=cdev)
     if dist:
         dist.all_reduce(counts)
     filtered, matches = (int(v) for v in counts.tolist())
-    for _ in range(a.warmup):
-        join()
+    if use_async:
+        pj_async_steps(pjoin, dR, dS, nR, args, a.warmup)
+    else:
+        for _ in range(a.warmup):
+            join()
+    info0 = pjoin.pj_async_info() if use_async else None
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     sums = {}
-    for _ in range(a.steps):
-        st = join()
-        for f in ("ms_total", "ms_r_scatter", "ms_r_index", "ms_build", "ms_s_scatter", "ms_surv",
-                  "ms_join"):
-            sums[f] = sums.get(f, 0.0) + getattr(st, f)
+    if use_async:  # K joins enqueued back to back (<= 8 in flight), no host wait between them
+        sts = pj_async_steps(pjoin, dR, dS, nR, args, a.steps)
+        sums["ms_total"] = sum(s.ms_total for s in sts)
+        same = all((s.filtered, s.matches) == (sts[0].filtered, sts[0].matches) for s in sts)
+        same = same and (sts[0].filtered, sts[0].matches) == (st.filtered, st.matches)
+    else:
+        for _ in range(a.steps):
+            st = join()
+            for f in ("ms_total", "ms_r_scatter", "ms_r_index", "ms_build", "ms_s_scatter", "ms_surv",
+                      "ms_join"):
+                sums[f] = sums.get(f, 0.0) + getattr(st, f)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    if use_async:
+        info1 = pjoin.pj_async_info()
+        async_rep = {"plan_blocks": {"BR_chunks": info1["BR"], "BI_items": info1["BI"], "BW_words": info1["BW"]},
+                     "reruns_in_timed": info1["overflow_reruns"] - info0["overflow_reruns"],
+                     "async_in_timed": info1["async_joins"] - info0["async_joins"],
+                     "events_ms_per_join_rank0": round(sums["ms_total"] / max(a.steps, 1), 4),
+                     "rank0_counts_all_equal": bool(same),
+                     "timing": "wall clock over K joins enqueued back to back; events: each join's "
+                               "first to last operation on the join stream (HIP events)"}
+    else:
+        async_rep = None
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -520,7 +585,9 @@ def run_partitioned(a, hw, torch, dist, rank, world, local, dR, dS, args, shared
                    "B": a.bloom_block_size,
                    "parallelism": f"R and S range-sharded x{world}, partitions owned by ranks "
                                   "(R + survivor all-to-all, slice all-gather)",
-                   "transport": "native RCCL (join stream)" if native else "torch.distributed callbacks"},
+                   "transport": ("native RCCL (join stream), async: padded exchanges" if use_async else
+                                 "native RCCL (join stream), synchronous" if native else
+                                 "torch.distributed callbacks")},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS * world,
                      "unit": "GB/s", "frac": round(achieved / (HBM_PEAK_GBS * world), 4),
                      "traffic": None, "algorithmic_bytes": alg_bytes,
@@ -532,6 +599,7 @@ def run_partitioned(a, hw, torch, dist, rank, world, local, dR, dS, args, shared
         "dist": {"world_size_seen": dist.get_world_size() if dist else 1,
                  "backend": dist.get_backend() if dist else None, "shared_gpu_rehearsal": shared},
         "stage_ms_rank0": {k[3:]: round(v / K, 4) for k, v in sums.items()},
+        "pj_async": async_rep,
     }
     print(json.dumps(out), flush=True)
     if native:

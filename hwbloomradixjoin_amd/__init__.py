@@ -265,8 +265,10 @@ def _take_result(r) -> Result:
     return out
 
 
-HOOK_JOIN_SPLIT, HOOK_PJ_FAIL_RANK, HOOK_BCAST_NONROOT = 1, 2, 3  # include/hwbrj.h hwbrj_set_test_hook
-_HOOK_OFF = {HOOK_JOIN_SPLIT: 0, HOOK_PJ_FAIL_RANK: -1, HOOK_BCAST_NONROOT: 0}
+# include/hwbrj.h hwbrj_set_test_hook
+HOOK_JOIN_SPLIT, HOOK_PJ_FAIL_RANK, HOOK_BCAST_NONROOT, HOOK_PJ_PLAN_DIV, HOOK_PJ_ASYNC_FAIL = 1, 2, 3, 4, 5
+_HOOK_OFF = {HOOK_JOIN_SPLIT: 0, HOOK_PJ_FAIL_RANK: -1, HOOK_BCAST_NONROOT: 0, HOOK_PJ_PLAN_DIV: 0,
+             HOOK_PJ_ASYNC_FAIL: 0}
 
 
 def version() -> str:

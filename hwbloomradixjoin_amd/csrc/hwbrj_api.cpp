@@ -50,7 +50,9 @@ const char* hwbrj_version(void) {
     if (h.join_split) add("HWBRJ_HOOK_JOIN_SPLIT=" + std::to_string(h.join_split));
     if (h.pj_fail_rank >= 0) add("HWBRJ_HOOK_PJ_FAIL_RANK=" + std::to_string(h.pj_fail_rank));
     if (h.bcast_nonroot) add("HWBRJ_HOOK_BCAST_NONROOT=" + std::to_string(h.bcast_nonroot));
-    v = std::string("hwbloomradixjoin_amd 0.5 (gfx950) src " HWBRJ_SRC_SHA) + (k.empty() ? "" : " knobs: " + k);
+    if (h.pj_plan_div) add("HWBRJ_HOOK_PJ_PLAN_DIV=" + std::to_string(h.pj_plan_div));
+    if (h.pj_async_fail) add("HWBRJ_HOOK_PJ_ASYNC_FAIL=" + std::to_string(h.pj_async_fail));
+    v =std::string("hwbloomradixjoin_amd 0.5 (gfx950) src " HWBRJ_SRC_SHA) + (k.empty() ? "" : " knobs: " + k);
     return v.c_str();
 }
 
@@ -67,6 +69,14 @@ int hwbrj_set_test_hook(int hook, int64_t value) {
         case HWBRJ_HOOK_BCAST_NONROOT:
             if (value < 0 || value > 2) break;
             h.bcast_nonroot = (int) value;
+            return 0;
+        case HWBRJ_HOOK_PJ_PLAN_DIV:
+            if (value < 0 || value > 1000000) break;
+            h.pj_plan_div = (int) value;
+            return 0;
+        case HWBRJ_HOOK_PJ_ASYNC_FAIL:
+            if (value < 0 || value > 1) break;
+            h.pj_async_fail = (int) value;
             return 0;
         default:
             set_last_error("unknown test hook");

@@ -17,6 +17,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <mutex>
 #include <string>
 #include <type_traits>
@@ -42,6 +43,7 @@ struct Rccl {
     ncclResult_t (*Recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t)   = nullptr;
     ncclResult_t (*AllGather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
     ncclResult_t (*Broadcast)(const void*, void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*AllReduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t, hipStream_t) = nullptr;
     const char* (*GetErrorString)(ncclResult_t)                                         = nullptr;
 };
 
@@ -74,6 +76,7 @@ const Rccl& rccl() {
         sym(r.Recv, "ncclRecv");
         sym(r.AllGather, "ncclAllGather");
         sym(r.Broadcast, "ncclBroadcast");
+        sym(r.AllReduce, "ncclAllReduce");
         sym(r.GetErrorString, "ncclGetErrorString");
         r.ok = all;
     });
@@ -210,6 +213,16 @@ int rccl_alltoall_u64_dev(Engine* e, const uint64_t* d_send, uint64_t* d_recv, u
     return 0;
 }
 
+// In-place max over the ranks of n u64 in device memory, on the engine's stream (the async
+// partitioned join's overflow flag and exchange sizes; a no-op at world 1 but with HWBRJ_RCCL_SELF).
+int rccl_allreduce_max_u64(Engine* e, uint64_t* d, uint64_t n) {
+    if (e->comm_world() == 1 && !rccl_self()) return 0;
+    if (int rc = need_rccl()) return rc;
+    RC_CALL(rccl().AllReduce(d, d, n, ncclUint64, ncclMax, (ncclComm_t) e->comm(), e->stream()),
+            "ncclAllReduce (max)");
+    return 0;
+}
+
 int rccl_broadcast(void* comm, void* buf, size_t bytes, int root, hipStream_t stream) {
     if (int rc = need_rccl()) return rc;
     RC_CALL(rccl().Broadcast(buf, buf, bytes, ncclUint8, root, (ncclComm_t) comm, stream),
@@ -255,7 +268,7 @@ int Engine::comm_init(const uint8_t* unique_id, int world, int rank) {
         set_last_error("hipSetDevice failed");
         return 1;
     }
-    comm_destroy();
+    comm_destroy();  // (drops the async join's plan and joins in flight)
     ncclUniqueId id;
     static_assert(sizeof(id.internal) == NCCL_UNIQUE_ID_BYTES, "unique id size");
     memcpy(id.internal, unique_id, NCCL_UNIQUE_ID_BYTES);
@@ -266,7 +279,7 @@ int Engine::comm_init(const uint8_t* unique_id, int world, int rank) {
     comm_rank_  = rank;
     // the status agreement's words, allocated here: an agreement never allocates, so a
     // rank whose big allocations just failed still takes part in it
-    if (!agree_.ensure((size_t) world * 8)) {
+    if (!agree_.ensure(std::max<size_t>(64, (size_t) world * 8))) {
         (void) comm_destroy();
         set_last_error("hipMalloc failed (status agreement words)");
         return 4;
@@ -278,6 +291,8 @@ int Engine::comm_destroy() {
     if (!comm_) return 0;
     (void) hipSetDevice(device_);
     (void) hipStreamSynchronize(own_stream_);
+    pj_plan_ = PjPlan{};  // (the plan and the joins in flight belong to the communicator)
+    pj_q_.clear();
     const ncclResult_t e = rccl().CommDestroy((ncclComm_t) comm_);
     comm_       = nullptr;
     comm_world_ = 1;
@@ -291,13 +306,19 @@ int Engine::join_partitioned_rccl(const uint2* dR, uint64_t nR, uint64_t nR_tota
         set_last_error("no communicator on this device (hwbrj_comm_init)");
         return 32;
     }
+    if (const int rc = pj_drain()) return rc;  // (async joins in flight use the buffers it may grow)
+    const hwbrj_exchange_t x = native_exchange();
+    return join_partitioned(&x, comm_rank_, comm_world_, dR, nR, nR_total, dS, nS, args, st, true);
+}
+
+hwbrj_exchange_t Engine::native_exchange() {
     hwbrj_exchange_t x;
     x.ctx          = this;
     x.buffer       = nx_buffer;
     x.alltoall_u64 = nx_alltoall_u64;
     x.alltoallv    = nx_alltoallv;
     x.allgather    = nx_allgather;
-    return join_partitioned(&x, comm_rank_, comm_world_, dR, nR, nR_total, dS, nS, args, st, true);
+    return x;
 }
 
 }  // namespace hwbrj

@@ -311,6 +311,10 @@ Engine::Engine(int device) : device_(device) {
 Engine::~Engine() { release(); }
 
 void Engine::release() {
+    (void) pj_drain();
+    pj_q_.clear();                       // (joins in flight are dropped)
+    if (pj_plan_.valid) pj_lost_ = true;  // (the next async join runs in the failed mode: a new plan)
+    for (DevBuf* b : {&pjX, &pjRitems, &pjRing}) b->release();
     for (DevBuf* b : {&poolR, &metaR, &usedR, &wgqcR, &wgqeR, &wgqoR, &lstartR, &estartR, &istartR,
                       &listR, &poolS, &metaS, &usedS, &wgqcS, &wgqeS, &wgqoS, &lstartS, &estartS,
                       &istartS, &listS, &slices, &bitmap, &rjoin, &rrun, &surv, &survcnt, &survoff,

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <deque>
 #include <string>
 #include <vector>
 
@@ -89,6 +90,65 @@ class Engine {
     DevBuf*     xslot(int s) { return &xslot_[s]; }
     DevBuf*     xcnt() { return &xcnt_; }
     void*       comm() const { return comm_; }
+    // the library's own RCCL exchange (hwbrj_comm.cpp): collectives on this engine's stream
+    hwbrj_exchange_t native_exchange();
+
+    // ---- the async partitioned join (hwbrj_pjoin_async.cpp; include/hwbrj.h) ----
+    static constexpr int kPjDepth = 8;   // joins in flight (result ring slots)
+    static constexpr int kPjKey   = 10;  // words of a plan's shape key
+    int  join_partitioned_async(const uint2* dR, uint64_t nR, uint64_t nR_total, const uint2* dS,
+                                uint64_t nS, const bloom_filter_args_t* args);
+    int  join_partitioned_wait(hwbrj_stats_t* st);
+    void pj_async_info(uint64_t* out) const;
+    // end of a synchronous native join asked for a plan (pj_make_plan()): a collective
+    bool pj_make_plan() const { return pj_make_plan_; }
+    int  pj_plan_from_sync(int world, int rank, uint64_t nR, uint64_t nR_total, uint64_t nS,
+                           const bloom_filter_args_t* args, uint64_t mr, uint64_t mi, uint64_t mw);
+    // drains the joins in flight (before a synchronous join grows buffers they use)
+    int  pj_drain();
+
+  private:
+    struct PjGeom {
+        Geometry g{};
+        uint32_t F = 0, NSUB = 0, W = 0, QL = 0, q0 = 0, nseg = 1, CH = 0, G = 0, NC = 0, items_max = 0;
+        uint64_t BSW = 0, SLOT = 0, capR = 0, capS = 0, LS = 0;
+        bool     slice_mode = false;
+    };
+    struct PjPlan {
+        bool     valid = false;
+        uint64_t BR = 0, BI = 0, BW = 0;  // block bounds: R chunks, survivor items, survivor words
+        uint64_t key[kPjKey] = {};
+    };
+    struct PjIn {
+        const uint2*        dR = nullptr;
+        const uint2*        dS = nullptr;
+        uint64_t            nR = 0, nR_total = 0, nS = 0;
+        bool                has_args = false;
+        bloom_filter_args_t args{};
+    };
+    struct PjPending {
+        PjIn          in;
+        PjGeom        G;
+        bool          sync = false;  // ran synchronously at enqueue (made the plan): rc, st
+        bool          failed_mode = false;
+        int           rc   = 0;
+        int           slot = 0;
+        hwbrj_stats_t st{};
+    };
+    bool pj_geom(int world, int rank, uint64_t nR, uint64_t nR_total, uint64_t nS,
+                 const bloom_filter_args_t* args, PjGeom* G);
+    int  pj_async_alloc(const PjGeom& G, const PjPlan& p, bool all);
+    int  pj_establish_plan(const PjGeom& G, uint64_t mr, uint64_t mi, uint64_t mw, const uint64_t* key);
+    int  pj_sync_join(const PjIn& in, hwbrj_stats_t* st);
+    PjPlan                pj_plan_;
+    bloom_filter_args_t   pj_plan_args_{};
+    bool                  pj_make_plan_ = false;
+    bool                  pj_lost_      = false;  // the plan's buffers were released (this rank)
+    std::deque<PjPending> pj_q_;
+    uint64_t              pj_seq_ = 0, pj_async_ = 0, pj_sync_ = 0, pj_fallbacks_ = 0, pj_plans_ = 0;
+    uint64_t              pj_last_flag_ = 0, pj_last_sizes_[3] = {0, 0, 0};
+    DevBuf                pjX, pjRitems, pjRing;  // flag + sizes + counts messages; ritems; result ring
+    hipEvent_t            pjEv_[2 * kPjDepth] = {};
 
   private:
     void*        comm_       = nullptr;  // ncclComm_t of this device's rank (hwbrj_comm_init)
@@ -166,6 +226,9 @@ int read_join_counts(const void* small, bool slots, hipStream_t stream, uint64_t
 int rccl_agree_status(void* comm, int world, int rank, int rc, hipStream_t stream, DevBuf* tmp);
 class Engine;
 int rccl_alltoall_u64_dev(Engine* e, const uint64_t* d_send, uint64_t* d_recv, uint64_t n);
+int rccl_allreduce_max_u64(Engine* e, uint64_t* d, uint64_t n);
+// chunks of a shard's partition pool for n tuples over G scatter workgroups and F partitions
+uint64_t pj_region_cap(uint64_t n, uint32_t G, uint32_t F);
 
 // glibc's rand() (stdlib/random_r.c TYPE_3) with private state (hwbrj_gen.cpp).
 struct GlibcRand {

@@ -215,11 +215,29 @@ void   launch_pj_items(const uint32_t* item_start, const uint32_t* list_start, c
                        uint32_t items_max, uint32_t F, uint32_t nseg, uint32_t CH, uint64_t seg_words, uint32_t NSUB,
                        uint64_t* region, uint32_t* tot, uint64_t* bsum, uint64_t* sofs, uint64_t* bound,
                        hipStream_t st);
+// (BI > 0: the async join's padded blocks of BI items / BW words per source, ritems[j] valid items)
 void   launch_pj_recv_scan(const uint32_t* cnt, uint32_t n, uint32_t NSUB, uint32_t* tot, uint64_t* bsum,
-                           uint64_t* wscan, hipStream_t st);
+                           uint64_t* wscan, hipStream_t st, uint32_t BI = 0, const uint32_t* ritems = nullptr);
 void   launch_pj_item_tables(const uint32_t* tab, uint32_t pairs, uint32_t W, const uint32_t* rcnt,
                              const uint64_t* wscan, uint32_t NSUB, uint64_t* ibase, uint32_t* icnt, uint32_t* ioff,
-                             uint32_t* jobs, hipStream_t st);
+                             uint32_t* jobs, hipStream_t st, uint32_t BI = 0, uint64_t BW = 0);
+// the async partitioned join's fixed exchange blocks (hwbrj_pjoin_async.cpp; k_pjx_*): R chunks
+// gathered into blocks of BR per destination, the owner's R tables from the received counts, the
+// survivors packed into blocks of BI items / BW words, the owner's survivor tables, and the exchange
+// sizes of the join for the next plan ({flag, R block, item block, word block} maxima)
+void   launch_pjx_gather(const uint32_t* pool, const uint32_t* list, const uint32_t* lstart, uint32_t F, uint32_t QL,
+                         uint64_t BR, void* out, uint32_t* ent, uint64_t* flag, hipStream_t st);
+void   launch_pjx_rtab(const uint64_t* rc, uint32_t W, uint32_t QL, uint32_t NC, uint64_t BR, uint32_t bsw,
+                       int64_t* tab, uint32_t* lsO, uint32_t* swO, uint64_t* flag, hipStream_t st);
+void   launch_pjx_surv_pack(const uint32_t* surv, const uint64_t* region, const uint32_t* tot, const uint64_t* sofs,
+                            const uint32_t* item_start, const uint64_t* bound, const uint32_t* cnt, uint32_t F,
+                            uint32_t QL, uint32_t NSUB, uint64_t BI, uint64_t BW, uint32_t* out, uint32_t* out_cnt,
+                            uint64_t* flag, hipStream_t st);
+void   launch_pjx_stab(const uint64_t* rc, uint32_t W, uint32_t QL, uint32_t NC, uint64_t BI, uint64_t BW,
+                       uint32_t* tab2, uint32_t* istart, uint32_t* ritems, uint64_t* flag, hipStream_t st);
+void   launch_pjx_stat(const uint64_t* rc1, const uint64_t* rc2, const uint32_t* ls, const uint32_t* is,
+                       const uint64_t* bd, uint32_t W, uint32_t QL, uint32_t NC, const uint64_t* flag, uint64_t* out,
+                       hipStream_t st);
 void   launch_pj_gather(const uint32_t* pool, const uint32_t* list, uint32_t n, void* out, uint32_t* ent,
                         hipStream_t st);
 // the native transport's per-destination counts message (k_pj_counts), built on the device
@@ -265,6 +283,8 @@ struct TestHooks {
     uint32_t join_split    = 0;   // HWBRJ_HOOK_JOIN_SPLIT: survivors per join part (0: the default)
     int      pj_fail_rank  = -1;  // HWBRJ_HOOK_PJ_FAIL_RANK: this rank fails the shard check
     int      bcast_nonroot = 0;   // HWBRJ_HOOK_BCAST_NONROOT: the broadcast join as a non-root rank
+    int      pj_plan_div   = 0;   // HWBRJ_HOOK_PJ_PLAN_DIV: async plans' blocks divided by it (overflow)
+    int      pj_async_fail = 0;   // HWBRJ_HOOK_PJ_ASYNC_FAIL: async joins run in the failed mode
 };
 TestHooks& test_hooks();
 

@@ -3752,16 +3752,18 @@ __global__ __launch_bounds__(1024) void k_pj_items(const uint32_t* __restrict__ 
 }
 
 // Received items (it < n, in received order): survivor total over the NSUB counts, block totals.
+// (BI > 0: received items in blocks of BI per source, of which the first ritems[j] are valid; the
+// others -- the block's padding -- count 0)
 __global__ __launch_bounds__(1024) void k_pj_recv_tot(const uint32_t* __restrict__ cnt, uint32_t n,
                                                       uint32_t NSUB, uint32_t* __restrict__ tot,
-                                                      uint64_t* __restrict__ bsum) {
+                                                      uint64_t* __restrict__ bsum, uint32_t BI,
+                                                      const uint32_t* __restrict__ ritems) {
     __shared__ uint32_t wsum[16];
     const uint32_t it = blockIdx.x * kPjScanBlock + threadIdx.x;
     uint32_t       t  = 0;
-    if (it < n) {
+    if (it < n && (BI == 0 || it % BI < ritems[it / BI]))
         for (uint32_t s = 0; s < NSUB; s++) t += cnt[(uint64_t) it * NSUB + s];
-        tot[it] = t;
-    }
+    if (it < n) tot[it] = t;
     uint32_t total;
     (void) block_excl_scan(t, wsum, total);
     if (threadIdx.x == 0) bsum[blockIdx.x] = total;
@@ -3802,11 +3804,14 @@ __global__ void k_pj_bound(const uint32_t* __restrict__ item_start, uint32_t F,
 // item out of received item src: ibase = its first word in the received survivors (wscan[src]),
 // icnt / ioff its NSUB run counts and offsets; jobs[i][s] += the counts (every output order: items
 // of partition i from source 0, 1, ...).
+// (BI > 0: received survivors in blocks of BW words per source: ibase = the source block's base plus
+// the item's offset in it)
 __global__ __launch_bounds__(256) void k_pj_item_tables(const uint32_t* __restrict__ tab, uint32_t W,
                                                         const uint32_t* __restrict__ rcnt,
                                                         const uint64_t* __restrict__ wscan, uint32_t NSUB,
                                                         uint64_t* __restrict__ ibase, uint32_t* __restrict__ icnt,
-                                                        uint32_t* __restrict__ ioff, uint32_t* __restrict__ jobs) {
+                                                        uint32_t* __restrict__ ioff, uint32_t* __restrict__ jobs,
+                                                        uint32_t BI, uint64_t BW) {
     __shared__ uint32_t js[64];
     const uint32_t* t  = tab + 3 * (uint64_t) blockIdx.x;
     const uint32_t  i  = blockIdx.x / W;
@@ -3815,7 +3820,7 @@ __global__ __launch_bounds__(256) void k_pj_item_tables(const uint32_t* __restri
     __syncthreads();
     for (uint32_t k = threadIdx.x; k < n; k += blockDim.x) {
         const uint32_t src = s0 + k, out = o0 + k;
-        ibase[out] = wscan[src];
+        ibase[out] = BI ? (src / BI) * BW + (wscan[src] - wscan[(src / BI) * BI]) : wscan[src];
         uint32_t o = 0;
         for (uint32_t s = 0; s < NSUB; s++) {
             const uint32_t c = rcnt[(uint64_t) src * NSUB + s];
@@ -3840,17 +3845,18 @@ void launch_pj_items(const uint32_t* item_start, const uint32_t* list_start, con
 }
 
 void launch_pj_recv_scan(const uint32_t* cnt, uint32_t n, uint32_t NSUB, uint32_t* tot, uint64_t* bsum,
-                         uint64_t* wscan, hipStream_t st) {
+                         uint64_t* wscan, hipStream_t st, uint32_t BI, const uint32_t* ritems) {
     const uint32_t nb = (n + kPjScanBlock) / kPjScanBlock;
-    k_pj_recv_tot<<<nb, 1024, 0, st>>>(cnt, n, NSUB, tot, bsum);
+    k_pj_recv_tot<<<nb, 1024, 0, st>>>(cnt, n, NSUB, tot, bsum, BI, ritems);
     k_pj_scan<<<nb, 1024, 0, st>>>(tot, n, nullptr, bsum, wscan);
 }
 
 void launch_pj_item_tables(const uint32_t* tab, uint32_t pairs, uint32_t W, const uint32_t* rcnt,
                            const uint64_t* wscan, uint32_t NSUB, uint64_t* ibase, uint32_t* icnt, uint32_t* ioff,
-                           uint32_t* jobs, hipStream_t st) {
-    if (pairs) k_pj_item_tables<<<pairs, 256, 0, st>>>(tab, W, rcnt, wscan, NSUB, ibase, icnt, ioff, jobs);
+                           uint32_t* jobs, hipStream_t st, uint32_t BI, uint64_t BW) {
+    if (pairs) k_pj_item_tables<<<pairs, 256, 0, st>>>(tab, W, rcnt, wscan, NSUB, ibase, icnt, ioff, jobs, BI, BW);
 }
+
 
 // The native transport's counts message to every destination j (out[j NC .. (j + 1) NC)), packed on
 // the device so no host read precedes its exchange: the item (or chunk) counts of j's QL partitions
@@ -3889,6 +3895,219 @@ void launch_pj_relist(const uint32_t* rent, const int64_t* tab, uint32_t pairs, 
 void launch_pj_surv_pack(const uint32_t* surv, const uint64_t* region, const uint32_t* tot,
                          const uint64_t* soff, uint32_t n, uint32_t* out, hipStream_t st) {
     if (n) k_pj_surv_pack<<<2048, 256, 0, st>>>(surv, region, tot, soff, n, out);
+}
+
+// ---- the async partitioned join (hwbrj_join_partitioned_rccl_async): fixed exchange blocks
+// Every (source, destination) block of the three variable all-to-alls is padded to the plan's
+// bound (R chunks BR, survivor items BI, survivor words BW; agreed by all ranks, host-known), so the
+// RCCL calls need no host-read counts. What does not fit sets flag[0]; the ranks all-reduce it at
+// the end of the join and rerun it synchronously when it is set (Engine::pj_wait).
+constexpr uint32_t kPjOverflow = 1u, kPjPeerFailed = 2u;
+
+// R chunks in list order into destination j's block at j * BR (entries: their index in the block
+// plus the list entry's count bits). n = lstart[F] (on the device).
+__global__ __launch_bounds__(256) void k_pjx_gather(const uint32_t* __restrict__ pool, const uint32_t* __restrict__ list,
+                                                    const uint32_t* __restrict__ lstart, uint32_t F, uint32_t QL,
+                                                    uint64_t BR, uint4* __restrict__ out, uint32_t* __restrict__ ent,
+                                                    uint64_t* flag) {
+    const uint32_t n      = lstart[F];
+    const uint64_t stride = (uint64_t) gridDim.x * blockDim.x;
+    bool           over   = false;
+    for (uint64_t t = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x; t < (uint64_t) n * 8; t += stride) {
+        const uint32_t p = (uint32_t) (t >> 3), l8 = (uint32_t) (t & 7);
+        const uint32_t j = find_q(lstart, F, p) / QL;
+        const uint64_t k = p - lstart[j * QL];  // index in j's block
+        if (k >= BR) {
+            over = true;
+            continue;
+        }
+        const uint32_t e = list[p];
+        out[(j * BR + k) * 8 + l8] = ((const uint4*) pool)[(uint64_t) (e & kListIdMask) * 8 + l8];
+        if (l8 == 0) ent[j * BR + k] = (uint32_t) k | (e & ~kListIdMask);
+    }
+    if (over) atomicOr((unsigned long long*) flag, (unsigned long long) kPjOverflow);
+}
+
+// The counts c(i, j) of the (owned partition i, source j) pairs from the received counts messages
+// rc[j NC + i], staged in LDS (F = W QL <= 1024 pairs), each clamped to what fits in source j's block
+// of B, so that nothing downstream leaves the padded receive buffers when a block overflowed (the
+// flag then reruns the join), and the pair's first element in the block (partition-major within
+// each source). Flags a source whose block overflowed (wb > 0: its words, at QL, must fit wb too)
+// or whose status (at QL + 1) is nonzero.
+__device__ __forceinline__ void pjx_pairs(const uint64_t* __restrict__ rc, uint32_t W, uint32_t QL, uint32_t NC,
+                                          uint64_t B, uint64_t wb, uint32_t* cnt, uint32_t* first, uint64_t* flag) {
+    for (uint32_t j = threadIdx.x; j < W; j += blockDim.x) {
+        uint64_t f = 0, c = 0;
+        for (uint32_t q = 0; q < QL; q++) {
+            const uint64_t v = rc[(uint64_t) j * NC + q];
+            cnt[q * W + j]   = (uint32_t) (c < B ? min<uint64_t>(v, B - c) : 0u);
+            first[q * W + j] = (uint32_t) min<uint64_t>(c, B);
+            c += v;
+        }
+        if (c > B || (wb && rc[(uint64_t) j * NC + QL] > wb)) f |= kPjOverflow;
+        if (rc[(uint64_t) j * NC + QL + 1]) f |= kPjPeerFailed;
+        if (f) atomicOr((unsigned long long*) flag, (unsigned long long) f);
+    }
+    __syncthreads();
+}
+
+// The owner's R tables (one block of 1024 threads): per (owned partition i, source j) pair tab =
+// {first received entry, count, list position, chunk id adjustment} (source j's chunks sit at
+// j * BR of the received ones and their entries carry their index in that block), list starts
+// lsO[QL + 1] and sweep starts swO[QL + 1] (bsw chunks per sweep).
+__global__ __launch_bounds__(1024) void k_pjx_rtab(const uint64_t* __restrict__ rc, uint32_t W, uint32_t QL,
+                                                   uint32_t NC, uint64_t BR, uint32_t bsw, int64_t* __restrict__ tab,
+                                                   uint32_t* __restrict__ lsO, uint32_t* __restrict__ swO,
+                                                   uint64_t* flag) {
+    __shared__ uint32_t wsum[16];
+    __shared__ uint32_t cnt[1024], first[1024], tot[1024];
+    pjx_pairs(rc, W, QL, NC, BR, 0, cnt, first, flag);
+    const uint32_t i = threadIdx.x;
+    uint32_t       t = 0;
+    if (i < QL)
+        for (uint32_t j = 0; j < W; j++) t += cnt[i * W + j];
+    uint32_t       total;
+    const uint32_t pos = block_excl_scan(i < QL ? t : 0u, wsum, total);  // list start of partition i
+    if (i < QL) {
+        lsO[i]     = pos;
+        tot[i]     = t;
+        uint32_t p = pos;
+        for (uint32_t j = 0; j < W; j++) {
+            int64_t* e = tab + 4 * ((uint64_t) i * W + j);
+            e[0]       = (int64_t) (j * BR + first[i * W + j]);
+            e[1]       = cnt[i * W + j];
+            e[2]       = p;
+            e[3]       = (int64_t) (j * BR);
+            p += cnt[i * W + j];
+        }
+    }
+    if (i == 0) lsO[QL] = total;
+    __syncthreads();
+    const uint32_t sw = i < QL ? (tot[i] + bsw - 1) / bsw : 0u;
+    const uint32_t so = block_excl_scan(sw, wsum, total);
+    if (i < QL) swO[i] = so;
+    if (i == 0) swO[QL] = total;
+}
+
+// Survivors of this rank's probe items, item it of destination j (j = its partition / QL, k its
+// index among j's items) into j's blocks: its words at j * BW + (sofs[it] - bound[j QL]), its NSUB
+// run counts at (j * BI + k) * NSUB. One wave per item; I = item_start[F] on the device.
+__global__ __launch_bounds__(256) void k_pjx_surv_pack(const uint32_t* __restrict__ surv, const uint64_t* __restrict__ region,
+                                                       const uint32_t* __restrict__ tot, const uint64_t* __restrict__ sofs,
+                                                       const uint32_t* __restrict__ item_start, const uint64_t* __restrict__ bound,
+                                                       const uint32_t* __restrict__ cnt, uint32_t F, uint32_t QL, uint32_t NSUB,
+                                                       uint64_t BI, uint64_t BW, uint32_t* __restrict__ out,
+                                                       uint32_t* __restrict__ out_cnt, uint64_t* flag) {
+    const uint32_t I    = item_start[F];
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wv   = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint32_t nw   = (gridDim.x * blockDim.x) >> 6;
+    bool           over = false;
+    for (uint32_t it = wv; it < I; it += nw) {
+        const uint32_t j = find_q(item_start, F, it) / QL;
+        const uint64_t k = it - item_start[j * QL];
+        const uint64_t w = sofs[it] - bound[j * QL];  // the item's first word in j's block
+        const uint32_t c = tot[it];
+        if (k >= BI || w + c > BW) {  // (does not fit: the item goes with no survivors, flagged)
+            over = true;
+            if (k < BI)
+                for (uint32_t s = lane; s < NSUB; s += 64) out_cnt[(j * BI + k) * NSUB + s] = 0;
+            continue;
+        }
+        const uint64_t src = region[it], dst = j * BW + w;
+        for (uint32_t x = lane; x < c; x += 64) out[dst + x] = surv[src + x];
+        for (uint32_t s = lane; s < NSUB; s += 64) out_cnt[(j * BI + k) * NSUB + s] = cnt[(uint64_t) it * NSUB + s];
+    }
+    if (over && lane == 0) atomicOr((unsigned long long*) flag, (unsigned long long) kPjOverflow);
+}
+
+// The owner's survivor tables (one block): per (owned partition i, source j) pair tab2 = {first
+// received item (in j's block of BI), items, first output item}, istart[QL + 1], and ritems[j] (the
+// valid items of source j's block).
+__global__ __launch_bounds__(1024) void k_pjx_stab(const uint64_t* __restrict__ rc, uint32_t W, uint32_t QL, uint32_t NC,
+                                                   uint64_t BI, uint64_t BW, uint32_t* __restrict__ tab2,
+                                                   uint32_t* __restrict__ istart, uint32_t* __restrict__ ritems,
+                                                   uint64_t* flag) {
+    __shared__ uint32_t wsum[16];
+    __shared__ uint32_t cnt[1024], first[1024];
+    pjx_pairs(rc, W, QL, NC, BI, BW, cnt, first, flag);
+    const uint32_t i = threadIdx.x;
+    for (uint32_t j = threadIdx.x; j < W; j += blockDim.x) {
+        uint32_t c = 0;
+        for (uint32_t q = 0; q < QL; q++) c += cnt[q * W + j];
+        ritems[j] = c;
+    }
+    uint32_t t = 0;
+    if (i < QL)
+        for (uint32_t j = 0; j < W; j++) t += cnt[i * W + j];
+    uint32_t       total;
+    const uint32_t pos = block_excl_scan(i < QL ? t : 0u, wsum, total);
+    if (i < QL) {
+        istart[i]  = pos;
+        uint32_t p = pos;
+        for (uint32_t j = 0; j < W; j++) {
+            uint32_t* e = tab2 + 3 * ((uint64_t) i * W + j);
+            e[0]        = (uint32_t) (j * BI + first[i * W + j]);
+            e[1]        = cnt[i * W + j];
+            e[2]        = p;
+            p += cnt[i * W + j];
+        }
+    }
+    if (i == 0) istart[QL] = total;
+}
+
+// The join's exchange sizes, for the next join's plan: out = {flag, the largest R block (chunks),
+// survivor item block and word block this rank sent or received} (all-reduced with MAX over the
+// ranks afterwards). rc1 / rc2: the received counts messages; ls / is / bd: this rank's R list
+// starts, item starts and survivor word bounds (what it sent).
+__global__ void k_pjx_stat(const uint64_t* __restrict__ rc1, const uint64_t* __restrict__ rc2, const uint32_t* __restrict__ ls,
+                           const uint32_t* __restrict__ is, const uint64_t* __restrict__ bd, uint32_t W, uint32_t QL,
+                           uint32_t NC, const uint64_t* flag, uint64_t* __restrict__ out) {
+    if (threadIdx.x != 0) return;
+    uint64_t mr = 0, mi = 0, mw = 0;
+    for (uint32_t j = 0; j < W; j++) {
+        uint64_t r = 0, it = 0;
+        for (uint32_t q = 0; q < QL; q++) {
+            r += rc1[(uint64_t) j * NC + q];
+            it += rc2[(uint64_t) j * NC + q];
+        }
+        mr = max(mr, max(r, (uint64_t) (ls[(j + 1) * QL] - ls[j * QL])));
+        mi = max(mi, max(it, (uint64_t) (is[(j + 1) * QL] - is[j * QL])));
+        mw = max(mw, max(rc2[(uint64_t) j * NC + QL], bd[(j + 1) * QL] - bd[j * QL]));
+    }
+    out[0] = *flag;
+    out[1] = mr;
+    out[2] = mi;
+    out[3] = mw;
+}
+
+void launch_pjx_gather(const uint32_t* pool, const uint32_t* list, const uint32_t* lstart, uint32_t F, uint32_t QL,
+                       uint64_t BR, void* out, uint32_t* ent, uint64_t* flag, hipStream_t st) {
+    k_pjx_gather<<<4096, 256, 0, st>>>(pool, list, lstart, F, QL, BR, (uint4*) out, ent, flag);
+}
+
+void launch_pjx_rtab(const uint64_t* rc, uint32_t W, uint32_t QL, uint32_t NC, uint64_t BR, uint32_t bsw,
+                     int64_t* tab, uint32_t* lsO, uint32_t* swO, uint64_t* flag, hipStream_t st) {
+    k_pjx_rtab<<<1, 1024, 0, st>>>(rc, W, QL, NC, BR, bsw, tab, lsO, swO, flag);
+}
+
+void launch_pjx_surv_pack(const uint32_t* surv, const uint64_t* region, const uint32_t* tot, const uint64_t* sofs,
+                          const uint32_t* item_start, const uint64_t* bound, const uint32_t* cnt, uint32_t F,
+                          uint32_t QL, uint32_t NSUB, uint64_t BI, uint64_t BW, uint32_t* out, uint32_t* out_cnt,
+                          uint64_t* flag, hipStream_t st) {
+    k_pjx_surv_pack<<<2048, 256, 0, st>>>(surv, region, tot, sofs, item_start, bound, cnt, F, QL, NSUB, BI, BW, out,
+                                          out_cnt, flag);
+}
+
+void launch_pjx_stab(const uint64_t* rc, uint32_t W, uint32_t QL, uint32_t NC, uint64_t BI, uint64_t BW,
+                     uint32_t* tab2, uint32_t* istart, uint32_t* ritems, uint64_t* flag, hipStream_t st) {
+    k_pjx_stab<<<1, 1024, 0, st>>>(rc, W, QL, NC, BI, BW, tab2, istart, ritems, flag);
+}
+
+void launch_pjx_stat(const uint64_t* rc1, const uint64_t* rc2, const uint32_t* ls, const uint32_t* is,
+                     const uint64_t* bd, uint32_t W, uint32_t QL, uint32_t NC, const uint64_t* flag, uint64_t* out,
+                     hipStream_t st) {
+    k_pjx_stat<<<1, 64, 0, st>>>(rc1, rc2, ls, is, bd, W, QL, NC, flag, out);
 }
 
 // ===================================================================== launch wrappers

@@ -51,7 +51,7 @@ namespace hwbrj {
         }                                                                                  \
     } while (0)
 
-static uint64_t pj_region_cap(uint64_t n, uint32_t G, uint32_t F) {
+uint64_t pj_region_cap(uint64_t n, uint32_t G, uint32_t F) {
     const uint64_t units = (n + 3) / 4;
     const uint64_t per   = ((units + G - 1) / G) * 4;
     return (per + 31) / 32 + F + 1;
@@ -169,6 +169,7 @@ int Engine::join_partitioned(const hwbrj_exchange_t* x, int rank, int world, con
     std::vector<uint64_t> soff(W), sbytes(W), roff(W), rbytes(W);
     uint64_t              RC = 0, sweeps = 0, RI = 0, RW = 0;
     uint64_t              RCmax = 0, RImax = 0, RWmax = 0;  // native: receive capacities (worst case)
+    uint64_t              plan_mr = 0, plan_mi = 0, plan_mw = 0;  // native: largest blocks (async plan)
     std::vector<uint64_t> ritems(W), rwords(W), sofs;
     ScatterParams sp{};
     // The native transport's counts step: the message to every destination is packed on the device
@@ -316,6 +317,11 @@ int Engine::join_partitioned(const hwbrj_exchange_t* x, int rank, int world, con
         if (const int rc = native_counts(lstartR.as<uint32_t>(), nullptr, rc1, nS, ls.data(), nullptr)) return rc;
         if (const int rc = peers(rcnt.data() + QL + 1, NC, rc1)) return rc;
         if (const int rc = check_r_total()) return rc;
+        for (uint32_t j = 0; j < W; j++) {  // (the async join's plan: the largest R block)
+            uint64_t c = 0;
+            for (uint32_t i = 0; i < QL; i++) c += rcnt[(uint64_t) j * NC + i];
+            plan_mr = std::max<uint64_t>(plan_mr, std::max<uint64_t>(c, ls[(j + 1) * QL] - ls[j * QL]));
+        }
         PJ_STAGE("R scatter");
         launch_pj_gather(poolR.as<uint32_t>(), listR.as<uint32_t>(), ls[F], sendC, sendE, stream);
         PJ_STAGE("k_pj_gather");
@@ -595,6 +601,8 @@ int Engine::join_partitioned(const hwbrj_exchange_t* x, int rank, int world, con
             rwords[j] = rcnt[j * NC + QL];
             RI += c;
             RW += rwords[j];
+            plan_mi = std::max<uint64_t>(plan_mi, std::max<uint64_t>(c, isS[(j + 1) * QL] - isS[j * QL]));
+            plan_mw = std::max<uint64_t>(plan_mw, std::max<uint64_t>(rwords[j], bnd[(j + 1) * QL] - bnd[j * QL]));
         }
         if (native) {  // (allocated at RImax / RWmax before the counts step, from every shard's exact
                        // |S|, so no input can exceed them: a bug guard)
@@ -643,10 +651,13 @@ int Engine::join_partitioned(const hwbrj_exchange_t* x, int rank, int world, con
             "survivor run counts");
     lap(5);
     // ------------------------------------------------------------- 7. join of the owned partitions
-    // (no collective follows: a failure here is this rank's alone)
+    // (no collective of the join follows: a failure here is this rank's alone; the async join's
+    // plan step, when asked for, comes after it on every rank whatever this returns)
     // The owner's item tables on the device (k_pj_item_tables) from the received per-item counts;
     // the host lays out only the (owned partition, source) pairs: items of owned partition i are
     // those of source 0, 1, ... (each source's block is in partition order).
+    uint64_t small_h[6] = {0, 0, 0, 0, 0, 0};
+    const int rc7 = [&]() -> int {
     const uint32_t NJ = QL * NSUB;
     std::vector<uint32_t> tab2((size_t) 3 * QL * W), istart(QL + 1, 0);
     {
@@ -734,9 +745,15 @@ int Engine::join_partitioned(const hwbrj_exchange_t* x, int rank, int world, con
     launch_join(jp, NJ, pjJobs.as<uint32_t>(), stream);
     PJ_STAGE("k_join");
     PJ_CHECK(hipGetLastError());
-    uint64_t small_h[6] = {0, 0, 0, 0, 0, 0};
-    if (const int rc = read_join_counts(d_result, true, stream, small_h)) return rc;
+    return read_join_counts(d_result, true, stream, small_h);
+    }();
     lap(6);
+    if (native && pj_make_plan()) {  // (every rank: a collective)
+        PJ_CHECK(hipStreamSynchronize(stream));
+        if (const int rc = pj_plan_from_sync(world, rank, nR, nR_total, nS, args, plan_mr, plan_mi, plan_mw))
+            return rc7 ? rc7 : rc;
+    }
+    if (rc7) return rc7;
     pending_ = false;
     have_filter_ = false;  // (the slices live in the caller's exchange buffer)
     last_nj_     = 0;      // job_surv holds this join's counts: the next enqueue clears the table

@@ -197,7 +197,46 @@ def join_partitioned_rccl(R, S, nR_total: int, args=None) -> Stats:
     return Stats(**{n: getattr(st, n) for n, _ in _Stats._fields_})
 
 
+def join_partitioned_rccl_async(R, S, nR_total: int, args=None) -> None:
+    """join_partitioned_rccl enqueued without host waits (hwbrj_join_partitioned_rccl_async): the
+    exchanges are padded to a plan made by an earlier synchronous join of the same shapes (the first
+    call runs synchronously and makes it). Collect with join_partitioned_wait, in call order; R and
+    S must stay alive and unchanged until then. A collective: every rank makes the same calls."""
+    _check_rel(R, S)
+    a = args._c() if args is not None else None
+    rc = lib().hwbrj_join_partitioned_rccl_async(_ptr(R), R.shape[0], int(nR_total), _ptr(S), S.shape[0],
+                                                 ctypes.byref(a) if a is not None else None)
+    _err(rc, "hwbrj_join_partitioned_rccl_async")
+
+
+def join_partitioned_wait() -> Stats:
+    """The oldest enqueued async partitioned join's result (hwbrj_join_partitioned_wait); a join
+    whose padded blocks overflowed on any rank is rerun synchronously here (same counts)."""
+    st = _Stats()
+    _err(lib().hwbrj_join_partitioned_wait(ctypes.byref(st)), "hwbrj_join_partitioned_wait")
+    return Stats(**{n: getattr(st, n) for n, _ in _Stats._fields_})
+
+
+PJ_INFO_FIELDS = ("plan_valid", "BR", "BI", "BW", "async_joins", "sync_plan_joins", "overflow_reruns",
+                  "plans", "in_flight", "last_rerun_flag", "last_r_block", "last_item_block",
+                  "last_word_block")
+
+
+def pj_async_info() -> dict:
+    """hwbrj_pj_async_info: the async join's plan (block bounds) and counters."""
+    out = (ctypes.c_uint64 * 16)()
+    _err(lib().hwbrj_pj_async_info(out), "hwbrj_pj_async_info")
+    return {k: int(out[i]) for i, k in enumerate(PJ_INFO_FIELDS)}
+
+
 def _bind(L):
+    L.hwbrj_join_partitioned_rccl_async.restype = ctypes.c_int
+    L.hwbrj_join_partitioned_rccl_async.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
+                                                    ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(_BloomArgs)]
+    L.hwbrj_join_partitioned_wait.restype = ctypes.c_int
+    L.hwbrj_join_partitioned_wait.argtypes = [ctypes.POINTER(_Stats)]
+    L.hwbrj_pj_async_info.restype = ctypes.c_int
+    L.hwbrj_pj_async_info.argtypes = [ctypes.c_void_p]
     L.hwbrj_comm_unique_id.restype = ctypes.c_int
     L.hwbrj_comm_unique_id.argtypes = [ctypes.c_void_p]
     L.hwbrj_comm_init.restype = ctypes.c_int

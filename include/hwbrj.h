@@ -250,6 +250,29 @@ int hwbrj_set_filter_broadcast(int on);
 int hwbrj_join_partitioned_rccl(const tuple_t * d_R, uint64_t nR, uint64_t nR_total,
                                 const tuple_t * d_S, uint64_t nS, const bloom_filter_args_t * args,
                                 hwbrj_stats_t * stats);
+/* The same join enqueued without host waits (no reference counterpart; the reference joins one
+ * relation pair per process run). Every variable all-to-all is padded to a plan's block bounds
+ * (the largest blocks of an earlier synchronous join of the same shapes + 12.5 % + 64, agreed by
+ * all ranks), so counts messages, padded exchanges, the owner's tables, build, probe and join are
+ * all enqueued on the join stream and up to 8 joins can be in flight. The first call (and the call
+ * after a plan was dropped) runs synchronously and makes the plan. A block that does not fit sets
+ * a device flag that is max-reduced over the ranks at the end of the join: its wait reruns it
+ * synchronously on every rank (same counts; a new plan). A rank whose shard sizes or filter
+ * differ from the plan's takes part with empty messages and flags the join the same way.
+ * A collective: every rank makes the same calls in the same order. The inputs must stay valid and
+ * unchanged until the join's wait returns.
+ *   hwbrj_join_partitioned_wait  collects the oldest enqueued join (FIFO): 0 or its error; stats:
+ *                                counts, and ms_total = its device time between its first and last
+ *                                operation on the join stream (0 phase times)
+ *   hwbrj_pj_async_info          out[16]: plan valid, BR (chunks), BI (items), BW (words), async
+ *                                joins, synchronous plan joins, overflow reruns, plans made, joins
+ *                                in flight, the last rerun's flag (1 overflow, 2 a rank in the
+ *                                failed mode), the last join's largest R / item / word block. */
+int hwbrj_join_partitioned_rccl_async(const tuple_t * d_R, uint64_t nR, uint64_t nR_total,
+                                      const tuple_t * d_S, uint64_t nS,
+                                      const bloom_filter_args_t * args);
+int hwbrj_join_partitioned_wait(hwbrj_stats_t * stats);
+int hwbrj_pj_async_info(uint64_t * out /* 16 */);
 
 /* Fill d_out / out with the reference generator's key multiset (src/generator.c:304-415 with
  * `nthreads` generator threads) in a seeded permuted order; payload = row index. */
@@ -342,8 +365,20 @@ const char * hwbrj_version(void);
  *                             empty unless something writes it: the counts must drop). Honoured
  *                             only on a communicator of world 1 (a test setting; ignored by a
  *                             real multi-rank broadcast).
+ *   HWBRJ_HOOK_PJ_PLAN_DIV    value > 0: the async partitioned join's plans get their block bounds
+ *                             divided by `value`, so the next async join overflows and is rerun
+ *                             synchronously (counts unchanged).
+ *   HWBRJ_HOOK_PJ_ASYNC_FAIL  1: this rank runs every async partitioned join in the failed mode
+ *                             (empty messages, failed status), as after a shape change: every rank
+ *                             reruns the join synchronously (counts unchanged).
  * Returns 0, or 2 for an unknown hook or a value out of range. */
-enum { HWBRJ_HOOK_JOIN_SPLIT = 1, HWBRJ_HOOK_PJ_FAIL_RANK = 2, HWBRJ_HOOK_BCAST_NONROOT = 3 };
+enum {
+    HWBRJ_HOOK_JOIN_SPLIT     = 1,
+    HWBRJ_HOOK_PJ_FAIL_RANK   = 2,
+    HWBRJ_HOOK_BCAST_NONROOT  = 3,
+    HWBRJ_HOOK_PJ_PLAN_DIV    = 4,
+    HWBRJ_HOOK_PJ_ASYNC_FAIL  = 5
+};
 int          hwbrj_set_test_hook(int hook, int64_t value);
 
 #ifdef __cplusplus

@@ -145,17 +145,22 @@ def test_filter_broadcast_world1(hw, cuda, orc, rccl1, a):
 
 
 # ------------------------------------------------- bench.py over the RCCL process group, world 1
-@pytest.mark.parametrize("case", ["partitioned-native", "partitioned-torch-nccl", "replicated-bcast"])
+@pytest.mark.parametrize("case", ["partitioned-native", "partitioned-native-sync", "partitioned-torch-nccl",
+                                  "replicated-bcast"])
 def test_bench_rccl_world1(hw, case):
     """bench.py's multi-GPU designs under torch.distributed.run with the RCCL ("nccl") group at
-    world 1 (HWBRJ_BENCH_DIST=1): the native partitioned transport, the torch callback transport
-    with its collectives forced (HWBRJ_PJ_FORCE_COLL=1: all_to_all_single / all_gather_into_tensor
-    on device uint8 over RCCL), and the replicated design with the filter broadcast."""
+    world 1 (HWBRJ_BENCH_DIST=1): the native partitioned transport (the async join, K joins back to
+    back with no overflow rerun in the timed region; and the synchronous one), the torch callback
+    transport with its collectives forced (HWBRJ_PJ_FORCE_COLL=1: all_to_all_single /
+    all_gather_into_tensor on device uint8 over RCCL), and the replicated design with the filter
+    broadcast."""
     g = GOLD["F3_grid"]
     base = ["-r", g["r"], "-s", g["s"], "-m", g["m"]]
     env = {"HWBRJ_BENCH_DIST": "1"}
-    if case == "partitioned-native":  # (the rank's own blocks through ncclSend / ncclRecv too)
+    if case.startswith("partitioned-native"):  # (the rank's own blocks through ncclSend / ncclRecv too)
         args = base + ["--design", "partitioned", "--transport", "native"]
+        if case.endswith("sync"):
+            args.append("--pj-sync")
         env["HWBRJ_RCCL_SELF"] = "1"
     elif case == "partitioned-torch-nccl":
         args = base + ["--design", "partitioned", "--transport", "torch"]
@@ -168,6 +173,12 @@ def test_bench_rccl_world1(hw, case):
     assert (line["parity"]["filtered"], line["parity"]["matches"]) == (g["rows"]["1024"][0], g["results"])
     assert line["dist"]["backend"] == "nccl" and line["dist"]["world_size_seen"] == 1
     assert line["scaling"] == "strong"
+    if case == "partitioned-native":
+        pa = line["pj_async"]
+        assert pa["reruns_in_timed"] == 0 and pa["async_in_timed"] == line["steps"], pa
+        assert pa["rank0_counts_all_equal"] and pa["events_ms_per_join_rank0"] > 0, pa
+    elif case == "partitioned-native-sync":
+        assert line["pj_async"] is None
 
 
 # ------------------------------------------------- status agreement (no hang on one rank's error)
@@ -252,3 +263,148 @@ def test_filter_broadcast_nonroot_world1(hw, cuda, orc, rccl1, hook, a):
     hook(hw.HOOK_BCAST_NONROOT, 0)
     st = hw.join_device(dR, dS, args)  # the root again rebuilds them
     assert (st.filtered, st.matches) == (filt, res)
+
+
+# ------------------------------------------------- the async partitioned join
+def _ref_counts(orc, R, S, args):
+    if args is None:
+        res, filt, _ = orc.bpro(R, S, 8, 0, 0, 0, 0, use_bloom=False)
+    else:
+        res, filt, _ = orc.bpro(R, S, 8, args.variant, args.m, args.k, args.B)
+    return filt, res
+
+
+@pytest.mark.parametrize("self_rccl", [False, True], ids=["self-copy", "self-rccl"])
+@pytest.mark.parametrize("a", PJ_ARGS, ids=str)
+def test_partitioned_async_world1_vs_oracle(hw, cuda, orc, rccl1, a, self_rccl, monkeypatch):
+    """hwbrj_join_partitioned_rccl_async: the first join of a shape runs synchronously and makes the
+    plan; the next ones (3 enqueued back to back, no host wait between them) use padded exchanges
+    and device-built owner tables, with no rerun. Every join's counts equal the oracle's; a new
+    shape's first join finds the old plan (the failed mode: it is rerun synchronously, same counts,
+    and makes the new plan). HWBRJ_RCCL_SELF=1 puts the padded blocks and the flag's all-reduce through RCCL."""
+    if self_rccl:
+        monkeypatch.setenv("HWBRJ_RCCL_SELF", "1")
+    args = None if a is None else hw.BloomFilterArgs.from_flag(a[0], a[1], a[2], a[3] or 1024)
+    rng = np.random.default_rng(43)
+    for nR, nS in [(0, 1000), (7, 33), (100003, 400009), (1000000, 4000000)]:
+        Rk = rng.permutation(nR).astype(np.int64) + 1
+        Sk = rng.integers(0, 2 * max(nR, 1) + 2, size=nS)
+        R, S = rel(Rk), rel(Sk)
+        want = _ref_counts(orc, R, S, args)
+        dR, dS = to_dev(cuda, R), to_dev(cuda, S)
+        # a new shape: the plan join (synchronous, or the failed mode rerun), then 3 back to back
+        rccl1.join_partitioned_rccl_async(dR, dS, nR, args)
+        st = rccl1.join_partitioned_wait()
+        assert (st.filtered, st.matches) == want, (a, nR, nS, st)
+        i0 = rccl1.pj_async_info()
+        assert i0["plan_valid"] == 1 and i0["last_rerun_flag"] in (0, 2), i0
+        for _ in range(3):
+            rccl1.join_partitioned_rccl_async(dR, dS, nR, args)
+        assert rccl1.pj_async_info()["in_flight"] == 3
+        for k in range(3):
+            st = rccl1.join_partitioned_wait()
+            assert (st.filtered, st.matches) == want, (a, nR, nS, k, st)
+        i1 = rccl1.pj_async_info()
+        assert i1["in_flight"] == 0 and i1["async_joins"] - i0["async_joins"] == 3, (i0, i1)
+        assert i1["overflow_reruns"] == i0["overflow_reruns"], (i0, i1)
+        del dR, dS
+
+
+def test_partitioned_async_northstar_back_to_back(hw, cuda, rccl1):
+    """The north-star golden through the async join: the plan join, then 3 joins
+    enqueued back to back; each join's device time is reported from its HIP events."""
+    g = GOLD["F4_northstar"]
+    R = cuda.empty((g["r"], 2), dtype=cuda.int32, device="cuda")
+    S = cuda.empty((g["s"], 2), dtype=cuda.int32, device="cuda")
+    hw.generate_device(R, 2, g["r"], g["r"], 1.0, 12345)
+    hw.generate_device(S, 2, INT_MAX, g["r"], g["q"], 54321)
+    args = hw.BloomFilterArgs(hw.BLOCKED, g["m"], 1, g["B"])
+    for _ in range(4):
+        rccl1.join_partitioned_rccl_async(R, S, g["r"], args)
+    sts = [rccl1.join_partitioned_wait() for _ in range(4)]
+    info = rccl1.pj_async_info()
+    del R, S
+    for st in sts:
+        assert (st.filtered, st.matches) == (g["k1_filtered"], g["results"])
+    assert info["overflow_reruns"] == 0 and info["async_joins"] >= 3, info
+    assert all(st.ms_total > 0 for st in sts[1:])
+    assert info["BR"] >= info["last_r_block"] and info["BW"] >= info["last_word_block"], info
+
+
+def test_partitioned_async_overflow_rerun_world1(hw, cuda, orc, rccl1, hook):
+    """A plan too small for the join (HWBRJ_HOOK_PJ_PLAN_DIV divides its block bounds): the padded
+    blocks overflow, the device flag is set, and the wait reruns the join synchronously -- counts
+    unchanged -- and makes a new plan; once the hook is off, the plan it makes holds and the joins
+    run async without reruns."""
+    g = GOLD["F3_grid"]
+    R = hw.generate_host(g["r"], 2, g["r"], g["r"], 1.0, 1)
+    S = hw.generate_host(g["s"], 2, INT_MAX, g["r"], g["q"], 2)
+    dR, dS = to_dev(cuda, R), to_dev(cuda, S)
+    args = hw.BloomFilterArgs(hw.BLOCKED, g["m"], 1, 1024)
+    want = (g["rows"]["1024"][0], g["results"])
+    hook(hw.HOOK_PJ_PLAN_DIV, 8)
+    rccl1.join_partitioned_rccl_async(dR, dS, g["r"], args)  # (synchronous: makes the small plan)
+    rccl1.join_partitioned_rccl_async(dR, dS, g["r"], args)  # (overflows)
+    for _ in range(2):
+        st = rccl1.join_partitioned_wait()
+        assert (st.filtered, st.matches) == want
+    i = rccl1.pj_async_info()
+    assert i["overflow_reruns"] == 1 and i["last_rerun_flag"] == 1 and i["plan_valid"] == 1, i
+    hw.set_test_hook(hw.HOOK_PJ_PLAN_DIV, 0)
+    # the plan the rerun made under the hook is still too small: one more overflow, whose rerun
+    # (hook off) makes a plan that holds
+    rccl1.join_partitioned_rccl_async(dR, dS, g["r"], args)
+    st = rccl1.join_partitioned_wait()
+    assert (st.filtered, st.matches) == want
+    i2 = rccl1.pj_async_info()
+    assert i2["overflow_reruns"] == 2, i2
+    for _ in range(3):
+        rccl1.join_partitioned_rccl_async(dR, dS, g["r"], args)
+    for _ in range(3):
+        st = rccl1.join_partitioned_wait()
+        assert (st.filtered, st.matches) == want
+    i3 = rccl1.pj_async_info()
+    assert i3["overflow_reruns"] == 2 and i3["async_joins"] - i2["async_joins"] == 3, (i2, i3)
+
+
+def test_partitioned_async_failed_mode_world1(hw, cuda, orc, rccl1, hook):
+    """The failed mode (HWBRJ_HOOK_PJ_ASYNC_FAIL: this rank sends empty counts messages with a failed
+    status, as after a shape change, and still takes part in every collective): the flag is set on
+    every rank, the wait reruns the join synchronously and the counts are right. A join of another
+    shape than the plan's takes the same path by itself. Also: more than 8 joins in flight is
+    refused, and a wait with none in flight is an error."""
+    g = GOLD["F3_grid"]
+    R = hw.generate_host(g["r"], 2, g["r"], g["r"], 1.0, 1)
+    S = hw.generate_host(g["s"], 2, INT_MAX, g["r"], g["q"], 2)
+    dR, dS = to_dev(cuda, R), to_dev(cuda, S)
+    args = hw.BloomFilterArgs(hw.BLOCKED, g["m"], 1, 1024)
+    want = (g["rows"]["1024"][0], g["results"])
+    with pytest.raises(RuntimeError, match="no partitioned join"):
+        rccl1.join_partitioned_wait()
+    rccl1.join_partitioned_rccl_async(dR, dS, g["r"], args)
+    assert (lambda s: (s.filtered, s.matches))(rccl1.join_partitioned_wait()) == want
+    hook(hw.HOOK_PJ_ASYNC_FAIL, 1)
+    rccl1.join_partitioned_rccl_async(dR, dS, g["r"], args)
+    st = rccl1.join_partitioned_wait()
+    assert (st.filtered, st.matches) == want
+    i = rccl1.pj_async_info()
+    assert i["overflow_reruns"] == 1 and i["last_rerun_flag"] == 2, i
+    hw.set_test_hook(hw.HOOK_PJ_ASYNC_FAIL, 0)
+    # another shape: half of S
+    half = S[: S.shape[0] // 2]
+    res, filt, _ = orc.bpro(R, half, 8, args.variant, args.m, args.k, args.B)
+    dH = to_dev(cuda, half)
+    rccl1.join_partitioned_rccl_async(dR, dH, g["r"], args)
+    st = rccl1.join_partitioned_wait()
+    assert (st.filtered, st.matches) == (filt, res)
+    assert rccl1.pj_async_info()["overflow_reruns"] == 2
+    for _ in range(8):
+        rccl1.join_partitioned_rccl_async(dR, dH, g["r"], args)
+    with pytest.raises(RuntimeError, match="too many"):
+        rccl1.join_partitioned_rccl_async(dR, dH, g["r"], args)
+    for _ in range(8):
+        st = rccl1.join_partitioned_wait()
+        assert (st.filtered, st.matches) == (filt, res)
+    # a single-GPU join after async ones on the same Engine is ordered after them and correct
+    st = hw.join_device(dR, dS, args)
+    assert (st.filtered, st.matches) == want

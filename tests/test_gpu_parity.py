@@ -391,7 +391,7 @@ def test_bench_two_ranks(hw):
     # the other designs on the same ranks: the broadcast needs a GPU per rank,
     # the partitioned join runs over the torch transport; its per-rank counts sum to the golden
     alt = line["alt_designs"]
-    assert "skipped" in alt["bcast"]
+    assert "skipped" in alt["bcast"] and "skipped" in alt["partitioned_async"]
     part = alt["partitioned"]
     assert len(part["per_rank"]) == 2 and part["sum"] == [g["rows"]["1024"][0], g["results"]], part
     assert part["ms"] > 0
@@ -420,7 +420,7 @@ def test_bench_rccl_process_group(hw):
     assert line["scaling"] == "strong" and line["dist"] == {"world_size_seen": 1, "backend": "nccl",
                                                             "shared_gpu_rehearsal": False}
     # the other designs on the same rank over the library's RCCL communicator
-    for name in ("bcast", "partitioned"):
+    for name in ("bcast", "partitioned", "partitioned_async"):
         leg = line["alt_designs"][name]
         assert leg.get("sum") == [g["rows"]["1024"][0], g["results"]] and leg["ms"] > 0, (name, leg)
         assert leg["per_rank"] == [leg["sum"]]

@@ -9,6 +9,6 @@ while [ $# -ge 2 ]; do
   name=$1; flags=$2; shift 2
   /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -shared -I$C -I$ROOT/include -DHWBRJ_DEV_BUILD $flags \
     $C/hwbrj_kernels.hip -x hip $C/hwbrj_engine.cpp $C/hwbrj_api.cpp $C/hwbrj_gen.cpp $C/hwbrj_pjoin.cpp $C/hwbrj_comm.cpp \
-    -o $ROOT/tools/abl_so/libhwbrj_$name.so -lpthread -ldl &
+    $C/hwbrj_pjoin_async.cpp -o $ROOT/tools/abl_so/libhwbrj_$name.so -lpthread -ldl &
 done
 wait

@@ -15,6 +15,7 @@ sed -i 's#"../../include/hwbrj.h"#"hwbrj.h"#' $T/csrc/*.h $T/csrc/*.cpp $T/csrc/
 C=$T/csrc
 /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -shared -I$C -I$T/include \
   $C/hwbrj_kernels.hip -x hip $C/hwbrj_engine.cpp $C/hwbrj_api.cpp $C/hwbrj_gen.cpp $C/hwbrj_pjoin.cpp $C/hwbrj_comm.cpp \
+  $(ls $C/hwbrj_pjoin_async.cpp 2>/dev/null) \
   -o $ROOT/tools/abl_so/libhwbrj_$name.so -lpthread -ldl
 rm -rf $T
 echo built tools/abl_so/libhwbrj_$name.so from $rev
