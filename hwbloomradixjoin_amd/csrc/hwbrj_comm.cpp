@@ -213,6 +213,8 @@ int rccl_alltoall_u64_dev(Engine* e, const uint64_t* d_send, uint64_t* d_recv, u
     return 0;
 }
 
+bool rccl_self_blocks() { return rccl_self(); }
+
 // In-place max over the ranks of n u64 in device memory, on the engine's stream (the async
 // partitioned join's overflow flag and exchange sizes; a no-op at world 1 but with HWBRJ_RCCL_SELF).
 int rccl_allreduce_max_u64(Engine* e, uint64_t* d, uint64_t n) {

@@ -227,6 +227,8 @@ int rccl_agree_status(void* comm, int world, int rank, int rc, hipStream_t strea
 class Engine;
 int rccl_alltoall_u64_dev(Engine* e, const uint64_t* d_send, uint64_t* d_recv, uint64_t n);
 int rccl_allreduce_max_u64(Engine* e, uint64_t* d, uint64_t n);
+// HWBRJ_RCCL_SELF (tests): a rank's own exchange blocks go through ncclSend / ncclRecv too
+bool rccl_self_blocks();
 // chunks of a shard's partition pool for n tuples over G scatter workgroups and F partitions
 uint64_t pj_region_cap(uint64_t n, uint32_t G, uint32_t F);
 

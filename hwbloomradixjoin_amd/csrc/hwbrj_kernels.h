@@ -225,28 +225,39 @@ void   launch_pj_item_tables(const uint32_t* tab, uint32_t pairs, uint32_t W, co
 // gathered into blocks of BR per destination, the owner's R tables from the received counts, the
 // survivors packed into blocks of BI items / BW words, the owner's survivor tables, and the exchange
 // sizes of the join for the next plan ({flag, R block, item block, word block} maxima)
+// (own >= 0: this rank's own block written straight into the receive buffers own_out / own_ent)
 void   launch_pjx_gather(const uint32_t* pool, const uint32_t* list, const uint32_t* lstart, uint32_t F, uint32_t QL,
-                         uint64_t BR, void* out, uint32_t* ent, uint64_t* flag, hipStream_t st);
+                         uint32_t W, uint64_t BR, void* out, uint32_t* ent, int own, void* own_out, uint32_t* own_ent,
+                         uint64_t* flag, hipStream_t st);
 void   launch_pjx_rtab(const uint64_t* rc, uint32_t W, uint32_t QL, uint32_t NC, uint64_t BR, uint32_t bsw,
                        int64_t* tab, uint32_t* lsO, uint32_t* swO, uint64_t* flag, hipStream_t st);
 void   launch_pjx_surv_pack(const uint32_t* surv, const uint64_t* region, const uint32_t* tot, const uint64_t* sofs,
                             const uint32_t* item_start, const uint64_t* bound, const uint32_t* cnt, uint32_t F,
                             uint32_t QL, uint32_t NSUB, uint64_t BI, uint64_t BW, uint32_t* out, uint32_t* out_cnt,
-                            uint64_t* flag, hipStream_t st);
+                            int own, uint32_t* own_out, uint32_t* own_cnt, uint64_t* flag, hipStream_t st);
 void   launch_pjx_stab(const uint64_t* rc, uint32_t W, uint32_t QL, uint32_t NC, uint64_t BI, uint64_t BW,
                        uint32_t* tab2, uint32_t* istart, uint32_t* ritems, uint64_t* flag, hipStream_t st);
 void   launch_pjx_stat(const uint64_t* rc1, const uint64_t* rc2, const uint32_t* ls, const uint32_t* is,
                        const uint64_t* bd, uint32_t W, uint32_t QL, uint32_t NC, const uint64_t* flag, uint64_t* out,
                        hipStream_t st);
+// The synchronous partitioned join's own block (this rank to itself) written straight into the
+// receive buffers: elements in [lo, hi) go to out / ent at index + delta (lo = hi: none).
+struct PjOwn {
+    uint32_t  lo = 0, hi = 0;
+    int64_t   delta = 0;
+    void*     out = nullptr;
+    uint32_t* ent = nullptr;
+};
 void   launch_pj_gather(const uint32_t* pool, const uint32_t* list, uint32_t n, void* out, uint32_t* ent,
-                        hipStream_t st);
+                        hipStream_t st, const PjOwn& own = PjOwn{});
 // the native transport's per-destination counts message (k_pj_counts), built on the device
 void   launch_pj_counts(const uint32_t* starts, const uint64_t* bound, uint32_t W, uint32_t QL, uint32_t NC,
                         uint64_t status, uint64_t extra, uint64_t extra2, uint64_t* out, hipStream_t st);
 void   launch_pj_relist(const uint32_t* rent, const int64_t* tab, uint32_t pairs, uint32_t* list,
                         hipStream_t st);
 void   launch_pj_surv_pack(const uint32_t* surv, const uint64_t* region, const uint32_t* tot,
-                           const uint64_t* soff, uint32_t n, uint32_t* out, hipStream_t st);
+                           const uint64_t* soff, uint32_t n, uint32_t* out, hipStream_t st,
+                           const PjOwn& own = PjOwn{});
 void   launch_export(const uint32_t* slices, const Geometry& g, uint32_t* out, uint64_t nwords,
                      hipStream_t st);
 // a streaming copy of bytes (multiple of 16) from src to dst, grid workgroups of contiguous ranges

@@ -3656,16 +3656,20 @@ void launch_mat_probe(const uint2* S, uint64_t n, const uint2* R, const unsigned
 // The S shard is scattered and probed locally against the full filter, and each item's survivors
 // go to the owner of its partition (k_pj_surv_pack), which joins them (k_join with item_base).
 
-// out chunk p (8 lanes of 16 B) = pool chunk of list entry p; ent[p] = p | the entry's count bits
+// out chunk p (8 lanes of 16 B) = pool chunk of list entry p; ent[p] = p | the entry's count bits.
+// Chunks p in [own.lo, own.hi) -- this rank's block to itself -- go to own.out / own.ent at p +
+// own.delta instead (the receive buffer: the exchange skips the copy to itself).
 __global__ __launch_bounds__(256) void k_pj_gather(const uint32_t* __restrict__ pool,
                                                    const uint32_t* __restrict__ list, uint32_t n,
-                                                   uint4* __restrict__ out, uint32_t* __restrict__ ent) {
+                                                   uint4* __restrict__ out, uint32_t* __restrict__ ent, PjOwn own) {
     const uint64_t stride = (uint64_t) gridDim.x * blockDim.x;
     for (uint64_t t = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x; t < (uint64_t) n * 8; t += stride) {
         const uint32_t p = (uint32_t) (t >> 3), l8 = (uint32_t) (t & 7);
         const uint32_t e = list[p];
-        out[t]           = ((const uint4*) pool)[(uint64_t) (e & kListIdMask) * 8 + l8];
-        if (l8 == 0) ent[p] = p | (e & ~kListIdMask);
+        const bool     me = p >= own.lo && p < own.hi;
+        const uint64_t d  = me ? (uint64_t) ((int64_t) p + own.delta) : p;
+        (me ? (uint4*) own.out : out)[d * 8 + l8] = ((const uint4*) pool)[(uint64_t) (e & kListIdMask) * 8 + l8];
+        if (l8 == 0) (me ? own.ent : ent)[d] = p | (e & ~kListIdMask);
     }
 }
 
@@ -3685,19 +3689,21 @@ __global__ __launch_bounds__(256) void k_pj_relist(const uint32_t* __restrict__ 
 }
 
 // One wave per item: its `tot` survivor words (contiguous from the item region's start, grouped
-// by sub) to out + soff[it].
+// by sub) to out + soff[it]; items in [own.lo, own.hi) to own.out + soff[it] + own.delta instead.
 __global__ __launch_bounds__(256) void k_pj_surv_pack(const uint32_t* __restrict__ surv,
                                                       const uint64_t* __restrict__ region,
                                                       const uint32_t* __restrict__ tot,
                                                       const uint64_t* __restrict__ soff, uint32_t n,
-                                                      uint32_t* __restrict__ out) {
+                                                      uint32_t* __restrict__ out, PjOwn own) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wv   = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint32_t nw   = (gridDim.x * blockDim.x) >> 6;
     for (uint32_t it = wv; it < n; it += nw) {
-        const uint64_t src = region[it], dst = soff[it];
+        const bool     me  = it >= own.lo && it < own.hi;
+        const uint64_t src = region[it], dst = me ? (uint64_t) ((int64_t) soff[it] + own.delta) : soff[it];
+        uint32_t*      o   = me ? (uint32_t*) own.out : out;
         const uint32_t c   = tot[it];
-        for (uint32_t i = lane; i < c; i += 64) out[dst + i] = surv[src + i];
+        for (uint32_t i = lane; i < c; i += 64) o[dst + i] = surv[src + i];
     }
 }
 
@@ -3883,8 +3889,8 @@ void launch_pj_counts(const uint32_t* starts, const uint64_t* bound, uint32_t W,
 }
 
 void launch_pj_gather(const uint32_t* pool, const uint32_t* list, uint32_t n, void* out, uint32_t* ent,
-                      hipStream_t st) {
-    if (n) k_pj_gather<<<4096, 256, 0, st>>>(pool, list, n, (uint4*) out, ent);
+                      hipStream_t st, const PjOwn& own) {
+    if (n) k_pj_gather<<<4096, 256, 0, st>>>(pool, list, n, (uint4*) out, ent, own);
 }
 
 void launch_pj_relist(const uint32_t* rent, const int64_t* tab, uint32_t pairs, uint32_t* list,
@@ -3893,8 +3899,8 @@ void launch_pj_relist(const uint32_t* rent, const int64_t* tab, uint32_t pairs, 
 }
 
 void launch_pj_surv_pack(const uint32_t* surv, const uint64_t* region, const uint32_t* tot,
-                         const uint64_t* soff, uint32_t n, uint32_t* out, hipStream_t st) {
-    if (n) k_pj_surv_pack<<<2048, 256, 0, st>>>(surv, region, tot, soff, n, out);
+                         const uint64_t* soff, uint32_t n, uint32_t* out, hipStream_t st, const PjOwn& own) {
+    if (n) k_pj_surv_pack<<<2048, 256, 0, st>>>(surv, region, tot, soff, n, out, own);
 }
 
 // ---- the async partitioned join (hwbrj_join_partitioned_rccl_async): fixed exchange blocks
@@ -3905,48 +3911,64 @@ void launch_pj_surv_pack(const uint32_t* surv, const uint64_t* region, const uin
 constexpr uint32_t kPjOverflow = 1u, kPjPeerFailed = 2u;
 
 // R chunks in list order into destination j's block at j * BR (entries: their index in the block
-// plus the list entry's count bits). n = lstart[F] (on the device).
+// plus the list entry's count bits). n = lstart[F] (on the device). The block of destination `own`
+// (this rank; -1: none) goes straight to own_out / own_ent at the same position: the receive
+// buffer's block of this source, so the exchange skips the rank's copy to itself.
 __global__ __launch_bounds__(256) void k_pjx_gather(const uint32_t* __restrict__ pool, const uint32_t* __restrict__ list,
                                                     const uint32_t* __restrict__ lstart, uint32_t F, uint32_t QL,
-                                                    uint64_t BR, uint4* __restrict__ out, uint32_t* __restrict__ ent,
-                                                    uint64_t* flag) {
+                                                    uint32_t W, uint64_t BR, uint4* __restrict__ out,
+                                                    uint32_t* __restrict__ ent, int own, uint4* __restrict__ own_out,
+                                                    uint32_t* __restrict__ own_ent, uint64_t* flag) {
     const uint32_t n      = lstart[F];
     const uint64_t stride = (uint64_t) gridDim.x * blockDim.x;
     bool           over   = false;
     for (uint64_t t = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x; t < (uint64_t) n * 8; t += stride) {
         const uint32_t p = (uint32_t) (t >> 3), l8 = (uint32_t) (t & 7);
-        const uint32_t j = find_q(lstart, F, p) / QL;
-        const uint64_t k = p - lstart[j * QL];  // index in j's block
+        // destination: the last block start at or below p (W starts, not F: empty blocks skipped)
+        uint32_t lo = 0, hi = W;
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (lstart[mid * QL] <= p) lo = mid;
+            else hi = mid;
+        }
+        const uint64_t k = p - lstart[lo * QL];  // index in the destination's block
         if (k >= BR) {
             over = true;
             continue;
         }
-        const uint32_t e = list[p];
-        out[(j * BR + k) * 8 + l8] = ((const uint4*) pool)[(uint64_t) (e & kListIdMask) * 8 + l8];
-        if (l8 == 0) ent[j * BR + k] = (uint32_t) k | (e & ~kListIdMask);
+        const uint32_t e   = list[p];
+        const bool     me  = (int) lo == own;
+        const uint64_t pos = lo * BR + k;
+        (me ? own_out : out)[pos * 8 + l8] = ((const uint4*) pool)[(uint64_t) (e & kListIdMask) * 8 + l8];
+        if (l8 == 0) (me ? own_ent : ent)[pos] = (uint32_t) k | (e & ~kListIdMask);
     }
     if (over) atomicOr((unsigned long long*) flag, (unsigned long long) kPjOverflow);
 }
 
 // The counts c(i, j) of the (owned partition i, source j) pairs from the received counts messages
-// rc[j NC + i], staged in LDS (F = W QL <= 1024 pairs), each clamped to what fits in source j's block
-// of B, so that nothing downstream leaves the padded receive buffers when a block overflowed (the
-// flag then reruns the join), and the pair's first element in the block (partition-major within
-// each source). Flags a source whose block overflowed (wb > 0: its words, at QL, must fit wb too)
-// or whose status (at QL + 1) is nonzero.
+// rc[j NC + i] (F = W QL <= 1024 pairs, in LDS), each clamped to what fits in source j's block of
+// B, so that nothing downstream leaves the padded receive buffers when a block overflowed (the flag
+// then reruns the join), and the pair's first element in the block (partition-major within each
+// source: one block scan per source). Flags a source whose block overflowed (wb > 0: its words, at
+// QL, must fit wb too) or whose status (at QL + 1) is nonzero. All 1024 threads take part.
 __device__ __forceinline__ void pjx_pairs(const uint64_t* __restrict__ rc, uint32_t W, uint32_t QL, uint32_t NC,
-                                          uint64_t B, uint64_t wb, uint32_t* cnt, uint32_t* first, uint64_t* flag) {
-    for (uint32_t j = threadIdx.x; j < W; j += blockDim.x) {
-        uint64_t f = 0, c = 0;
-        for (uint32_t q = 0; q < QL; q++) {
-            const uint64_t v = rc[(uint64_t) j * NC + q];
-            cnt[q * W + j]   = (uint32_t) (c < B ? min<uint64_t>(v, B - c) : 0u);
-            first[q * W + j] = (uint32_t) min<uint64_t>(c, B);
-            c += v;
+                                          uint64_t B, uint64_t wb, uint32_t* cnt, uint32_t* first, uint32_t* wsum,
+                                          uint64_t* flag) {
+    const uint32_t i = threadIdx.x;
+    for (uint32_t j = 0; j < W; j++) {
+        const uint32_t v = i < QL ? (uint32_t) rc[(uint64_t) j * NC + i] : 0u;
+        uint32_t       total;
+        const uint32_t c = block_excl_scan(v, wsum, total);
+        if (i < QL) {
+            cnt[i * W + j]   = (uint32_t) (c < B ? min<uint64_t>(v, B - c) : 0u);
+            first[i * W + j] = (uint32_t) min<uint64_t>(c, B);
         }
-        if (c > B || (wb && rc[(uint64_t) j * NC + QL] > wb)) f |= kPjOverflow;
-        if (rc[(uint64_t) j * NC + QL + 1]) f |= kPjPeerFailed;
-        if (f) atomicOr((unsigned long long*) flag, (unsigned long long) f);
+        if (i == 0) {
+            uint64_t f = 0;
+            if (total > B || (wb && rc[(uint64_t) j * NC + QL] > wb)) f |= kPjOverflow;
+            if (rc[(uint64_t) j * NC + QL + 1]) f |= kPjPeerFailed;
+            if (f) atomicOr((unsigned long long*) flag, (unsigned long long) f);
+        }
     }
     __syncthreads();
 }
@@ -3960,8 +3982,8 @@ __global__ __launch_bounds__(1024) void k_pjx_rtab(const uint64_t* __restrict__ 
                                                    uint32_t* __restrict__ lsO, uint32_t* __restrict__ swO,
                                                    uint64_t* flag) {
     __shared__ uint32_t wsum[16];
-    __shared__ uint32_t cnt[1024], first[1024], tot[1024];
-    pjx_pairs(rc, W, QL, NC, BR, 0, cnt, first, flag);
+    __shared__ uint32_t cnt[1024], first[1024];
+    pjx_pairs(rc, W, QL, NC, BR, 0, cnt, first, wsum, flag);
     const uint32_t i = threadIdx.x;
     uint32_t       t = 0;
     if (i < QL)
@@ -3970,7 +3992,6 @@ __global__ __launch_bounds__(1024) void k_pjx_rtab(const uint64_t* __restrict__ 
     const uint32_t pos = block_excl_scan(i < QL ? t : 0u, wsum, total);  // list start of partition i
     if (i < QL) {
         lsO[i]     = pos;
-        tot[i]     = t;
         uint32_t p = pos;
         for (uint32_t j = 0; j < W; j++) {
             int64_t* e = tab + 4 * ((uint64_t) i * W + j);
@@ -3982,8 +4003,7 @@ __global__ __launch_bounds__(1024) void k_pjx_rtab(const uint64_t* __restrict__ 
         }
     }
     if (i == 0) lsO[QL] = total;
-    __syncthreads();
-    const uint32_t sw = i < QL ? (tot[i] + bsw - 1) / bsw : 0u;
+    const uint32_t sw = i < QL ? (t + bsw - 1) / bsw : 0u;
     const uint32_t so = block_excl_scan(sw, wsum, total);
     if (i < QL) swO[i] = so;
     if (i == 0) swO[QL] = total;
@@ -3991,51 +4011,56 @@ __global__ __launch_bounds__(1024) void k_pjx_rtab(const uint64_t* __restrict__ 
 
 // Survivors of this rank's probe items, item it of destination j (j = its partition / QL, k its
 // index among j's items) into j's blocks: its words at j * BW + (sofs[it] - bound[j QL]), its NSUB
-// run counts at (j * BI + k) * NSUB. One wave per item; I = item_start[F] on the device.
+// run counts at (j * BI + k) * NSUB; destination `own` (this rank; -1: none) straight into the
+// receive buffers own_out / own_cnt at the same positions. One wave per item; I = item_start[F]
+// on the device.
 __global__ __launch_bounds__(256) void k_pjx_surv_pack(const uint32_t* __restrict__ surv, const uint64_t* __restrict__ region,
                                                        const uint32_t* __restrict__ tot, const uint64_t* __restrict__ sofs,
                                                        const uint32_t* __restrict__ item_start, const uint64_t* __restrict__ bound,
                                                        const uint32_t* __restrict__ cnt, uint32_t F, uint32_t QL, uint32_t NSUB,
                                                        uint64_t BI, uint64_t BW, uint32_t* __restrict__ out,
-                                                       uint32_t* __restrict__ out_cnt, uint64_t* flag) {
+                                                       uint32_t* __restrict__ out_cnt, int own, uint32_t* __restrict__ own_out,
+                                                       uint32_t* __restrict__ own_cnt, uint64_t* flag) {
     const uint32_t I    = item_start[F];
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wv   = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint32_t nw   = (gridDim.x * blockDim.x) >> 6;
     bool           over = false;
     for (uint32_t it = wv; it < I; it += nw) {
-        const uint32_t j = find_q(item_start, F, it) / QL;
-        const uint64_t k = it - item_start[j * QL];
-        const uint64_t w = sofs[it] - bound[j * QL];  // the item's first word in j's block
-        const uint32_t c = tot[it];
+        const uint32_t j  = find_q(item_start, F, it) / QL;
+        const uint64_t k  = it - item_start[j * QL];
+        const uint64_t w  = sofs[it] - bound[j * QL];  // the item's first word in j's block
+        const uint32_t c  = tot[it];
+        uint32_t*      oc = (int) j == own ? own_cnt : out_cnt;
         if (k >= BI || w + c > BW) {  // (does not fit: the item goes with no survivors, flagged)
             over = true;
             if (k < BI)
-                for (uint32_t s = lane; s < NSUB; s += 64) out_cnt[(j * BI + k) * NSUB + s] = 0;
+                for (uint32_t s = lane; s < NSUB; s += 64) oc[(j * BI + k) * NSUB + s] = 0;
             continue;
         }
         const uint64_t src = region[it], dst = j * BW + w;
-        for (uint32_t x = lane; x < c; x += 64) out[dst + x] = surv[src + x];
-        for (uint32_t s = lane; s < NSUB; s += 64) out_cnt[(j * BI + k) * NSUB + s] = cnt[(uint64_t) it * NSUB + s];
+        uint32_t*      o   = (int) j == own ? own_out : out;
+        for (uint32_t x = lane; x < c; x += 64) o[dst + x] = surv[src + x];
+        for (uint32_t s = lane; s < NSUB; s += 64) oc[(j * BI + k) * NSUB + s] = cnt[(uint64_t) it * NSUB + s];
     }
     if (over && lane == 0) atomicOr((unsigned long long*) flag, (unsigned long long) kPjOverflow);
 }
 
-// The owner's survivor tables (one block): per (owned partition i, source j) pair tab2 = {first
-// received item (in j's block of BI), items, first output item}, istart[QL + 1], and ritems[j] (the
-// valid items of source j's block).
+// The owner's survivor tables (one block of 1024 threads): per (owned partition i, source j) pair
+// tab2 = {first received item (in j's block of BI), items, first output item}, istart[QL + 1], and
+// ritems[j] (the valid items of source j's block).
 __global__ __launch_bounds__(1024) void k_pjx_stab(const uint64_t* __restrict__ rc, uint32_t W, uint32_t QL, uint32_t NC,
                                                    uint64_t BI, uint64_t BW, uint32_t* __restrict__ tab2,
                                                    uint32_t* __restrict__ istart, uint32_t* __restrict__ ritems,
                                                    uint64_t* flag) {
     __shared__ uint32_t wsum[16];
     __shared__ uint32_t cnt[1024], first[1024];
-    pjx_pairs(rc, W, QL, NC, BI, BW, cnt, first, flag);
+    pjx_pairs(rc, W, QL, NC, BI, BW, cnt, first, wsum, flag);
     const uint32_t i = threadIdx.x;
-    for (uint32_t j = threadIdx.x; j < W; j += blockDim.x) {
-        uint32_t c = 0;
-        for (uint32_t q = 0; q < QL; q++) c += cnt[q * W + j];
-        ritems[j] = c;
+    for (uint32_t j = 0; j < W; j++) {  // (block-uniform: every thread takes part in the scans)
+        uint32_t total;
+        (void) block_excl_scan(i < QL ? cnt[i * W + j] : 0u, wsum, total);
+        if (i == 0) ritems[j] = total;
     }
     uint32_t t = 0;
     if (i < QL)
@@ -4059,31 +4084,35 @@ __global__ __launch_bounds__(1024) void k_pjx_stab(const uint64_t* __restrict__ 
 // The join's exchange sizes, for the next join's plan: out = {flag, the largest R block (chunks),
 // survivor item block and word block this rank sent or received} (all-reduced with MAX over the
 // ranks afterwards). rc1 / rc2: the received counts messages; ls / is / bd: this rank's R list
-// starts, item starts and survivor word bounds (what it sent).
-__global__ void k_pjx_stat(const uint64_t* __restrict__ rc1, const uint64_t* __restrict__ rc2, const uint32_t* __restrict__ ls,
-                           const uint32_t* __restrict__ is, const uint64_t* __restrict__ bd, uint32_t W, uint32_t QL,
-                           uint32_t NC, const uint64_t* flag, uint64_t* __restrict__ out) {
-    if (threadIdx.x != 0) return;
-    uint64_t mr = 0, mi = 0, mw = 0;
-    for (uint32_t j = 0; j < W; j++) {
-        uint64_t r = 0, it = 0;
-        for (uint32_t q = 0; q < QL; q++) {
-            r += rc1[(uint64_t) j * NC + q];
-            it += rc2[(uint64_t) j * NC + q];
-        }
-        mr = max(mr, max(r, (uint64_t) (ls[(j + 1) * QL] - ls[j * QL])));
-        mi = max(mi, max(it, (uint64_t) (is[(j + 1) * QL] - is[j * QL])));
+// starts, item starts and survivor word bounds (what it sent). One block of 1024 threads.
+__global__ __launch_bounds__(1024) void k_pjx_stat(const uint64_t* __restrict__ rc1, const uint64_t* __restrict__ rc2,
+                                                   const uint32_t* __restrict__ ls, const uint32_t* __restrict__ is,
+                                                   const uint64_t* __restrict__ bd, uint32_t W, uint32_t QL, uint32_t NC,
+                                                   const uint64_t* flag, uint64_t* __restrict__ out) {
+    __shared__ uint32_t wsum[16];
+    const uint32_t i  = threadIdx.x;
+    uint64_t       mr = 0, mi = 0, mw = 0;
+    for (uint32_t j = 0; j < W; j++) {  // (block-uniform)
+        uint32_t r, it;
+        (void) block_excl_scan(i < QL ? (uint32_t) rc1[(uint64_t) j * NC + i] : 0u, wsum, r);
+        (void) block_excl_scan(i < QL ? (uint32_t) rc2[(uint64_t) j * NC + i] : 0u, wsum, it);
+        mr = max(mr, max((uint64_t) r, (uint64_t) (ls[(j + 1) * QL] - ls[j * QL])));
+        mi = max(mi, max((uint64_t) it, (uint64_t) (is[(j + 1) * QL] - is[j * QL])));
         mw = max(mw, max(rc2[(uint64_t) j * NC + QL], bd[(j + 1) * QL] - bd[j * QL]));
     }
-    out[0] = *flag;
-    out[1] = mr;
-    out[2] = mi;
-    out[3] = mw;
+    if (i == 0) {
+        out[0] = *flag;
+        out[1] = mr;
+        out[2] = mi;
+        out[3] = mw;
+    }
 }
 
 void launch_pjx_gather(const uint32_t* pool, const uint32_t* list, const uint32_t* lstart, uint32_t F, uint32_t QL,
-                       uint64_t BR, void* out, uint32_t* ent, uint64_t* flag, hipStream_t st) {
-    k_pjx_gather<<<4096, 256, 0, st>>>(pool, list, lstart, F, QL, BR, (uint4*) out, ent, flag);
+                       uint32_t W, uint64_t BR, void* out, uint32_t* ent, int own, void* own_out, uint32_t* own_ent,
+                       uint64_t* flag, hipStream_t st) {
+    k_pjx_gather<<<4096, 256, 0, st>>>(pool, list, lstart, F, QL, W, BR, (uint4*) out, ent, own, (uint4*) own_out,
+                                       own_ent, flag);
 }
 
 void launch_pjx_rtab(const uint64_t* rc, uint32_t W, uint32_t QL, uint32_t NC, uint64_t BR, uint32_t bsw,
@@ -4094,9 +4123,9 @@ void launch_pjx_rtab(const uint64_t* rc, uint32_t W, uint32_t QL, uint32_t NC, u
 void launch_pjx_surv_pack(const uint32_t* surv, const uint64_t* region, const uint32_t* tot, const uint64_t* sofs,
                           const uint32_t* item_start, const uint64_t* bound, const uint32_t* cnt, uint32_t F,
                           uint32_t QL, uint32_t NSUB, uint64_t BI, uint64_t BW, uint32_t* out, uint32_t* out_cnt,
-                          uint64_t* flag, hipStream_t st) {
+                          int own, uint32_t* own_out, uint32_t* own_cnt, uint64_t* flag, hipStream_t st) {
     k_pjx_surv_pack<<<2048, 256, 0, st>>>(surv, region, tot, sofs, item_start, bound, cnt, F, QL, NSUB, BI, BW, out,
-                                          out_cnt, flag);
+                                          out_cnt, own, own_out, own_cnt, flag);
 }
 
 void launch_pjx_stab(const uint64_t* rc, uint32_t W, uint32_t QL, uint32_t NC, uint64_t BI, uint64_t BW,
@@ -4107,7 +4136,7 @@ void launch_pjx_stab(const uint64_t* rc, uint32_t W, uint32_t QL, uint32_t NC, u
 void launch_pjx_stat(const uint64_t* rc1, const uint64_t* rc2, const uint32_t* ls, const uint32_t* is,
                      const uint64_t* bd, uint32_t W, uint32_t QL, uint32_t NC, const uint64_t* flag, uint64_t* out,
                      hipStream_t st) {
-    k_pjx_stat<<<1, 64, 0, st>>>(rc1, rc2, ls, is, bd, W, QL, NC, flag, out);
+    k_pjx_stat<<<1, 1024, 0, st>>>(rc1, rc2, ls, is, bd, W, QL, NC, flag, out);
 }
 
 // ===================================================================== launch wrappers

@@ -151,6 +151,10 @@ int Engine::join_partitioned(const hwbrj_exchange_t* x, int rank, int world, con
     };
     // counts exchanges: QL partition counts, a total, the status, this rank's |S| and |R| shards
     const uint32_t NC = QL + 4;
+    // native: a rank's own R-chunk and survivor blocks are written by the gather / pack kernels
+    // straight into its receive buffers, and the exchanges skip the copy to itself (HWBRJ_RCCL_SELF:
+    // through RCCL like the others)
+    const bool self_direct = native && !rccl_self_blocks();
     std::vector<double> ms(8, 0.0);
     auto lap = [&, t = std::chrono::steady_clock::now()](int k) mutable {
         const auto n = std::chrono::steady_clock::now();
@@ -323,7 +327,18 @@ int Engine::join_partitioned(const hwbrj_exchange_t* x, int rank, int world, con
             plan_mr = std::max<uint64_t>(plan_mr, std::max<uint64_t>(c, ls[(j + 1) * QL] - ls[j * QL]));
         }
         PJ_STAGE("R scatter");
-        launch_pj_gather(poolR.as<uint32_t>(), listR.as<uint32_t>(), ls[F], sendC, sendE, stream);
+        PjOwn own;  // (this rank's block to itself: straight into the receive buffers)
+        if (self_direct) {
+            uint64_t base = 0;  // its first receive chunk: every lower source's chunks come first
+            for (uint32_t j = 0; j < (uint32_t) rank; j++)
+                for (uint32_t i = 0; i < QL; i++) base += rcnt[(uint64_t) j * NC + i];
+            own.lo    = ls[rank * QL];
+            own.hi    = ls[(rank + 1) * QL];
+            own.delta = (int64_t) base - (int64_t) own.lo;
+            own.out   = recvC;
+            own.ent   = recvE;
+        }
+        launch_pj_gather(poolR.as<uint32_t>(), listR.as<uint32_t>(), ls[F], sendC, sendE, stream, own);
         PJ_STAGE("k_pj_gather");
     } else {
         for (uint32_t j = 0; j < W; j++) scnt[j * NC + QL + 1] = (uint64_t) (uint32_t) rc1;
@@ -341,6 +356,7 @@ int Engine::join_partitioned(const hwbrj_exchange_t* x, int rank, int world, con
             rbytes[j] = c * 128;
             RC += c;
         }
+        if (self_direct) sbytes[rank] = rbytes[rank] = 0;  // (written by k_pj_gather)
         if (native) {  // (allocated at RCmax before the counts step; with the R shards summing to at
                        // most nR_total, RC cannot exceed it: a bug guard)
             if (RC > RCmax) {
@@ -565,10 +581,28 @@ int Engine::join_partitioned(const hwbrj_exchange_t* x, int rank, int world, con
                     PJ_FAIL("item " + std::to_string(it) + " region or survivor scan inconsistent");
             if (so[I] != bnd[F]) PJ_FAIL("survivor scan total");
         }
+        PjOwn own;
+        uint64_t own_items = 0;  // (self_direct: this rank's items to itself, at receive item own_ri)
+        uint64_t own_ri = 0;
+        if (self_direct) {
+            uint64_t rw = 0;  // its first receive word / item: every lower source's come first
+            for (uint32_t j = 0; j < (uint32_t) rank; j++) {
+                rw += rcnt[(uint64_t) j * NC + QL];
+                for (uint32_t i = 0; i < QL; i++) own_ri += rcnt[(uint64_t) j * NC + i];
+            }
+            own.lo    = isS[rank * QL];
+            own.hi    = isS[(rank + 1) * QL];
+            own.delta = (int64_t) rw - (int64_t) bnd[rank * QL];
+            own.out   = recvS;
+            own_items = own.hi - own.lo;
+        }
         launch_pj_surv_pack(surv.as<uint32_t>(), pjRegion.as<uint64_t>(), pjTot.as<uint32_t>(), pjSoff.as<uint64_t>(),
-                            I, sendS, stream);
+                            I, sendS, stream, own);
         PJ_STAGE("k_pj_surv_pack");
         if (I) PJ_CHECK(hipMemcpyAsync(sendM, survcnt.p, (size_t) I * NSUB * 4, hipMemcpyDeviceToDevice, stream));
+        if (own_items)
+            PJ_CHECK(hipMemcpyAsync(recvM + own_ri * NSUB, survcnt.as<uint32_t>() + (uint64_t) own.lo * NSUB,
+                                    own_items * NSUB * 4, hipMemcpyDeviceToDevice, stream));
         return 0;
     };
     lap(4);
@@ -634,6 +668,7 @@ int Engine::join_partitioned(const hwbrj_exchange_t* x, int rank, int world, con
             rbytes[j] = rwords[j] * 4;
             ro += rwords[j];
         }
+        if (self_direct) sbytes[rank] = rbytes[rank] = 0;  // (written by k_pj_surv_pack)
     }
     PJ_XCHG(x->alltoallv(x->ctx, HWBRJ_PJ_S_SEND, soff.data(), sbytes.data(), HWBRJ_PJ_S_RECV, roff.data(), rbytes.data()),
             "survivors");
@@ -646,6 +681,7 @@ int Engine::join_partitioned(const hwbrj_exchange_t* x, int rank, int world, con
             rbytes[j] = ritems[j] * NSUB * 4;
             ri += ritems[j];
         }
+        if (self_direct) sbytes[rank] = rbytes[rank] = 0;  // (copied from survcnt)
     }
     PJ_XCHG(x->alltoallv(x->ctx, HWBRJ_PJ_M_SEND, soff.data(), sbytes.data(), HWBRJ_PJ_M_RECV, roff.data(), rbytes.data()),
             "survivor run counts");

@@ -266,9 +266,12 @@ int Engine::join_partitioned_async(const uint2* dR, uint64_t nR, uint64_t nR_tot
     if (pending_ && pending_stream_ != stream) PX_CHECK(hipStreamWaitEvent(stream, ev_[8], 0));
     PX_CHECK(hipEventRecord(pjEv_[2 * slot], stream));
     PX_CHECK(hipMemsetAsync(flag, 0, 8, stream));
+    // this rank's own blocks are written by k_pjx_gather / k_pjx_surv_pack straight into the
+    // receive buffers (no copy to itself; HWBRJ_RCCL_SELF: through RCCL like the others)
+    const int own = rccl_self_blocks() ? -1 : comm_rank_;
     std::vector<uint64_t> soff(W), sbytes(W), roff(W), rbytes(W);
     auto xchg = [&](int ss, int rs, uint64_t b, const char* what) -> int {
-        for (uint32_t j = 0; j < W; j++) soff[j] = roff[j] = j * b, sbytes[j] = rbytes[j] = b;
+        for (uint32_t j = 0; j < W; j++) soff[j] = roff[j] = j * b, sbytes[j] = rbytes[j] = (int) j == own ? 0 : b;
         if (x.alltoallv(x.ctx, ss, soff.data(), sbytes.data(), rs, roff.data(), rbytes.data())) {
             set_last_error(std::string("exchange failed: ") + what);
             return 20;
@@ -314,8 +317,8 @@ int Engine::join_partitioned_async(const uint2* dR, uint64_t nR, uint64_t nR_tot
     // ---- 2. R exchange: blocks of BR chunks
     if (const int rc = rccl_alltoall_u64_dev(this, rc1s, rc1r, NC)) return rc;
     if (!fail)
-        launch_pjx_gather(poolR.as<uint32_t>(), listR.as<uint32_t>(), lstartR.as<uint32_t>(), F, QL, p.BR, sendC,
-                          sendE, flag, stream);
+        launch_pjx_gather(poolR.as<uint32_t>(), listR.as<uint32_t>(), lstartR.as<uint32_t>(), F, QL, W, p.BR, sendC,
+                          sendE, own, recvC, recvE, flag, stream);
     if (const int rc = xchg(HWBRJ_PJ_R_SEND, HWBRJ_PJ_R_RECV, p.BR * 128, "R chunks")) return rc;
     if (const int rc = xchg(HWBRJ_PJ_R_SEND_ENT, HWBRJ_PJ_R_RECV_ENT, p.BR * 4, "R chunk entries")) return rc;
     // ---- 3. owned partitions: tables on the device, lists, build
@@ -389,7 +392,8 @@ int Engine::join_partitioned_async(const uint2* dR, uint64_t nR, uint64_t nR_tot
     if (!fail)
         launch_pjx_surv_pack(surv.as<uint32_t>(), pjRegion.as<uint64_t>(), pjTot.as<uint32_t>(),
                              pjSoff.as<uint64_t>(), istartS.as<uint32_t>(), pjBound.as<uint64_t>(),
-                             survcnt.as<uint32_t>(), F, QL, NSUB, p.BI, p.BW, sendS, sendM, flag, stream);
+                             survcnt.as<uint32_t>(), F, QL, NSUB, p.BI, p.BW, sendS, sendM, own, recvS, recvM, flag,
+                             stream);
     if (const int rc = xchg(HWBRJ_PJ_S_SEND, HWBRJ_PJ_S_RECV, p.BW * 4, "survivors")) return rc;
     if (const int rc = xchg(HWBRJ_PJ_M_SEND, HWBRJ_PJ_M_RECV, p.BI * NSUB * 4, "survivor run counts")) return rc;
     // ---- 7. the owner's survivor tables on the device, join

@@ -319,6 +319,7 @@ def test_partitioned_async_northstar_back_to_back(hw, cuda, rccl1):
     hw.generate_device(R, 2, g["r"], g["r"], 1.0, 12345)
     hw.generate_device(S, 2, INT_MAX, g["r"], g["q"], 54321)
     args = hw.BloomFilterArgs(hw.BLOCKED, g["m"], 1, g["B"])
+    i0 = rccl1.pj_async_info()  # (the counters are the Engine's, over every communicator)
     for _ in range(4):
         rccl1.join_partitioned_rccl_async(R, S, g["r"], args)
     sts = [rccl1.join_partitioned_wait() for _ in range(4)]
@@ -326,7 +327,8 @@ def test_partitioned_async_northstar_back_to_back(hw, cuda, rccl1):
     del R, S
     for st in sts:
         assert (st.filtered, st.matches) == (g["k1_filtered"], g["results"])
-    assert info["overflow_reruns"] == 0 and info["async_joins"] >= 3, info
+    assert info["overflow_reruns"] == i0["overflow_reruns"], (i0, info)
+    assert info["async_joins"] - i0["async_joins"] == 3 and info["sync_plan_joins"] - i0["sync_plan_joins"] == 1
     assert all(st.ms_total > 0 for st in sts[1:])
     assert info["BR"] >= info["last_r_block"] and info["BW"] >= info["last_word_block"], info
 
@@ -342,6 +344,7 @@ def test_partitioned_async_overflow_rerun_world1(hw, cuda, orc, rccl1, hook):
     dR, dS = to_dev(cuda, R), to_dev(cuda, S)
     args = hw.BloomFilterArgs(hw.BLOCKED, g["m"], 1, 1024)
     want = (g["rows"]["1024"][0], g["results"])
+    i0 = rccl1.pj_async_info()  # (the counters are the Engine's, over every communicator)
     hook(hw.HOOK_PJ_PLAN_DIV, 8)
     rccl1.join_partitioned_rccl_async(dR, dS, g["r"], args)  # (synchronous: makes the small plan)
     rccl1.join_partitioned_rccl_async(dR, dS, g["r"], args)  # (overflows)
@@ -349,7 +352,8 @@ def test_partitioned_async_overflow_rerun_world1(hw, cuda, orc, rccl1, hook):
         st = rccl1.join_partitioned_wait()
         assert (st.filtered, st.matches) == want
     i = rccl1.pj_async_info()
-    assert i["overflow_reruns"] == 1 and i["last_rerun_flag"] == 1 and i["plan_valid"] == 1, i
+    assert i["overflow_reruns"] - i0["overflow_reruns"] == 1 and i["last_rerun_flag"] == 1, (i0, i)
+    assert i["plan_valid"] == 1
     hw.set_test_hook(hw.HOOK_PJ_PLAN_DIV, 0)
     # the plan the rerun made under the hook is still too small: one more overflow, whose rerun
     # (hook off) makes a plan that holds
@@ -357,14 +361,14 @@ def test_partitioned_async_overflow_rerun_world1(hw, cuda, orc, rccl1, hook):
     st = rccl1.join_partitioned_wait()
     assert (st.filtered, st.matches) == want
     i2 = rccl1.pj_async_info()
-    assert i2["overflow_reruns"] == 2, i2
+    assert i2["overflow_reruns"] - i0["overflow_reruns"] == 2, (i0, i2)
     for _ in range(3):
         rccl1.join_partitioned_rccl_async(dR, dS, g["r"], args)
     for _ in range(3):
         st = rccl1.join_partitioned_wait()
         assert (st.filtered, st.matches) == want
     i3 = rccl1.pj_async_info()
-    assert i3["overflow_reruns"] == 2 and i3["async_joins"] - i2["async_joins"] == 3, (i2, i3)
+    assert i3["overflow_reruns"] == i2["overflow_reruns"] and i3["async_joins"] - i2["async_joins"] == 3, (i2, i3)
 
 
 def test_partitioned_async_failed_mode_world1(hw, cuda, orc, rccl1, hook):
@@ -381,6 +385,7 @@ def test_partitioned_async_failed_mode_world1(hw, cuda, orc, rccl1, hook):
     want = (g["rows"]["1024"][0], g["results"])
     with pytest.raises(RuntimeError, match="no partitioned join"):
         rccl1.join_partitioned_wait()
+    i0 = rccl1.pj_async_info()  # (the counters are the Engine's, over every communicator)
     rccl1.join_partitioned_rccl_async(dR, dS, g["r"], args)
     assert (lambda s: (s.filtered, s.matches))(rccl1.join_partitioned_wait()) == want
     hook(hw.HOOK_PJ_ASYNC_FAIL, 1)
@@ -388,7 +393,7 @@ def test_partitioned_async_failed_mode_world1(hw, cuda, orc, rccl1, hook):
     st = rccl1.join_partitioned_wait()
     assert (st.filtered, st.matches) == want
     i = rccl1.pj_async_info()
-    assert i["overflow_reruns"] == 1 and i["last_rerun_flag"] == 2, i
+    assert i["overflow_reruns"] - i0["overflow_reruns"] == 1 and i["last_rerun_flag"] == 2, (i0, i)
     hw.set_test_hook(hw.HOOK_PJ_ASYNC_FAIL, 0)
     # another shape: half of S
     half = S[: S.shape[0] // 2]
@@ -397,7 +402,7 @@ def test_partitioned_async_failed_mode_world1(hw, cuda, orc, rccl1, hook):
     rccl1.join_partitioned_rccl_async(dR, dH, g["r"], args)
     st = rccl1.join_partitioned_wait()
     assert (st.filtered, st.matches) == (filt, res)
-    assert rccl1.pj_async_info()["overflow_reruns"] == 2
+    assert rccl1.pj_async_info()["overflow_reruns"] - i0["overflow_reruns"] == 2
     for _ in range(8):
         rccl1.join_partitioned_rccl_async(dR, dH, g["r"], args)
     with pytest.raises(RuntimeError, match="too many"):
