@@ -27,6 +27,7 @@ import argparse
 import json
 import os
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -71,6 +72,9 @@ def parse():
                     help="N > 1 (or any process group): skip the extra legs that time the other "
                          "multi-GPU designs on the same ranks after the headline (alt_designs)")
     ap.add_argument("--alt-steps", type=int, default=5, help="timed joins per alt_designs leg")
+    ap.add_argument("--alt-timeout", type=float, default=150.0,
+                    help="seconds the alt_designs legs may take before the headline is printed without "
+                         "the rest and every rank exits (a collective that never completes)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the PCIe-inclusive end-to-end time")
     ap.add_argument("--cpu-sample", type=int, default=0,
@@ -246,16 +250,38 @@ def main():
         t = torch.tensor([elapsed, dev_ms], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, dev_ms = (float(x) for x in t.tolist())
-    # the other multi-GPU designs on the same ranks, after the headline (never its value)
+    out = headline_line(a, hw, torch, dist, rank, world, dR, dS, args, st, last, sums, elapsed, dev_ms,
+                        total_units, filtered, matches, ranks_agree, per_rank, shared) if rank == 0 else None
+    # the other multi-GPU designs on the same ranks, after the headline (never its value); a
+    # watchdog bounds them: if a leg has not finished in --alt-timeout seconds (a collective that
+    # never completes), rank 0 prints the headline with what the legs reported so far and every
+    # rank exits
     alt = None
     if dist and not a.no_alt_designs and not a.filter_bcast:
-        alt = alt_designs(a, hw, torch, dist, rank, world, local, dR, dS, args, shared)
+        alt = {}
 
-    if rank != 0:
-        if dist:
-            dist.destroy_process_group()
-        return
+        def expire():
+            if out is not None:
+                out["alt_designs"] = dict(alt, timeout_s=a.alt_timeout)
+                print(json.dumps(out), flush=True)
+            os._exit(0)
+        dog = threading.Timer(a.alt_timeout, expire)
+        dog.daemon = True
+        dog.start()
+        alt_designs(a, hw, torch, dist, rank, world, local, dR, dS, args, shared, alt)
+        dog.cancel()
+    if rank == 0:
+        out["alt_designs"] = alt
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
 
+
+def headline_line(a, hw, torch, dist, rank, world, dR, dS, args, st, last, sums, elapsed, dev_ms, total_units,
+                  filtered, matches, ranks_agree, per_rank, shared):
+    """Rank 0's bench line of the replicated design (its alt_designs are filled in by the caller)."""
+    nR, nS_total = a.r_size, a.s_size
+    nS = dS.shape[0]
     K = max(a.steps, 1)
     mean = {k: v / K for k, v in sums.items()}
     # Roofline (SURVEY.md s8(d)): ALG_BYTES = sizeof(tuple_t) * (|R| + |S|), every input tuple read
@@ -345,13 +371,11 @@ def main():
                  "backend": dist.get_backend() if dist else None,
                  "shared_gpu_rehearsal": shared},
         "phase_ms": {k[3:]: round(v, 4) for k, v in mean.items()},
-        "alt_designs": alt,
+        "alt_designs": None,
         "published_ref": {"value": 3.98e8, "config": "blocked B=512 k=1 m=2^30, 2x Xeon Gold 6226 "
                           "48 threads (thesis data, BASELINE.md)"},
     }
-    print(json.dumps(out), flush=True)
-    if dist:
-        dist.destroy_process_group()
+    return out
 
 
 def pj_async_steps(pjoin, dR, dS, nR, args, K, depth=8):
@@ -369,7 +393,7 @@ def pj_async_steps(pjoin, dR, dS, nR, args, K, depth=8):
     return out
 
 
-def alt_designs(a, hw, torch, dist, rank, world, local, dR, dS, args, shared):
+def alt_designs(a, hw, torch, dist, rank, world, local, dR, dS, args, shared, out):
     """The designs the headline does not run, timed on the same ranks and shards right after it, so
     one multi-GPU run decides between them:
       bcast        the replicated design with the north_star's bitmap broadcast: rank 0 builds the
@@ -389,8 +413,8 @@ def alt_designs(a, hw, torch, dist, rank, world, local, dR, dS, args, shared):
     nR, nS_total = a.r_size, a.s_size
     K = max(1, min(a.steps, a.alt_steps))
     cdev = "cpu" if shared else "cuda"
-    out = {"steps": K, "what": "the other multi-GPU designs on the same ranks and shards after the "
-                               "headline's timed region (DESIGN.md s6); value = |S| / the slowest rank"}
+    out.update({"steps": K, "what": "the other multi-GPU designs on the same ranks and shards after the "
+                                    "headline's timed region (DESIGN.md s6); value = |S| / the slowest rank"})
 
     def gather_counts(st):
         c = torch.tensor([st.filtered, st.matches], dtype=torch.int64, device=cdev)

@@ -413,3 +413,17 @@ def test_partitioned_async_failed_mode_world1(hw, cuda, orc, rccl1, hook):
     # a single-GPU join after async ones on the same Engine is ordered after them and correct
     st = hw.join_device(dR, dS, args)
     assert (st.filtered, st.matches) == want
+
+
+def test_bench_alt_watchdog_world1(hw):
+    """bench.py's alt_designs legs run under a watchdog (a collective that never completes on a
+    node must not cost the headline): with --alt-timeout far below what the legs take, rank 0 still
+    prints the headline line, its parity ok, with alt_designs marked by the timeout, and the run
+    exits 0."""
+    g = GOLD["F3_grid"]
+    rc, out, err = torchrun(1, ["-r", g["r"], "-s", g["s"], "-m", g["m"], "--alt-timeout", "0.01"],
+                            {"HWBRJ_BENCH_DIST": "1"})
+    assert rc == 0, out[-2000:] + err[-3000:]
+    line = last_json(out)
+    assert (line["parity"]["filtered"], line["parity"]["matches"]) == (g["rows"]["1024"][0], g["results"])
+    assert line["alt_designs"]["timeout_s"] == 0.01, line["alt_designs"]
