@@ -46,7 +46,22 @@ for G in [int(x) for x in sys.argv[1:]] or [1, 8]:
         wall = (time.perf_counter() - t0) * 1e3
         if best is None or wall < best[0]:
             best = (wall, st)
+    # the async form: 8 joins enqueued back to back after the plan join, each join's device time
+    # from its HIP events, and the wall time of the 8
+    pjoin.join_partitioned_rccl_async(dRs, dS, nR, args)
+    pjoin.join_partitioned_wait()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(8):
+        pjoin.join_partitioned_rccl_async(dRs, dS, nR, args)
+    sts = [pjoin.join_partitioned_wait() for i in range(8)]
+    wall8 = (time.perf_counter() - t0) * 1e3 / 8
+    info = pjoin.pj_async_info()
     pjoin.comm_destroy()
+    ev = sorted(x.ms_total for x in sts)
+    print(f"G={G} partitioned rank (world 1, native RCCL, async): wall {wall8:.3f} ms per join over 8, events "
+          f"median {ev[4]:.3f} min {ev[0]:.3f} ms; reruns {info['overflow_reruns']}, plan BR {info['BR']} BI {info['BI']} "
+          f"BW {info['BW']}; counts {sts[-1].filtered} {sts[-1].matches}", flush=True)
     w, st = best
     print(f"G={G} partitioned rank (world 1, native RCCL): wall {w:.3f} ms: R pass {st.ms_r_scatter:.3f} R xchg {st.ms_r_index:.3f} "
           f"build {st.ms_build:.3f} S pass {st.ms_s_scatter:.3f} xchg(slices+surv) {st.ms_surv:.3f} join {st.ms_join:.3f} "
