@@ -2418,17 +2418,23 @@ __global__ __launch_bounds__(256) void k_join_split(const uint32_t* __restrict__
     nparts[job] = np;
 }
 
+#ifndef HWBRJ_JFLAT
+#define HWBRJ_JFLAT 0  // 1: the flat bitmap path in join_job (dev A/B: as fast as the fused path, DESIGN s9)
+#endif
+#define HWBRJ_JFLAT_LDS (HWBRJ_JFLAT ? 4 * kJoinWaves : 1)
 // One (job, part) of the join on workgroup slot blk; MIXED: survivor runs of both formats (below).
 // Adds this thread's matches to cnt_acc and (P.timing) the workgroup's probe ticks to tp_acc.
 template <bool MIXED>
 __device__ __forceinline__ void join_job(const JoinParams& P, const uint32_t blk, uint64_t& cnt_acc, uint64_t& tp_acc) {
     __shared__ __attribute__((aligned(16))) uint32_t tab[kJoinWords];  // bitmap or hash table
     __shared__ uint64_t dbase[kJoinDesc];  // run starts (byte offsets) of a batch: S survivor runs
-    __shared__ uint32_t dcnt[kJoinDesc];
+    __shared__ __attribute__((aligned(16))) uint32_t dcnt[kJoinDesc];
     __shared__ uint64_t rbase[kJoinDesc];  // R runs (one per build sweep of q)
-    __shared__ uint32_t rcnt[kJoinDesc];
-    __shared__ uint32_t pend[kJoinDesc + 1];  // hash path: piece boundaries inside an R batch
+    __shared__ __attribute__((aligned(16))) uint32_t rcnt[kJoinDesc];
+    __shared__ __attribute__((aligned(16))) uint32_t pend[kJoinDesc + 1];  // hash path: piece
+                                                                          // boundaries in an R batch
     __shared__ uint32_t dupflag, npieces;
+    __shared__ uint32_t fws[HWBRJ_JFLAT_LDS];  // flat path: wave totals of its four block scans
     const uint32_t NSUB = 1u << P.log2NSUB;
     uint32_t       job = blk, part = 0;  // workgroup j < jobs: part 0 of job j
 #ifndef HWBRJ_JXCD
@@ -2618,7 +2624,144 @@ __device__ __forceinline__ void join_job(const JoinParams& P, const uint32_t blk
 #endif
     constexpr int FR = HWBRJ_JFR, FW = HWBRJ_JFW;
     const uint32_t nRd = w1 - w0, nSd = i1 - i0;
-    if (!hashed && nRd <= (uint32_t) (kJoinWaves * FR) && nSd <= kJoinDesc) {
+#ifndef HWBRJ_JFU
+#define HWBRJ_JFU 32  // flat path: keys per lane per round
+#endif
+    constexpr uint32_t kFlatBlocks = 128;  // flat path: key blocks of 64 per side (8192 keys)
+    if (HWBRJ_JFLAT && !MIXED && !hashed && nRd <= kJoinDesc && nSd <= kJoinDesc) {
+        // Flat bitmap path. A job's R runs (one per build sweep) and survivor runs (one per probe
+        // item) are read as two flat key sequences: key f of a side is word f - pre[k] of its k-th
+        // non-empty run, and every lane loads keys f = f0 + 64 (wave + 4 u) + lane, so a whole side
+        // is one round of loads (FU per lane in flight) instead of one round per few runs. A lane
+        // finds its run without a search: the runs are compacted to the non-empty ones, block b of
+        // 64 keys records the run holding key 64 b (k0[b]) and a mask of the runs starting inside
+        // it, so k = k0[b] + the mask bits at or below the lane (mbcnt); the run's origin
+        // adj[k] = its byte offset - pre[k] * stride gives key f at adj[k] + f * stride. Two memory
+        // latencies per side-round (descriptors, keys) against four chained ones before.
+        uint32_t rn_t = 0, sn_t = 0;
+        uint64_t rb_t = 0, sb_t = 0;
+        if ((uint32_t) tid < nRd) {
+            const uint64_t r = (uint64_t) (w0 + tid) * NSUB + s;
+            rn_t             = P.r_cnt[r];
+            rb_t             = rtag(w0 + tid, P.r_off[r]) & ~kPk;
+        }
+        if ((uint32_t) tid < nSd) {
+            const uint32_t it    = i0 + tid;
+            const uint32_t local = it - qi0;
+            const uint32_t seg   = local / npc;
+            const uint32_t piece = local - seg * npc;
+            sn_t                 = P.surv_cnt[(uint64_t) it * NSUB + s];
+            sb_t = stag(P.item_base ? P.item_base[it] : (uint64_t) seg * P.surv_seg_stride + (uint64_t) (lq0 + piece * P.CH) * 32,
+                        P.surv_off[(uint64_t) it * NSUB + s]) & ~kPk;
+        }
+        uint64_t* const adjR = rbase;  // (the descriptor arrays are free on this path)
+        uint64_t* const adjS = dbase;
+        uint64_t* const mR   = (uint64_t*) rcnt;  // [kFlatBlocks] run starts inside block b
+        uint64_t* const mS   = (uint64_t*) dcnt;
+        uint16_t* const kR0  = (uint16_t*) pend;  // [kFlatBlocks] run holding key 64 b
+        uint16_t* const kS0  = kR0 + kFlatBlocks;
+        for (uint32_t i = tid; i < kJoinWords / 4; i += kJoinThreads) ((uint4*) tab)[i] = make_uint4(0, 0, 0, 0);
+        if ((uint32_t) tid < kFlatBlocks) mR[tid] = 0;
+        else if ((uint32_t) tid < 2 * kFlatBlocks) mS[tid - kFlatBlocks] = 0;
+        if (tid == 0) dupflag = 0;
+        // four exclusive block scans at once: R keys, R non-empty runs, S keys, S non-empty runs
+        const uint32_t sv4[4] = {rn_t, rn_t != 0, sn_t, sn_t != 0};
+        uint32_t       ex4[4], tot4[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint32_t inc = wave_incl_scan_dpp(sv4[k]);
+            ex4[k]             = inc - sv4[k];
+            if (lane == 63) fws[k * kJoinWaves + wave] = inc;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            uint32_t base = 0, t = 0;
+#pragma unroll
+            for (int w = 0; w < kJoinWaves; w++) {
+                const uint32_t x = fws[k * kJoinWaves + w];
+                base += w < wave ? x : 0u;
+                t += x;
+            }
+            ex4[k] += base;
+            tot4[k] = t;
+        }
+        const uint32_t tR = tot4[0], tS = tot4[2];
+        if (tR <= 64u * kFlatBlocks && tS <= 64u * kFlatBlocks) {  // (uniform)
+            // the compact runs' origins, block heads and start masks
+            auto place = [&](uint32_t n, uint64_t b, uint32_t p, uint32_t k, uint64_t* adj, uint16_t* k0, uint64_t* m) {
+                if (!n) return;
+                adj[k] = b - (uint64_t) p * kst;
+                for (uint32_t bb = (p + 63u) >> 6; (bb << 6) < p + n; bb++) k0[bb] = (uint16_t) k;
+                if (p & 63u)
+                    __hip_atomic_fetch_or(&m[p >> 6], 1ull << (p & 63u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            };
+            place(rn_t, rb_t, ex4[0], ex4[1], adjR, kR0, mR);
+            place(sn_t, sb_t, ex4[2], ex4[3], adjS, kS0, mS);
+            __syncthreads();
+            stamp(0);
+            // key f of a side: its run's origin + f * stride (wave-uniform block b = f >> 6)
+            auto flat_key = [&](const uint64_t* adj, const uint16_t* k0, const uint64_t* m, const uint8_t* base8,
+                                uint32_t f) -> uint32_t {
+                const uint32_t b  = f >> 6;
+                const uint64_t mb = m[b];
+                const uint32_t k  = k0[b] + __builtin_amdgcn_mbcnt_hi((uint32_t) (mb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t) mb, 0u)) +
+                                   (uint32_t) ((mb >> lane) & 1u);
+                return *(const u32_unaligned*) (base8 + adj[k] + (uint64_t) f * kst);
+            };
+            constexpr int FU = HWBRJ_JFU;
+            auto set = [&](uint32_t x) { __hip_atomic_fetch_or(&tab[x >> 5], 1u << (x & 31u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); };
+            for (uint32_t f0 = 0; f0 < tR; f0 += kJoinThreads * FU) {
+                uint32_t v[FU];
+#pragma unroll
+                for (int u = 0; u < FU; u++) {
+                    const uint32_t f = f0 + 64u * (wave + kJoinWaves * u) + lane;
+                    v[u]             = f < tR ? flat_key(adjR, kR0, mR, r8, f) : 0u;
+                }
+#pragma unroll
+                for (int u = 0; u < FU; u++)
+                    if (f0 + 64u * (wave + kJoinWaves * u) + lane < tR) set(key(SideR{}, v[u], rpk));
+            }
+            __syncthreads();
+            stamp(1);
+            {
+                uint32_t pc = 0;
+                for (uint32_t i = tid; i < kJoinWords / 4; i += kJoinThreads) {
+                    const uint4 q4 = ((const uint4*) tab)[i];
+                    pc += __builtin_popcount(q4.x) + __builtin_popcount(q4.y) + __builtin_popcount(q4.z) + __builtin_popcount(q4.w);
+                }
+                pc = __builtin_amdgcn_readlane(wave_incl_scan_dpp(pc), 63);
+                if (lane == 0 && pc) atomicAdd(&dupflag, pc);  // (dupflag: the set bits)
+            }
+            __syncthreads();
+            hashed = dupflag != tR;  // uniform: a duplicate R key sets fewer bits than the R keys
+            stamp(2);
+            if (!hashed) {
+                probe_begin();
+                for (uint32_t f0 = 0; f0 < tS; f0 += kJoinThreads * FU) {
+                    uint32_t v[FU];
+#pragma unroll
+                    for (int u = 0; u < FU; u++) {
+                        const uint32_t f = f0 + 64u * (wave + kJoinWaves * u) + lane;
+                        v[u]             = f < tS ? flat_key(adjS, kS0, mS, s8, f) : 0u;
+                    }
+#pragma unroll
+                    for (int u = 0; u < FU; u++)
+                        if (f0 + 64u * (wave + kJoinWaves * u) + lane < tS) {
+                            const uint32_t x = key(SideS{}, v[u], rpk);
+                            cnt += (tab[x >> 5] >> (x & 31u)) & 1u;
+                        }
+                }
+                stamp(3);
+                stamp(4);
+                probe_end();
+                done = true;
+            }
+        } else {
+            __syncthreads();  // (fws read before any later scan; the fused or walking path follows)
+        }
+    }
+    if (!done && !hashed && nRd <= (uint32_t) (kJoinWaves * FR) && nSd <= kJoinDesc) {
         // Fused bitmap path (every job of the north star): both descriptor sets in one phase, then
         // the loads of all R runs and of the first survivor runs are issued before any is used, so
         // a job costs two memory latencies (descriptors, data) instead of one per batch.
@@ -4433,6 +4576,8 @@ const char* kernel_build_knobs() {
         num("HWBRJ_JG12", HWBRJ_JG12, 0);
         num("HWBRJ_JBM", HWBRJ_JBM, 18);
         num("HWBRJ_JWPE", HWBRJ_JWPE, 0);
+        num("HWBRJ_JFLAT", HWBRJ_JFLAT, 0);
+        num("HWBRJ_JFU", HWBRJ_JFU, 32);
         num("HWBRJ_ABL_PROBE", HWBRJ_ABL_PROBE, 0);
         num("HWBRJ_PCO", HWBRJ_PCO, 1);
         num("HWBRJ_PCO_AUX", HWBRJ_PCO_AUX, 0);
