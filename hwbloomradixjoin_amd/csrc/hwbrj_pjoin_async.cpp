@@ -543,6 +543,10 @@ int hwbrj_join_partitioned_wait(hwbrj_stats_t* stats) {
 }
 
 int hwbrj_pj_async_info(uint64_t* out) {
+    if (!out) {
+        set_last_error("out must hold 16 words");
+        return 2;
+    }
     Engine* e = engine_for_current_device();
     if (!e) return 10;
     e->pj_async_info(out);

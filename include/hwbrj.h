@@ -259,8 +259,9 @@ int hwbrj_join_partitioned_rccl(const tuple_t * d_R, uint64_t nR, uint64_t nR_to
  * a device flag that is max-reduced over the ranks at the end of the join: its wait reruns it
  * synchronously on every rank (same counts; a new plan). A rank whose shard sizes or filter
  * differ from the plan's takes part with empty messages and flags the join the same way.
- * A collective: every rank makes the same calls in the same order. The inputs must stay valid and
- * unchanged until the join's wait returns.
+ * A collective: every rank makes the same calls in the same order (hwbrj_release and
+ * hwbrj_comm_destroy included: they drop the joins in flight and the plan's buffers). The inputs
+ * must stay valid and unchanged until the join's wait returns.
  *   hwbrj_join_partitioned_wait  collects the oldest enqueued join (FIFO): 0 or its error; stats:
  *                                counts, and ms_total = its device time between its first and last
  *                                operation on the join stream (0 phase times)
