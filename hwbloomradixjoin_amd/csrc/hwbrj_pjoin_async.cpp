@@ -442,7 +442,9 @@ int Engine::join_partitioned_async(const uint2* dR, uint64_t nR, uint64_t nR_tot
     // ---- 8. the flag and the block sizes, max over the ranks; the counts into this join's ring slot
     if (const int rc = rccl_allreduce_max_u64(this, stat, 4)) return rc;
     uint8_t* ring = pjRing.as<uint8_t>() + (size_t) slot * ring_slot_bytes();
-    PX_CHECK(hipMemcpyAsync(ring, small.p, ring_counts_bytes(), hipMemcpyDeviceToDevice, stream));
+    if (!fail)  // (the failed mode's counts are never read: its flag reruns the join; and after
+                // hwbrj_release the counts buffer may not exist)
+        PX_CHECK(hipMemcpyAsync(ring, small.p, ring_counts_bytes(), hipMemcpyDeviceToDevice, stream));
     PX_CHECK(hipMemcpyAsync(ring + ring_counts_bytes(), flag, 40, hipMemcpyDeviceToDevice, stream));
     PX_CHECK(hipEventRecord(pjEv_[2 * slot + 1], stream));
     PX_CHECK(hipEventRecord(ev_[8], stream));

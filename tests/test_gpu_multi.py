@@ -427,3 +427,32 @@ def test_bench_alt_watchdog_world1(hw):
     line = last_json(out)
     assert (line["parity"]["filtered"], line["parity"]["matches"]) == (g["rows"]["1024"][0], g["results"])
     assert line["alt_designs"]["timeout_s"] == 0.01, line["alt_designs"]
+
+
+def test_partitioned_async_after_release_world1(hw, cuda, orc, rccl1):
+    """hwbrj_release between async joins frees the plan's buffers: the next async join runs in the
+    failed mode (every collective with empty messages, flag 2), its wait reruns it synchronously
+    with the right counts and makes a new plan, and the join after that is async again. PRO (no
+    filter) and a sectorized filter, the two other slice paths."""
+    rng = np.random.default_rng(47)
+    nR, nS = 300007, 1200011
+    Rk = rng.permutation(nR).astype(np.int64) + 1
+    Sk = rng.integers(0, 2 * nR, size=nS)
+    R, S = rel(Rk), rel(Sk)
+    dR, dS = to_dev(cuda, R), to_dev(cuda, S)
+    for args in (None, hw.BloomFilterArgs.from_flag("sectorized", 1 << 24, 2, 512)):
+        want = _ref_counts(orc, R, S, args)
+        for _ in range(2):  # the plan join, then an async one
+            rccl1.join_partitioned_rccl_async(dR, dS, nR, args)
+        for _ in range(2):
+            st = rccl1.join_partitioned_wait()
+            assert (st.filtered, st.matches) == want, (args, st)
+        hw.lib().hwbrj_release()
+        i0 = rccl1.pj_async_info()
+        for _ in range(2):  # failed mode (rerun: a new plan), then async on the new plan
+            rccl1.join_partitioned_rccl_async(dR, dS, nR, args)
+            st = rccl1.join_partitioned_wait()
+            assert (st.filtered, st.matches) == want, (args, st)
+        i1 = rccl1.pj_async_info()
+        assert i1["overflow_reruns"] - i0["overflow_reruns"] == 1 and i1["last_rerun_flag"] == 2, (i0, i1)
+        assert i1["async_joins"] - i0["async_joins"] == 2 and i1["plan_valid"] == 1, (i0, i1)
