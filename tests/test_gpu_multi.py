@@ -413,6 +413,16 @@ def test_partitioned_async_failed_mode_world1(hw, cuda, orc, rccl1, hook):
     # a single-GPU join after async ones on the same Engine is ordered after them and correct
     st = hw.join_device(dR, dS, args)
     assert (st.filtered, st.matches) == want
+    # arguments the partitioned join refuses (basic k = 2: no partition slices), after a plan: the
+    # join runs in the failed mode, its wait reruns it synchronously, which returns the error; the
+    # plan is dropped and the next join (synchronous, a new plan) is right
+    rccl1.join_partitioned_rccl_async(dR, dS, g["r"], hw.BloomFilterArgs(hw.BASIC, 1 << 24, 2, 1024))
+    with pytest.raises(RuntimeError, match="partition slices"):
+        rccl1.join_partitioned_wait()
+    assert rccl1.pj_async_info()["plan_valid"] == 0
+    rccl1.join_partitioned_rccl_async(dR, dS, g["r"], args)
+    st = rccl1.join_partitioned_wait()
+    assert (st.filtered, st.matches) == want
 
 
 def test_bench_alt_watchdog_world1(hw):
