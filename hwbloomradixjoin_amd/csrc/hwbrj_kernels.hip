@@ -2424,17 +2424,32 @@ __global__ __launch_bounds__(256) void k_join_split(const uint32_t* __restrict__
 #define HWBRJ_JFLAT_LDS (HWBRJ_JFLAT ? 4 * kJoinWaves : 1)
 // One (job, part) of the join on workgroup slot blk; MIXED: survivor runs of both formats (below).
 // Adds this thread's matches to cnt_acc and (P.timing) the workgroup's probe ticks to tp_acc.
+// A join workgroup's LDS, declared once by the kernel: both join_job instantiations (uniform and
+// mixed formats) in one kernel share it (a static __shared__ array per instantiation would be
+// allocated twice).
+struct JoinShared {
+    __attribute__((aligned(16))) uint32_t tab[kJoinWords];  // bitmap or hash table
+    uint64_t dbase[kJoinDesc];  // run starts (byte offsets) of a batch: S survivor runs
+    __attribute__((aligned(16))) uint32_t dcnt[kJoinDesc];
+    uint64_t rbase[kJoinDesc];  // R runs (one per build sweep of q)
+    __attribute__((aligned(16))) uint32_t rcnt[kJoinDesc];
+    __attribute__((aligned(16))) uint32_t pend[kJoinDesc + 1];  // hash path: piece boundaries in an R batch
+    uint32_t dupflag, npieces;
+    uint32_t fws[HWBRJ_JFLAT_LDS];  // flat path: wave totals of its four block scans
+};
+
 template <bool MIXED>
-__device__ __forceinline__ void join_job(const JoinParams& P, const uint32_t blk, uint64_t& cnt_acc, uint64_t& tp_acc) {
-    __shared__ __attribute__((aligned(16))) uint32_t tab[kJoinWords];  // bitmap or hash table
-    __shared__ uint64_t dbase[kJoinDesc];  // run starts (byte offsets) of a batch: S survivor runs
-    __shared__ __attribute__((aligned(16))) uint32_t dcnt[kJoinDesc];
-    __shared__ uint64_t rbase[kJoinDesc];  // R runs (one per build sweep of q)
-    __shared__ __attribute__((aligned(16))) uint32_t rcnt[kJoinDesc];
-    __shared__ __attribute__((aligned(16))) uint32_t pend[kJoinDesc + 1];  // hash path: piece
-                                                                          // boundaries in an R batch
-    __shared__ uint32_t dupflag, npieces;
-    __shared__ uint32_t fws[HWBRJ_JFLAT_LDS];  // flat path: wave totals of its four block scans
+__device__ __forceinline__ void join_job(const JoinParams& P, const uint32_t blk, JoinShared& L, uint64_t& cnt_acc,
+                                         uint64_t& tp_acc) {
+    uint32_t* const tab   = L.tab;
+    uint64_t* const dbase = L.dbase;
+    uint32_t* const dcnt  = L.dcnt;
+    uint64_t* const rbase = L.rbase;
+    uint32_t* const rcnt  = L.rcnt;
+    uint32_t* const pend  = L.pend;
+    uint32_t* const fws   = L.fws;
+    uint32_t&       dupflag = L.dupflag;
+    uint32_t&       npieces = L.npieces;
     const uint32_t NSUB = 1u << P.log2NSUB;
     uint32_t       job = blk, part = 0;  // workgroup j < jobs: part 0 of job j
 #ifndef HWBRJ_JXCD
@@ -3149,21 +3164,31 @@ __device__ __forceinline__ void join_finish(const JoinParams& P, uint64_t cnt, u
     }
 }
 
+#ifndef HWBRJ_JONE
+#define HWBRJ_JONE 0  // 1: k_join runs the mixed-format jobs too, no k_join_mixed launch (A/B:
+                      // +0.012 ms of join, SGPR spills 166 -> 300; DESIGN s7 Round 5)
+#endif
 __global__ __launch_bounds__(kJoinThreads) HWBRJ_JOIN_ATTR void k_join(JoinParams P) {
-    if (P.r_pack3 && P.fmt_cnt && *P.fmt_cnt) return;
+    __shared__ JoinShared L;
+    const bool mixed = __builtin_amdgcn_readfirstlane(P.r_pack3 && P.fmt_cnt && *P.fmt_cnt ? 1u : 0u) != 0;
+    if (!HWBRJ_JONE && mixed) return;
     const uint64_t t_start = P.timing ? wall_clock64() : 0;
     uint64_t       cnt = 0, t_probe = 0;
-    join_job<false>(P, blockIdx.x, cnt, t_probe);
+    if (HWBRJ_JONE && mixed)
+        join_job<true>(P, blockIdx.x, L, cnt, t_probe);
+    else
+        join_job<false>(P, blockIdx.x, L, cnt, t_probe);
     join_finish(P, cnt, t_probe, t_start);
 }
 
 __global__ __launch_bounds__(kJoinThreads) void k_join_mixed(JoinParams P) {
+    __shared__ JoinShared L;
     if (!(P.r_pack3 && P.fmt_cnt && *P.fmt_cnt)) return;
     const uint64_t t_start = P.timing ? wall_clock64() : 0;
     uint64_t       cnt = 0, t_probe = 0;
     for (uint32_t b = blockIdx.x; b < P.jobs + kJoinExtra; b += gridDim.x) {
         __syncthreads();  // the previous job's LDS reads are done
-        join_job<true>(P, b, cnt, t_probe);
+        join_job<true>(P, b, L, cnt, t_probe);
     }
     join_finish(P, cnt, t_probe, t_start);
 }
@@ -4516,7 +4541,7 @@ void launch_join(const JoinParams& p0, uint32_t jobs, uint32_t* job_surv, hipStr
     k_join_split<<<(jobs + 255) / 256, 256, 0, st>>>(p.item_start, job_surv, p.log2NSUB, jobs, split,
                                                      p.nparts, p.extra, p.nextra, p.jsum);
     k_join<<<jobs + kJoinExtra, kJoinThreads, 0, st>>>(p);
-    k_join_mixed<<<std::min<uint32_t>(jobs + kJoinExtra, 1024u), kJoinThreads, 0, st>>>(p);
+    if (!HWBRJ_JONE) k_join_mixed<<<std::min<uint32_t>(jobs + kJoinExtra, 1024u), kJoinThreads, 0, st>>>(p);
 }
 
 uint32_t join_extra_tasks() { return kJoinExtra; }
@@ -4578,6 +4603,7 @@ const char* kernel_build_knobs() {
         num("HWBRJ_JWPE", HWBRJ_JWPE, 0);
         num("HWBRJ_JFLAT", HWBRJ_JFLAT, 0);
         num("HWBRJ_JFU", HWBRJ_JFU, 32);
+        num("HWBRJ_JONE", HWBRJ_JONE, 0);
         num("HWBRJ_ABL_PROBE", HWBRJ_ABL_PROBE, 0);
         num("HWBRJ_PCO", HWBRJ_PCO, 1);
         num("HWBRJ_PCO_AUX", HWBRJ_PCO_AUX, 0);

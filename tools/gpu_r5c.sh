@@ -8,6 +8,7 @@ OUT=gpurun_out/$1; mkdir -p $OUT
 [ "${TESTS}" = none ] || timeout -k 10 600 python -u -m pytest ${TESTS:-tests} -m gpu -x -q --timeout 200 --timeout-method thread > $OUT/gpu_tests.log 2>&1 || { echo TESTS_FAIL; tail -30 $OUT/gpu_tests.log; exit 1; }
 tail -1 $OUT/gpu_tests.log
 for v in jst4 jst5; do
+  [ -f tools/abl_so/libhwbrj_$v.so ] || continue
   HWBRJ_LIB=tools/abl_so/libhwbrj_$v.so HWBRJ_DBG=1 timeout -k 10 200 python3 tools/run_ns.py 4 > $OUT/$v.log 2>&1 \
     || { echo "STAMP_FAIL $v"; tail -5 $OUT/$v.log; exit 1; }
   echo "== $v"; grep -E "join cyc|^[0-9]" $OUT/$v.log | tail -3
