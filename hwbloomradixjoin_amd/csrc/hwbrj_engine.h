@@ -96,8 +96,10 @@ class Engine {
     // ---- the async partitioned join (hwbrj_pjoin_async.cpp; include/hwbrj.h) ----
     static constexpr int kPjDepth = 8;   // joins in flight (result ring slots)
     static constexpr int kPjKey   = 10;  // words of a plan's shape key
-    int  join_partitioned_async(const uint2* dR, uint64_t nR, uint64_t nR_total, const uint2* dS,
-                                uint64_t nS, const bloom_filter_args_t* args);
+    // x == nullptr: over this engine's RCCL communicator (no host wait); else the caller's
+    // exchange callbacks (host-synchronous exchanges, the same padded layout and plan)
+    int  join_partitioned_async(const hwbrj_exchange_t* x, int rank, int world, const uint2* dR, uint64_t nR,
+                                uint64_t nR_total, const uint2* dS, uint64_t nS, const bloom_filter_args_t* args);
     int  join_partitioned_wait(hwbrj_stats_t* st);
     void pj_async_info(uint64_t* out) const;
     // end of a synchronous native join asked for a plan (pj_make_plan()): a collective
@@ -119,7 +121,13 @@ class Engine {
         uint64_t BR = 0, BI = 0, BW = 0;  // block bounds: R chunks, survivor items, survivor words
         uint64_t key[kPjKey] = {};
     };
+    struct PjX {  // the transport of an async join
+        hwbrj_exchange_t x{};
+        bool             native = true;
+        int              rank = 0, world = 1;
+    };
     struct PjIn {
+        PjX                 xc;
         const uint2*        dR = nullptr;
         const uint2*        dS = nullptr;
         uint64_t            nR = 0, nR_total = 0, nS = 0;
@@ -137,10 +145,14 @@ class Engine {
     };
     bool pj_geom(int world, int rank, uint64_t nR, uint64_t nR_total, uint64_t nS,
                  const bloom_filter_args_t* args, PjGeom* G);
-    int  pj_async_alloc(const PjGeom& G, const PjPlan& p, bool all);
+    int  pj_async_alloc(const PjGeom& G, const PjPlan& p, bool all, const PjX& c);
+    int  pj_a2a_u64(const PjX& c, const uint64_t* d_send, uint64_t* d_recv, uint64_t n);
+    int  pj_max_dev(const PjX& c, uint64_t* d, uint64_t n);
+    int  pj_max_host(const PjX& c, uint64_t* h, uint64_t n);
     int  pj_establish_plan(const PjGeom& G, uint64_t mr, uint64_t mi, uint64_t mw, const uint64_t* key);
     int  pj_sync_join(const PjIn& in, hwbrj_stats_t* st);
     PjPlan                pj_plan_;
+    PjX                   pj_cur_;  // the transport of the synchronous join making a plan
     bloom_filter_args_t   pj_plan_args_{};
     bool                  pj_make_plan_ = false;
     bool                  pj_lost_      = false;  // the plan's buffers were released (this rank)

@@ -345,6 +345,11 @@ int Engine::join_partitioned(const hwbrj_exchange_t* x, int rank, int world, con
         PJ_XCHG(x->alltoall_u64(x->ctx, scnt.data(), rcnt.data(), NC), "R chunk counts");
         if (const int rc = peers(rcnt.data() + QL + 1, NC, rc1)) return rc;
         if (const int rc = check_r_total()) return rc;
+        for (uint32_t j = 0; j < W; j++) {  // (the async join's plan: the largest R block)
+            uint64_t c = 0;
+            for (uint32_t i = 0; i < QL; i++) c += rcnt[(uint64_t) j * NC + i];
+            plan_mr = std::max<uint64_t>(plan_mr, std::max<uint64_t>(c, ls[(j + 1) * QL] - ls[j * QL]));
+        }
     }
     const int rc2 = [&]() -> int {
         for (uint32_t j = 0; j < W; j++) {
@@ -784,7 +789,7 @@ int Engine::join_partitioned(const hwbrj_exchange_t* x, int rank, int world, con
     return read_join_counts(d_result, true, stream, small_h);
     }();
     lap(6);
-    if (native && pj_make_plan()) {  // (every rank: a collective)
+    if (pj_make_plan()) {  // (every rank: a collective, on the join's transport)
         PJ_CHECK(hipStreamSynchronize(stream));
         if (const int rc = pj_plan_from_sync(world, rank, nR, nR_total, nS, args, plan_mr, plan_mi, plan_mw))
             return rc7 ? rc7 : rc;

@@ -98,8 +98,8 @@ bool Engine::pj_geom(int world, int rank, uint64_t nR, uint64_t nR_total, uint64
 
 // The exchange buffers and tables of an async join under plan p (grow-only). `all`: also what only
 // a join that computes needs (a rank in the failed mode only exchanges).
-int Engine::pj_async_alloc(const PjGeom& G, const PjPlan& p, bool all) {
-    hwbrj_exchange_t x = native_exchange();
+int Engine::pj_async_alloc(const PjGeom& G, const PjPlan& p, bool all, const PjX& c) {
+    const hwbrj_exchange_t& x = c.x;
     const uint64_t   W = G.W, NSUB = G.NSUB, QL = G.QL;
     bool             ok = true;
     ok &= x.buffer(x.ctx, HWBRJ_PJ_R_SEND, W * p.BR * 128 + 16) != nullptr;
@@ -133,46 +133,88 @@ int Engine::pj_async_alloc(const PjGeom& G, const PjPlan& p, bool all) {
     return ok ? 0 : 4;
 }
 
-// Called by every rank at the end of a synchronous native partitioned join asked to make a plan
+// The collectives of an async join on either transport. Native: RCCL on the join stream, no host
+// wait. Callbacks: host-synchronous (the join stream drained, the words through the host).
+int Engine::pj_a2a_u64(const PjX& c, const uint64_t* d_send, uint64_t* d_recv, uint64_t n) {
+    if (c.native) return rccl_alltoall_u64_dev(this, d_send, d_recv, n);
+    const uint64_t        W = (uint64_t) c.world;
+    std::vector<uint64_t> hs(W * n), hr(W * n);
+    PX_CHECK(hipMemcpyAsync(hs.data(), d_send, W * n * 8, hipMemcpyDeviceToHost, own_stream_));
+    PX_CHECK(hipStreamSynchronize(own_stream_));
+    if (c.x.alltoall_u64(c.x.ctx, hs.data(), hr.data(), n) != 0) {
+        set_last_error("exchange failed: counts");
+        return 20;
+    }
+    PX_CHECK(hipMemcpyAsync(d_recv, hr.data(), W * n * 8, hipMemcpyHostToDevice, own_stream_));
+    PX_CHECK(hipStreamSynchronize(own_stream_));  // (hr is scoped)
+    return 0;
+}
+
+int Engine::pj_max_host(const PjX& c, uint64_t* h, uint64_t n) {
+    if (c.native) {  // (the agreement words: allocated by comm_init, >= 8 words)
+        uint64_t* d = agree_.as<uint64_t>();
+        if (!d || agree_.bytes < n * 8) {
+            set_last_error("no communicator words for the plan");
+            return 32;
+        }
+        PX_CHECK(hipMemcpyAsync(d, h, n * 8, hipMemcpyHostToDevice, own_stream_));
+        if (const int rc = rccl_allreduce_max_u64(this, d, n)) return rc;
+        PX_CHECK(hipMemcpyAsync(h, d, n * 8, hipMemcpyDeviceToHost, own_stream_));
+        PX_CHECK(hipStreamSynchronize(own_stream_));
+        return 0;
+    }
+    const uint64_t        W = (uint64_t) c.world;
+    std::vector<uint64_t> hs(W * n), hr(W * n);
+    for (uint64_t j = 0; j < W; j++) memcpy(&hs[j * n], h, n * 8);
+    if (c.x.alltoall_u64(c.x.ctx, hs.data(), hr.data(), n) != 0) {
+        set_last_error("exchange failed: plan words");
+        return 20;
+    }
+    for (uint64_t j = 0; j < W; j++)
+        for (uint64_t i = 0; i < n; i++) h[i] = std::max(h[i], hr[j * n + i]);
+    return 0;
+}
+
+int Engine::pj_max_dev(const PjX& c, uint64_t* d, uint64_t n) {
+    if (c.native) return rccl_allreduce_max_u64(this, d, n);
+    std::vector<uint64_t> h(n);
+    PX_CHECK(hipMemcpyAsync(h.data(), d, n * 8, hipMemcpyDeviceToHost, own_stream_));
+    PX_CHECK(hipStreamSynchronize(own_stream_));
+    if (const int rc = pj_max_host(c, h.data(), n)) return rc;
+    PX_CHECK(hipMemcpyAsync(d, h.data(), n * 8, hipMemcpyHostToDevice, own_stream_));
+    PX_CHECK(hipStreamSynchronize(own_stream_));  // (h is scoped)
+    return 0;
+}
+
+// Called by every rank at the end of a synchronous partitioned join asked to make a plan
 // (pj_make_plan_): this rank's largest blocks (R chunks, survivor items, survivor words it sent or
-// received) are all-reduced (MAX), the bounds get headroom, every rank allocates the padded buffers,
-// and the ranks agree (a second all-reduce) that all could: the plan is valid on all or on none.
+// received) are max-reduced over the ranks, the bounds get headroom, every rank allocates the padded
+// buffers, and the ranks agree (a second max-reduction) that all could: the plan is valid on all or
+// on none. (The transport is pj_cur_, the synchronous join's.)
 int Engine::pj_establish_plan(const PjGeom& G, uint64_t mr, uint64_t mi, uint64_t mw, const uint64_t* key) {
     pj_plan_.valid = false;
-    hipStream_t st = own_stream_;
-    PjPlan      p;
+    const PjX c    = pj_cur_;
+    PjPlan    p;
     memcpy(p.key, key, sizeof p.key);
-    uint64_t h[4] = {mr, mi, mw, 0};
-    // (pjX is tiny; if even it cannot be had, the agreement words (comm_init) carry a failed plan)
-    const bool have = pjX.ensure((8 + 4 * (uint64_t) G.W * G.NC) * 8);
-    uint64_t*  d    = have ? pjX.as<uint64_t>() + 1 : agree_.as<uint64_t>();
-    if (!have) h[0] = h[1] = h[2] = ~0ull;
-    PX_CHECK(hipMemcpyAsync(d, h, 24, hipMemcpyHostToDevice, st));
-    if (const int rc = rccl_allreduce_max_u64(this, d, 3)) return rc;
-    PX_CHECK(hipMemcpyAsync(h, d, 24, hipMemcpyDeviceToHost, st));
-    PX_CHECK(hipStreamSynchronize(st));
+    uint64_t h[3] = {mr, mi, mw};
+    if (const int rc = pj_max_host(c, h, 3)) return rc;
     auto     pad  = [](uint64_t v) { return ((v + v / 8 + 64 + 63) / 64) * 64; };  // +12.5 % + 64, in 64s
-    uint64_t fail = h[0] == ~0ull ? 1u : 0u;
-    if (!fail) {
-        p.BR = pad(h[0]);
-        p.BI = pad(h[1]);
-        p.BW = pad(h[2]);
-        if (const int div = test_hooks().pj_plan_div) {  // (tests: a plan too small, the next join overflows)
-            p.BR = std::max<uint64_t>(1, p.BR / (uint64_t) div);
-            p.BI = std::max<uint64_t>(1, p.BI / (uint64_t) div);
-            p.BW = std::max<uint64_t>(1, p.BW / (uint64_t) div);
-        }
-        // (27-bit chunk ids in the received entries; 32-bit item and word positions)
-        if ((uint64_t) G.W * p.BR >= (1ull << 27) || (uint64_t) G.W * p.BI >= (1ull << 31) ||
-            (uint64_t) G.W * p.BW >= (1ull << 32))
-            fail = 1;
-        else
-            fail = pj_async_alloc(G, p, true) ? 1u : 0u;
+    uint64_t fail = 0;
+    p.BR          = pad(h[0]);
+    p.BI          = pad(h[1]);
+    p.BW          = pad(h[2]);
+    if (const int div = test_hooks().pj_plan_div) {  // (tests: a plan too small, the next join overflows)
+        p.BR = std::max<uint64_t>(1, p.BR / (uint64_t) div);
+        p.BI = std::max<uint64_t>(1, p.BI / (uint64_t) div);
+        p.BW = std::max<uint64_t>(1, p.BW / (uint64_t) div);
     }
-    PX_CHECK(hipMemcpyAsync(d, &fail, 8, hipMemcpyHostToDevice, st));
-    if (const int rc = rccl_allreduce_max_u64(this, d, 1)) return rc;
-    PX_CHECK(hipMemcpyAsync(&fail, d, 8, hipMemcpyDeviceToHost, st));
-    PX_CHECK(hipStreamSynchronize(st));
+    // (27-bit chunk ids in the received entries; 32-bit item and word positions)
+    if ((uint64_t) G.W * p.BR >= (1ull << 27) || (uint64_t) G.W * p.BI >= (1ull << 31) ||
+        (uint64_t) G.W * p.BW >= (1ull << 32))
+        fail = 1;
+    else
+        fail = pj_async_alloc(G, p, true, c) ? 1u : 0u;
+    if (const int rc = pj_max_host(c, &fail, 1)) return rc;
     p.valid  = fail == 0;
     pj_lost_ = false;
     pj_plan_ = p;
@@ -198,23 +240,43 @@ int Engine::pj_drain() {
 int Engine::pj_sync_join(const PjIn& in, hwbrj_stats_t* st) {
     if (const int rc = pj_drain()) return rc;  // (the joins in flight finish before buffers grow)
     pj_make_plan_ = true;
-    const int rc  = join_partitioned_rccl(in.dR, in.nR, in.nR_total, in.dS, in.nS, in.has_args ? &in.args : nullptr, st);
+    pj_cur_       = in.xc;
+    const bloom_filter_args_t* a = in.has_args ? &in.args : nullptr;
+    const int rc = in.xc.native ? join_partitioned_rccl(in.dR, in.nR, in.nR_total, in.dS, in.nS, a, st)
+                                : join_partitioned(&in.xc.x, in.xc.rank, in.xc.world, in.dR, in.nR, in.nR_total,
+                                                   in.dS, in.nS, a, st, false);
     pj_make_plan_ = false;
     return rc;
 }
 
-int Engine::join_partitioned_async(const uint2* dR, uint64_t nR, uint64_t nR_total, const uint2* dS, uint64_t nS,
-                                   const bloom_filter_args_t* args) {
+int Engine::join_partitioned_async(const hwbrj_exchange_t* xa, int rank, int world, const uint2* dR, uint64_t nR,
+                                   uint64_t nR_total, const uint2* dS, uint64_t nS, const bloom_filter_args_t* args) {
     PX_CHECK(hipSetDevice(device_));
-    if (!comm_) {
-        set_last_error("no communicator on this device (hwbrj_comm_init)");
-        return 32;
+    PjX c;
+    if (!xa) {
+        if (!comm_) {
+            set_last_error("no communicator on this device (hwbrj_comm_init)");
+            return 32;
+        }
+        c.x     = native_exchange();
+        c.rank  = comm_rank_;
+        c.world = comm_world_;
+    } else {
+        if (world < 1 || rank < 0 || rank >= world) {
+            set_last_error("rank must lie in [0, world)");
+            return 2;
+        }
+        c.x      = *xa;
+        c.native = false;
+        c.rank   = rank;
+        c.world  = world;
     }
     if (pj_q_.size() >= (size_t) kPjDepth) {  // (every rank makes the same calls: fails alike)
         set_last_error("too many partitioned joins in flight (wait for the oldest first)");
         return 6;
     }
     PjPending e{};
+    e.in.xc       = c;
     e.in.dR       = dR;
     e.in.nR       = nR;
     e.in.nR_total = nR_total;
@@ -231,22 +293,22 @@ int Engine::join_partitioned_async(const uint2* dR, uint64_t nR, uint64_t nR_tot
         return 0;  // (its status is its wait's)
     }
     uint64_t key[kPjKey];
-    pj_shape(key, comm_world_, comm_rank_, nR, nR_total, nS, args);
+    pj_shape(key, c.world, c.rank, nR, nR_total, nS, args);
     PjGeom     G;
-    const bool geom_ok = pj_geom(comm_world_, comm_rank_, nR, nR_total, nS, args, &G);
+    const bool geom_ok = pj_geom(c.world, c.rank, nR, nR_total, nS, args, &G);
     // the failed mode: this rank's shapes are not the plan's (or its buffers were released); it
     // takes part in the join's collectives with empty messages, under the plan's geometry
     const bool fail = !geom_ok || pj_lost_ || memcmp(key, pj_plan_.key, sizeof key) != 0 || test_hooks().pj_async_fail;
     if (fail) {
         const bloom_filter_args_t* pa = pj_plan_.key[5] ? &pj_plan_args_ : nullptr;
-        if (!pj_geom(comm_world_, comm_rank_, pj_plan_.key[2], pj_plan_.key[3], pj_plan_.key[4], pa, &G)) return 2;
+        if (!pj_geom(c.world, c.rank, pj_plan_.key[2], pj_plan_.key[3], pj_plan_.key[4], pa, &G)) return 2;
     }
     const PjPlan& p = pj_plan_;
-    if (const int rc = pj_async_alloc(G, p, !fail)) return rc;  // (lookups: allocated with the plan)
+    if (const int rc = pj_async_alloc(G, p, !fail, c)) return rc;  // (lookups: allocated with the plan)
     const Geometry&  g = G.g;
     const uint32_t   W = G.W, QL = G.QL, F = G.F, NSUB = G.NSUB, NC = G.NC, NJ = QL * NSUB;
     hipStream_t      stream = own_stream_;
-    hwbrj_exchange_t x      = native_exchange();
+    const hwbrj_exchange_t& x = c.x;
     uint8_t*  sendC    = (uint8_t*) x.buffer(x.ctx, HWBRJ_PJ_R_SEND, 0);
     uint32_t* sendE    = (uint32_t*) x.buffer(x.ctx, HWBRJ_PJ_R_SEND_ENT, 0);
     uint8_t*  recvC    = (uint8_t*) x.buffer(x.ctx, HWBRJ_PJ_R_RECV, 0);
@@ -268,10 +330,17 @@ int Engine::join_partitioned_async(const uint2* dR, uint64_t nR, uint64_t nR_tot
     PX_CHECK(hipMemsetAsync(flag, 0, 8, stream));
     // this rank's own blocks are written by k_pjx_gather / k_pjx_surv_pack straight into the
     // receive buffers (no copy to itself; HWBRJ_RCCL_SELF: through RCCL like the others)
-    const int own = rccl_self_blocks() ? -1 : comm_rank_;
+    // (a callback transport moves every block itself, on its own stream: the join stream is drained
+    // before each of its calls)
+    const int own = !c.native || rccl_self_blocks() ? -1 : c.rank;
     std::vector<uint64_t> soff(W), sbytes(W), roff(W), rbytes(W);
+    auto drain = [&]() -> int {
+        if (!c.native) PX_CHECK(hipStreamSynchronize(stream));
+        return 0;
+    };
     auto xchg = [&](int ss, int rs, uint64_t b, const char* what) -> int {
         for (uint32_t j = 0; j < W; j++) soff[j] = roff[j] = j * b, sbytes[j] = rbytes[j] = (int) j == own ? 0 : b;
+        if (const int rc = drain()) return rc;
         if (x.alltoallv(x.ctx, ss, soff.data(), sbytes.data(), rs, roff.data(), rbytes.data())) {
             set_last_error(std::string("exchange failed: ") + what);
             return 20;
@@ -315,7 +384,7 @@ int Engine::join_partitioned_async(const uint2* dR, uint64_t nR, uint64_t nR_tot
         if (const int rc = fail_msg(rc1s)) return rc;
     }
     // ---- 2. R exchange: blocks of BR chunks
-    if (const int rc = rccl_alltoall_u64_dev(this, rc1s, rc1r, NC)) return rc;
+    if (const int rc = pj_a2a_u64(c, rc1s, rc1r, NC)) return rc;
     if (!fail)
         launch_pjx_gather(poolR.as<uint32_t>(), listR.as<uint32_t>(), lstartR.as<uint32_t>(), F, QL, W, p.BR, sendC,
                           sendE, own, recvC, recvE, flag, stream);
@@ -343,7 +412,7 @@ int Engine::join_partitioned_async(const uint2* dR, uint64_t nR, uint64_t nR_tot
         launch_build(bp, QL, stream);
     }
     // ---- 4. the whole filter on every rank
-    if (G.slice_mode && W > 1 && x.allgather(x.ctx, HWBRJ_PJ_SLICES, (uint64_t) QL * G.nseg * g.seg_words * 4)) {
+    if (G.slice_mode && W > 1 && (drain() || x.allgather(x.ctx, HWBRJ_PJ_SLICES, (uint64_t) QL * G.nseg * g.seg_words * 4))) {
         set_last_error("exchange failed: filter slices");
         return 20;
     }
@@ -388,7 +457,7 @@ int Engine::join_partitioned_async(const uint2* dR, uint64_t nR, uint64_t nR_tot
         return rc;
     }
     // ---- 6. survivor exchange: blocks of BW words and BI items
-    if (const int rc = rccl_alltoall_u64_dev(this, rc2s, rc2r, NC)) return rc;
+    if (const int rc = pj_a2a_u64(c, rc2s, rc2r, NC)) return rc;
     if (!fail)
         launch_pjx_surv_pack(surv.as<uint32_t>(), pjRegion.as<uint64_t>(), pjTot.as<uint32_t>(),
                              pjSoff.as<uint64_t>(), istartS.as<uint32_t>(), pjBound.as<uint64_t>(),
@@ -440,7 +509,7 @@ int Engine::join_partitioned_async(const uint2* dR, uint64_t nR, uint64_t nR_tot
         PX_CHECK(hipStreamSynchronize(stream));  // (h is scoped)
     }
     // ---- 8. the flag and the block sizes, max over the ranks; the counts into this join's ring slot
-    if (const int rc = rccl_allreduce_max_u64(this, stat, 4)) return rc;
+    if (const int rc = pj_max_dev(c, stat, 4)) return rc;
     uint8_t* ring = pjRing.as<uint8_t>() + (size_t) slot * ring_slot_bytes();
     if (!fail)  // (the failed mode's counts are never read: its flag reruns the join; and after
                 // hwbrj_release the counts buffer may not exist)
@@ -535,7 +604,18 @@ int hwbrj_join_partitioned_rccl_async(const tuple_t* d_R, uint64_t nR, uint64_t 
                                       uint64_t nS, const bloom_filter_args_t* args) {
     Engine* e = engine_for_current_device();
     if (!e) return 10;
-    return e->join_partitioned_async((const uint2*) d_R, nR, nR_total, (const uint2*) d_S, nS, args);
+    return e->join_partitioned_async(nullptr, 0, 1, (const uint2*) d_R, nR, nR_total, (const uint2*) d_S, nS, args);
+}
+
+int hwbrj_join_partitioned_async(const hwbrj_exchange_t* x, int rank, int world, const tuple_t* d_R, uint64_t nR,
+                                 uint64_t nR_total, const tuple_t* d_S, uint64_t nS, const bloom_filter_args_t* args) {
+    if (!x) {
+        set_last_error("no exchange (hwbrj_join_partitioned_rccl_async runs over the library's communicator)");
+        return 2;
+    }
+    Engine* e = engine_for_current_device();
+    if (!e) return 10;
+    return e->join_partitioned_async(x, rank, world, (const uint2*) d_R, nR, nR_total, (const uint2*) d_S, nS, args);
 }
 
 int hwbrj_join_partitioned_wait(hwbrj_stats_t* stats) {

@@ -209,6 +209,24 @@ def join_partitioned_rccl_async(R, S, nR_total: int, args=None) -> None:
     _err(rc, "hwbrj_join_partitioned_rccl_async")
 
 
+def join_partitioned_async(R, S, nR_total: int, args=None, exchange=None) -> None:
+    """The async partitioned join over torch.distributed callbacks (hwbrj_join_partitioned_async):
+    the same plan and padded layout as join_partitioned_rccl_async, with host-synchronous exchanges
+    (ranks may share a GPU: gloo). Collect with join_partitioned_wait; `exchange` (a TorchExchange)
+    must outlive the wait."""
+    _check_rel(R, S)
+    x = exchange or TorchExchange(R.device)
+    a = args._c() if args is not None else None
+    rc = lib().hwbrj_join_partitioned_async(ctypes.byref(x._c), x.rank, x.world, _ptr(R), R.shape[0],
+                                            int(nR_total), _ptr(S), S.shape[0],
+                                            ctypes.byref(a) if a is not None else None)
+    if x.error is not None:
+        e, x.error = x.error, None
+        raise RuntimeError(f"hwbrj_join_partitioned_async: exchange failed: {e!r}") from e
+    _err(rc, "hwbrj_join_partitioned_async")
+    return x
+
+
 def join_partitioned_wait() -> Stats:
     """The oldest enqueued async partitioned join's result (hwbrj_join_partitioned_wait); a join
     whose padded blocks overflowed on any rank is rerun synchronously here (same counts)."""
@@ -233,6 +251,10 @@ def _bind(L):
     L.hwbrj_join_partitioned_rccl_async.restype = ctypes.c_int
     L.hwbrj_join_partitioned_rccl_async.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
                                                     ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(_BloomArgs)]
+    L.hwbrj_join_partitioned_async.restype = ctypes.c_int
+    L.hwbrj_join_partitioned_async.argtypes = [ctypes.POINTER(_Exchange), ctypes.c_int, ctypes.c_int,
+                                               ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
+                                               ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(_BloomArgs)]
     L.hwbrj_join_partitioned_wait.restype = ctypes.c_int
     L.hwbrj_join_partitioned_wait.argtypes = [ctypes.POINTER(_Stats)]
     L.hwbrj_pj_async_info.restype = ctypes.c_int

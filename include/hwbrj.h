@@ -272,6 +272,14 @@ int hwbrj_join_partitioned_rccl(const tuple_t * d_R, uint64_t nR, uint64_t nR_to
 int hwbrj_join_partitioned_rccl_async(const tuple_t * d_R, uint64_t nR, uint64_t nR_total,
                                       const tuple_t * d_S, uint64_t nS,
                                       const bloom_filter_args_t * args);
+/* The async join over the caller's transport (the hwbrj_exchange_t callbacks of
+ * hwbrj_join_partitioned): the same plan, padded layout, device tables, overflow flag and failed
+ * mode, with the exchanges made by the callbacks (host-synchronous, so this form has host waits;
+ * it is what lets several ranks share one GPU in tests). The exchange's callbacks and context must
+ * stay valid until the join's wait returns. Collected by hwbrj_join_partitioned_wait. */
+int hwbrj_join_partitioned_async(const hwbrj_exchange_t * x, int rank, int world, const tuple_t * d_R,
+                                 uint64_t nR, uint64_t nR_total, const tuple_t * d_S, uint64_t nS,
+                                 const bloom_filter_args_t * args);
 int hwbrj_join_partitioned_wait(hwbrj_stats_t * stats);
 int hwbrj_pj_async_info(uint64_t * out /* 16 */);
 

@@ -466,3 +466,34 @@ def test_partitioned_async_after_release_world1(hw, cuda, orc, rccl1):
         i1 = rccl1.pj_async_info()
         assert i1["overflow_reruns"] - i0["overflow_reruns"] == 1 and i1["last_rerun_flag"] == 2, (i0, i1)
         assert i1["async_joins"] - i0["async_joins"] == 2 and i1["plan_valid"] == 1, (i0, i1)
+
+
+@pytest.mark.parametrize("scen,world", [("steady", 2), ("overflow", 2), ("shape", 2), ("fail1", 2), ("steady", 4),
+                                        ("overflow", 4)])
+def test_partitioned_async_ranks_shared_gpu(hw, scen, world):
+    """The async partitioned join with two and four ranks (hwbrj_join_partitioned_async over
+    torch.distributed gloo callbacks, every rank on the one GPU): the W > 1 parts of the padded layout -- destination
+    blocks found among the block starts, two sources per owner table, survivor blocks per source --
+    the plan max-reduced over the ranks, and the collective reruns: a plan too small (the flag set
+    on a rank reruns the join on both), a shard that changes size on one rank only (the failed mode
+    there), a rank forced into the failed mode. Counts summed over the ranks equal F3 (or, for the
+    changed shard, the synchronous join of the same shards)."""
+    g = GOLD["F3_grid"]
+    rc, out, err = torchrun(world, [scen, g["r"], g["s"], g["m"]], {}, timeout=300, script="pj_async_worker.py")
+    assert rc == 0, out[-2000:] + err[-3000:]
+    sums = [tuple(int(v) for v in l.split()[-2:]) for l in out.splitlines() if l.startswith("sum: ok ")]
+    info = [[int(v) for v in l.split()[1:]] for l in out.splitlines() if l.startswith("info: ")]
+    assert len(info) == 1, out[-2000:]
+    n_async, reruns, flag, plan_joins = info[0]
+    assert plan_joins == 1
+    want = (g["rows"]["1024"][0], g["results"])
+    if scen == "steady":
+        assert sums == [want] * 4 and (n_async, reruns) == (3, 0), out[-2000:]
+    elif scen == "overflow":
+        assert sums == [want] * 2 and (n_async, reruns, flag) == (1, 1, 1), out[-2000:]
+    elif scen == "fail1":
+        assert sums == [want] * 2 and (n_async, reruns, flag) == (1, 1, 2), out[-2000:]
+    else:
+        sync = [tuple(int(v) for v in l.split()[-2:]) for l in out.splitlines() if l.startswith("sync: ")]
+        assert sums[0] == want and sums[1] == sync[0] and sums[1] != want, out[-2000:]
+        assert (n_async, reruns, flag) == (1, 1, 2), out[-2000:]
