@@ -378,15 +378,19 @@ def headline_line(a, hw, torch, dist, rank, world, dR, dS, args, st, last, sums,
     return out
 
 
-def pj_async_steps(pjoin, dR, dS, nR, args, K, depth=8):
-    """K async partitioned joins (hwbrj_join_partitioned_rccl_async) back to back, at most `depth`
-    in flight: no host wait but the collection of the oldest. Their stats, in order."""
+def pj_async_steps(pjoin, dR, dS, nR, args, K, depth=8, x=None):
+    """K async partitioned joins (hwbrj_join_partitioned_rccl_async; with x, a pjoin.TorchExchange:
+    hwbrj_join_partitioned_async over its callbacks) back to back, at most `depth` in flight: no
+    host wait but the collection of the oldest. Their stats, in order."""
     out, inflight = [], 0
     for _ in range(K):
         if inflight == depth:
             out.append(pjoin.join_partitioned_wait())
             inflight -= 1
-        pjoin.join_partitioned_rccl_async(dR, dS, nR, args)
+        if x is None:
+            pjoin.join_partitioned_rccl_async(dR, dS, nR, args)
+        else:
+            pjoin.join_partitioned_async(dR, dS, nR, args, x)
         inflight += 1
     for _ in range(inflight):
         out.append(pjoin.join_partitioned_wait())
@@ -404,8 +408,9 @@ def alt_designs(a, hw, torch, dist, rank, world, local, dR, dS, args, shared, ou
                    callback transport when ranks share a GPU); host-synchronous, so timed by wall
                    clock between barriers, max over ranks;
       partitioned_async  the same join with padded exchanges and no host wait
-                   (hwbrj_join_partitioned_rccl_async; one GPU per rank): K joins back to back,
-                   wall clock between barriers, max over ranks.
+                   (hwbrj_join_partitioned_rccl_async; when ranks share a GPU, the same async join
+                   over the torch callbacks, host-synchronous): K joins back to back, wall clock
+                   between barriers, max over ranks.
     Each leg reports its ms per join, the probe-tuples/s that gives, and every rank's own
     (filtered, matches), whose sums must be the headline's counts. A failing leg is reported, and
     never stops the headline line."""
@@ -487,12 +492,13 @@ def alt_designs(a, hw, torch, dist, rank, world, local, dR, dS, args, shared, ou
     def partitioned_async():
         rlo, rhi = hw.shard_range(nR, rank, world)
         dRs = dR[rlo:rhi]
-        sts = pj_async_steps(pjoin, dRs, dS, nR, args, 2)  # (the plan join, then one async)
+        x = None if native else pjoin.TorchExchange(torch.device("cuda", local))
+        sts = pj_async_steps(pjoin, dRs, dS, nR, args, 2, x=x)  # (the plan join, then one async)
         per, tot = gather_counts(sts[-1])
         dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        sts = pj_async_steps(pjoin, dRs, dS, nR, args, K)
+        sts = pj_async_steps(pjoin, dRs, dS, nR, args, K, x=x)
         torch.cuda.synchronize()
         dist.barrier()
         if any((s.filtered, s.matches) != (sts[0].filtered, sts[0].matches) for s in sts):
@@ -505,10 +511,7 @@ def alt_designs(a, hw, torch, dist, rank, world, local, dR, dS, args, shared, ou
         out["bcast"] = {"skipped": "needs one GPU per rank (RCCL) and a slice filter"}
     if args is None or slice_filter:
         leg("partitioned", partitioned)
-        if native:
-            leg("partitioned_async", partitioned_async)
-        else:
-            out["partitioned_async"] = {"skipped": "needs one GPU per rank (RCCL)"}
+        leg("partitioned_async", partitioned_async)
     else:
         out["partitioned"] = {"skipped": "basic k > 1 has no partition slices"}
     if native:
