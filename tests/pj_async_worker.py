@@ -7,6 +7,7 @@ R and S range-sharded over the ranks, which share the one GPU. Scenario argv[1]:
   shape    after a plan, rank 1's S shard changes size alone (the failed mode on that rank): every
            rank reruns the join
   fail1    rank 1 runs the async join in the failed mode (HWBRJ_HOOK_PJ_ASYNC_FAIL)
+argv[5] (optional): the filter, "blocked" (k = 1, B = 1024; the default), "sect" or "pro".
 Rank 0 prints "sum: ok filtered matches" per join (each summed over the ranks) and the async-info
 deltas as "info: async reruns"; exit 3 with the library's error on stderr."""
 import os
@@ -35,7 +36,10 @@ def main():
     dS = torch.empty((hi - lo, 2), dtype=torch.int32, device="cuda")
     hw.generate_device_range(dR, r, rlo, 2, r, r, 1.0, 12345)
     hw.generate_device_range(dS, s, lo, 2, 2**31 - 1, r, 0.01, 54321)
-    args = hw.BloomFilterArgs(hw.BLOCKED, m, 1, 1024)
+    # (argv[5], optional: "pro" = no filter, "sect" = sectorized k = 2 B = 512; default blocked k = 1)
+    flt = sys.argv[5] if len(sys.argv) > 5 else "blocked"
+    args = {"blocked": hw.BloomFilterArgs(hw.BLOCKED, m, 1, 1024), "pro": None,
+            "sect": hw.BloomFilterArgs.from_flag("sectorized", m, 2, 512)}[flt]
     x = pjoin.TorchExchange(torch.device("cuda", 0))
 
     def report(sts):

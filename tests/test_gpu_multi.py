@@ -468,9 +468,10 @@ def test_partitioned_async_after_release_world1(hw, cuda, orc, rccl1):
         assert i1["async_joins"] - i0["async_joins"] == 2 and i1["plan_valid"] == 1, (i0, i1)
 
 
-@pytest.mark.parametrize("scen,world", [("steady", 2), ("overflow", 2), ("shape", 2), ("fail1", 2), ("steady", 4),
-                                        ("overflow", 4)])
-def test_partitioned_async_ranks_shared_gpu(hw, scen, world):
+@pytest.mark.parametrize("scen,world,flt", [("steady", 2, "blocked"), ("overflow", 2, "blocked"), ("shape", 2, "blocked"),
+                                            ("fail1", 2, "blocked"), ("steady", 4, "blocked"), ("overflow", 4, "blocked"),
+                                            ("steady", 2, "pro"), ("steady", 4, "sect")])
+def test_partitioned_async_ranks_shared_gpu(hw, scen, world, flt):
     """The async partitioned join with two and four ranks (hwbrj_join_partitioned_async over
     torch.distributed gloo callbacks, every rank on the one GPU): the W > 1 parts of the padded layout -- destination
     blocks found among the block starts, two sources per owner table, survivor blocks per source --
@@ -479,7 +480,7 @@ def test_partitioned_async_ranks_shared_gpu(hw, scen, world):
     there), a rank forced into the failed mode. Counts summed over the ranks equal F3 (or, for the
     changed shard, the synchronous join of the same shards)."""
     g = GOLD["F3_grid"]
-    rc, out, err = torchrun(world, [scen, g["r"], g["s"], g["m"]], {}, timeout=300, script="pj_async_worker.py")
+    rc, out, err = torchrun(world, [scen, g["r"], g["s"], g["m"], flt], {}, timeout=300, script="pj_async_worker.py")
     assert rc == 0, out[-2000:] + err[-3000:]
     sums = [tuple(int(v) for v in l.split()[-2:]) for l in out.splitlines() if l.startswith("sum: ok ")]
     info = [[int(v) for v in l.split()[1:]] for l in out.splitlines() if l.startswith("info: ")]
@@ -487,6 +488,16 @@ def test_partitioned_async_ranks_shared_gpu(hw, scen, world):
     n_async, reruns, flag, plan_joins = info[0]
     assert plan_joins == 1
     want = (g["rows"]["1024"][0], g["results"])
+    if flt != "blocked":  # (the single-GPU join of the same relations: the F3 rows hold blocked k = 1)
+        import torch
+        R = torch.empty((g["r"], 2), dtype=torch.int32, device="cuda")
+        S = torch.empty((g["s"], 2), dtype=torch.int32, device="cuda")
+        hw.generate_device_range(R, g["r"], 0, 2, g["r"], g["r"], 1.0, 12345)
+        hw.generate_device_range(S, g["s"], 0, 2, INT_MAX, g["r"], 0.01, 54321)
+        a = None if flt == "pro" else hw.BloomFilterArgs.from_flag("sectorized", g["m"], 2, 512)
+        st = hw.join_device(R, S, a)
+        want = (st.filtered, st.matches)
+        del R, S
     if scen == "steady":
         assert sums == [want] * 4 and (n_async, reruns) == (3, 0), out[-2000:]
     elif scen == "overflow":
