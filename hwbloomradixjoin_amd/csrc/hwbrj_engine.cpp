@@ -530,8 +530,9 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
         return 0;
     };
     HWBRJ_CHECK(mark(0, stream));
-    const bool ovl = dev_knobs().ovl && g.mode != MODE_GLOBAL && !basic_kk && !mat && !bcast;
-    if (ovl) {  // dev A/B: S pass on the side stream (its phases then show inside the R side's)
+    const bool ovl = (dev_knobs().ovl || (HWBRJ_OVL_ASYNC && !phase_ev_)) && g.mode != MODE_GLOBAL && !basic_kk &&
+                     !mat && !bcast;
+    if (ovl) {  // S pass on the side stream (with phase events, its phases would show inside the R side's)
         if (!ovl_stream_) {
             HWBRJ_CHECK(hipStreamCreateWithFlags(&ovl_stream_, hipStreamNonBlocking));
             HWBRJ_CHECK(hipEventCreateWithFlags(&ovl_ev_[0], hipEventDisableTiming));

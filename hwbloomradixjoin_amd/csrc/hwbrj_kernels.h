@@ -45,6 +45,13 @@ struct ScatterParams {
 #endif
 inline bool join_pack3(const Geometry& g) { return HWBRJ_PACK3 != 0 && g.sub_shift > 0 && g.hash_shift >= 8; }
 
+// Joins enqueued without phase events (hwbrj_join_device_async: the timed back-to-back joins) run
+// their S pass on a second stream beside the R side, joined before the probe (A/B: 0 = one stream,
+// S pass first). Synchronous joins keep one stream, so their phase times stay separate.
+#ifndef HWBRJ_OVL_ASYNC
+#define HWBRJ_OVL_ASYNC 1
+#endif
+
 struct BuildParams {
     Geometry         g;
     const CrcTables* tabs;
