@@ -561,8 +561,7 @@ def run_partitioned(a, hw, torch, dist, rank, world, local, dR, dS, args, shared
     if use_async:  # K joins enqueued back to back (<= 8 in flight), no host wait between them
         sts = pj_async_steps(pjoin, dR, dS, nR, args, a.steps)
         sums["ms_total"] = sum(s.ms_total for s in sts)
-        same = all((s.filtered, s.matches) == (sts[0].filtered, sts[0].matches) for s in sts)
-        same = same and (sts[0].filtered, sts[0].matches) == (st.filtered, st.matches)
+        same = all((s.filtered, s.matches) == (st.filtered, st.matches) for s in sts)
     else:
         for _ in range(a.steps):
             st = join()
