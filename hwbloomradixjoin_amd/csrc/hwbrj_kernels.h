@@ -51,6 +51,9 @@ inline bool join_pack3(const Geometry& g) { return HWBRJ_PACK3 != 0 && g.sub_shi
 #ifndef HWBRJ_OVL_ASYNC
 #define HWBRJ_OVL_ASYNC 1
 #endif
+#ifndef HWBRJ_PJ_OVL
+#define HWBRJ_PJ_OVL 1  // async partitioned joins: the S shard's partitioning on a second stream
+#endif
 
 struct BuildParams {
     Geometry         g;

@@ -4605,6 +4605,7 @@ const char* kernel_build_knobs() {
         num("HWBRJ_JFU", HWBRJ_JFU, 32);
         num("HWBRJ_JONE", HWBRJ_JONE, 0);
         num("HWBRJ_OVL_ASYNC", HWBRJ_OVL_ASYNC, 1);
+        num("HWBRJ_PJ_OVL", HWBRJ_PJ_OVL, 1);
         num("HWBRJ_ABL_PROBE", HWBRJ_ABL_PROBE, 0);
         num("HWBRJ_PCO", HWBRJ_PCO, 1);
         num("HWBRJ_PCO_AUX", HWBRJ_PCO_AUX, 0);

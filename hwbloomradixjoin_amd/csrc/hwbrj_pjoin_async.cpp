@@ -357,6 +357,40 @@ int Engine::join_partitioned_async(const hwbrj_exchange_t* xa, int rank, int wor
         return 0;
     };
     ScatterParams sp{};
+    // The S shard's partitioning (scatter, plan, lists) does not depend on R: it runs on a second
+    // stream beside the R side, the R exchange and the slice all-gather, and the probe waits for it,
+    // so the collectives' transfer time hides behind the S scatter (HWBRJ_PJ_OVL).
+    auto s_pass = [&](hipStream_t st) {
+        ScatterParams ss{};
+        ss.tabs       = d_tabs_;
+        ss.g          = g;
+        ss.src        = dS;
+        ss.n          = nS;
+        ss.pool       = poolS.as<uint32_t>();
+        ss.meta       = metaS.as<uint32_t>();
+        ss.wg_used    = usedS.as<uint32_t>();
+        ss.wgq_chunks = wgqcS.as<uint32_t>();
+        ss.wgq_elems  = wgqeS.as<uint32_t>();
+        ss.cap        = G.capS;
+        launch_scatter(ss, SRC_TUPLES, SIDE_S, G.G, st);
+        launch_plan(wgqcS.as<uint32_t>(), wgqeS.as<uint32_t>(), G.G, g.log2F, wgqoS.as<uint32_t>(),
+                    colS.as<uint32_t>() + 2 * F, colS.as<uint64_t>(), st);
+        launch_list_fill(metaS.as<uint32_t>(), usedS.as<uint32_t>(), G.capS, g.log2F, wgqoS.as<uint32_t>(),
+                         colS.as<uint32_t>() + 2 * F, colS.as<uint64_t>(), G.CH, G.nseg, lstartS.as<uint32_t>(),
+                         estartS.as<uint64_t>(), istartS.as<uint32_t>(), listS.as<uint32_t>(), G.G, st);
+    };
+    const bool s_side = HWBRJ_PJ_OVL && !fail;
+    if (s_side) {
+        if (!ovl_stream_) {
+            PX_CHECK(hipStreamCreateWithFlags(&ovl_stream_, hipStreamNonBlocking));
+            PX_CHECK(hipEventCreateWithFlags(&ovl_ev_[0], hipEventDisableTiming));
+            PX_CHECK(hipEventCreateWithFlags(&ovl_ev_[1], hipEventDisableTiming));
+        }
+        PX_CHECK(hipEventRecord(ovl_ev_[0], stream));
+        PX_CHECK(hipStreamWaitEvent(ovl_stream_, ovl_ev_[0], 0));
+        s_pass(ovl_stream_);
+        PX_CHECK(hipEventRecord(ovl_ev_[1], ovl_stream_));
+    }
     if (!fail) {
         // ---- 1. R shard: partitions and the counts message
         PX_CHECK(hipMemsetAsync(small.p, 0, 64, stream));
@@ -416,22 +450,12 @@ int Engine::join_partitioned_async(const hwbrj_exchange_t* xa, int rank, int wor
         set_last_error("exchange failed: filter slices");
         return 20;
     }
-    // ---- 5. S shard: partitions, probe, item tables, the counts message
+    // ---- 5. S shard: partitions (unless on the side stream), probe, item tables, the counts message
     if (!fail) {
-        sp.src        = dS;
-        sp.n          = nS;
-        sp.pool       = poolS.as<uint32_t>();
-        sp.meta       = metaS.as<uint32_t>();
-        sp.wg_used    = usedS.as<uint32_t>();
-        sp.wgq_chunks = wgqcS.as<uint32_t>();
-        sp.wgq_elems  = wgqeS.as<uint32_t>();
-        sp.cap        = G.capS;
-        launch_scatter(sp, SRC_TUPLES, SIDE_S, G.G, stream);
-        launch_plan(wgqcS.as<uint32_t>(), wgqeS.as<uint32_t>(), G.G, g.log2F, wgqoS.as<uint32_t>(),
-                    colS.as<uint32_t>() + 2 * F, colS.as<uint64_t>(), stream);
-        launch_list_fill(metaS.as<uint32_t>(), usedS.as<uint32_t>(), G.capS, g.log2F, wgqoS.as<uint32_t>(),
-                         colS.as<uint32_t>() + 2 * F, colS.as<uint64_t>(), G.CH, G.nseg, lstartS.as<uint32_t>(),
-                         estartS.as<uint64_t>(), istartS.as<uint32_t>(), listS.as<uint32_t>(), G.G, stream);
+        if (s_side)
+            PX_CHECK(hipStreamWaitEvent(stream, ovl_ev_[1], 0));
+        else
+            s_pass(stream);
         ProbeParams pp{};
         pp.g               = g;
         pp.tabs            = d_tabs_;
