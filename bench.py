@@ -214,8 +214,7 @@ def main():
     stream = torch.cuda.Stream()
     for _ in range(a.warmup):
         hw.join_device_async(dR, dS, args, stream=stream)
-    if a.warmup:
-        hw.join_wait()
+    warm = hw.join_wait_all(capacity=a.warmup) if a.warmup else []
 
     # Timed region: K full joins enqueued back to back on one stream (hwbrj_join_device_async: no
     # host round trip between them), bracketed by barrier + synchronize; HIP events on that same
@@ -229,15 +228,27 @@ def main():
     for _ in range(a.steps):
         hw.join_device_async(dR, dS, args, stream=stream)
     ev1.record(stream)
-    last = hw.join_wait()
+    timed = hw.join_wait_all(capacity=max(a.steps, 1))  # every timed join's own counts
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     dev_ms = ev0.elapsed_time(ev1) / max(a.steps, 1)  # device ms per join on this rank
-    if (last.filtered, last.matches) != (st.filtered, st.matches):
-        raise SystemExit(f"timed join counts {last.filtered, last.matches} differ from the parity "
-                         f"run {st.filtered, st.matches}")
+    # every join is checked, not only the last (the reference sums every thread's count of every
+    # run, src/parallel_radix_join_bloom.c:1696-1707): the warmup and each timed join must give the
+    # parity run's counts
+    ref = (st.filtered, st.matches)
+    bad = [i for i, s in enumerate(timed) if (s.filtered, s.matches) != ref]
+    wbad = [i for i, s in enumerate(warm) if (s.filtered, s.matches) != ref]
+    if len(timed) != a.steps or bad or wbad or len(warm) != a.warmup:
+        raise SystemExit(f"timed joins: {len(timed)} collected for {a.steps} enqueued; joins {bad} (warmup "
+                         f"{wbad}) differ from the parity run {ref}")
+    timed_ok = torch.tensor([len(timed) - len(bad), len(timed)], dtype=torch.int64,
+                            device="cpu" if shared else "cuda")
+    if dist:
+        dist.all_reduce(timed_ok)
+    timed_ok = [int(x) for x in timed_ok.tolist()]
+    last = timed[-1] if timed else hw.join_wait()
 
     # per-phase device times (HIP events, one synchronous join each, after the timed region)
     sums = {}
@@ -252,24 +263,18 @@ def main():
         elapsed, dev_ms = (float(x) for x in t.tolist())
     out = headline_line(a, hw, torch, dist, rank, world, dR, dS, args, st, last, sums, elapsed, dev_ms,
                         total_units, filtered, matches, ranks_agree, per_rank, shared) if rank == 0 else None
-    # the other multi-GPU designs on the same ranks, after the headline (never its value); a
-    # watchdog bounds them: if a leg has not finished in --alt-timeout seconds (a collective that
-    # never completes), rank 0 prints the headline with what the legs reported so far and every
-    # rank exits
+    if out is not None:
+        out["parity"]["timed_joins_ok"] = f"{timed_ok[0]}/{timed_ok[1]}"
+        out["parity"]["timed_joins_what"] = ("every timed join's own (filtered, matches) equal to the parity "
+                                             "run's (hwbrj_join_wait_all), summed over the ranks")
+    # the other multi-GPU designs on the same ranks, after the headline (never its value); every
+    # leg runs under its own watchdog: a leg that has not finished in --alt-timeout seconds (a
+    # collective that never completes) makes rank 0 print the headline with the legs reported so far
+    # and the stalled leg named, and every rank exit with status 124 (a timeout is not a clean run)
     alt = None
     if dist and not a.no_alt_designs and not a.filter_bcast:
         alt = {}
-
-        def expire():
-            if out is not None:
-                out["alt_designs"] = dict(alt, timeout_s=a.alt_timeout)
-                print(json.dumps(out), flush=True)
-            os._exit(0)
-        dog = threading.Timer(a.alt_timeout, expire)
-        dog.daemon = True
-        dog.start()
-        alt_designs(a, hw, torch, dist, rank, world, local, dR, dS, args, shared, alt)
-        dog.cancel()
+        alt_designs(a, hw, torch, dist, rank, world, local, dR, dS, args, shared, alt, out)
     if rank == 0:
         out["alt_designs"] = alt
         print(json.dumps(out), flush=True)
@@ -397,7 +402,10 @@ def pj_async_steps(pjoin, dR, dS, nR, args, K, depth=8, x=None):
     return out
 
 
-def alt_designs(a, hw, torch, dist, rank, world, local, dR, dS, args, shared, out):
+ALT_LEGS = ("partitioned_async", "bcast", "partitioned")  # by what one node run decides
+
+
+def alt_designs(a, hw, torch, dist, rank, world, local, dR, dS, args, shared, out, line=None):
     """The designs the headline does not run, timed on the same ranks and shards right after it, so
     one multi-GPU run decides between them:
       bcast        the replicated design with the north_star's bitmap broadcast: rank 0 builds the
@@ -413,7 +421,12 @@ def alt_designs(a, hw, torch, dist, rank, world, local, dR, dS, args, shared, ou
                    between barriers, max over ranks.
     Each leg reports its ms per join, the probe-tuples/s that gives, and every rank's own
     (filtered, matches), whose sums must be the headline's counts. A failing leg is reported, and
-    never stops the headline line."""
+    never stops the headline line. The legs run in ALT_LEGS order, the async partitioned join first
+    (the design a node run has to decide) and the host-synchronous one last, each under its own
+    --alt-timeout watchdog: when one expires, rank 0 prints `line` (the headline) with the legs
+    done so far, the stalled leg under "timed_out_leg" and the legs not run, and every rank exits
+    with status 124 (a hung collective cannot be abandoned and the next leg started).
+    HWBRJ_BENCH_HOOK_STALL_LEG=<leg> (tests only) makes that leg sleep past its watchdog."""
     from hwbloomradixjoin_amd import pjoin
     nR, nS_total = a.r_size, a.s_size
     K = max(1, min(a.steps, a.alt_steps))
@@ -433,13 +446,29 @@ def alt_designs(a, hw, torch, dist, rank, world, local, dR, dS, args, shared, ou
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
+    stall = os.environ.get("HWBRJ_BENCH_HOOK_STALL_LEG")
+
+    def expire(name):
+        if line is not None:
+            later = list(ALT_LEGS[ALT_LEGS.index(name) + 1:])
+            line["alt_designs"] = dict(out, timed_out_leg=name, timeout_s=a.alt_timeout, not_run=later)
+            print(json.dumps(line), flush=True)
+        os._exit(124)
+
     def leg(name, run):
+        dog = threading.Timer(a.alt_timeout, expire, args=(name,))
+        dog.daemon = True
+        dog.start()
         try:
+            if stall == name:  # (test hook: a leg that never completes)
+                time.sleep(a.alt_timeout * 20 + 5)
             ms, per, tot = run()
             out[name] = {"ms": round(ms, 4), "value": round(nS_total / (ms * 1e-3), 1),
                          "per_rank": per, "sum": tot}
         except Exception as e:  # (reported; the headline stands)
             out[name] = {"failed": str(e)[:300]}
+        finally:
+            dog.cancel()
 
     native = not shared
     if native:
@@ -460,9 +489,11 @@ def alt_designs(a, hw, torch, dist, rank, world, local, dR, dS, args, shared, ou
             for _ in range(K):
                 hw.join_device_async(dR, dS, args, stream=stream)
             ev1.record(stream)
-            hw.join_wait()
+            sts = hw.join_wait_all(capacity=K)
             torch.cuda.synchronize()
             dist.barrier()
+            if len(sts) != K or any((s.filtered, s.matches) != tuple(per[rank]) for s in sts):
+                raise RuntimeError("broadcast joins disagree with its first join")
             return slowest(ev0.elapsed_time(ev1) / K), per, tot
         finally:
             pjoin.set_filter_broadcast(False)
@@ -505,15 +536,13 @@ def alt_designs(a, hw, torch, dist, rank, world, local, dR, dS, args, shared, ou
             raise RuntimeError("async partitioned joins disagree")
         return slowest((time.perf_counter() - t0) / K * 1e3), per, tot
 
-    if native and slice_filter:
-        leg("bcast", bcast)
-    else:
-        out["bcast"] = {"skipped": "needs one GPU per rank (RCCL) and a slice filter"}
-    if args is None or slice_filter:
-        leg("partitioned", partitioned)
-        leg("partitioned_async", partitioned_async)
-    else:
-        out["partitioned"] = {"skipped": "basic k > 1 has no partition slices"}
+    for name in ALT_LEGS:
+        if name == "bcast" and not (native and slice_filter):
+            out[name] = {"skipped": "needs one GPU per rank (RCCL) and a slice filter"}
+        elif name != "bcast" and not (args is None or slice_filter):
+            out[name] = {"skipped": "basic k > 1 has no partition slices"}
+        else:
+            leg(name, {"bcast": bcast, "partitioned": partitioned, "partitioned_async": partitioned_async}[name])
     if native:
         pjoin.comm_destroy()
     return out

@@ -18,7 +18,7 @@ import numpy as np
 
 __all__ = [
     "BASIC", "BLOCKED", "SECTORIZED", "BloomFilterArgs", "Relation", "Result", "Stats",
-    "BPRO", "PRO", "join_materialize_device", "set_materialize", "set_gpus", "BPRH", "BPRHO", "BRJ", "PRH", "PRHO", "RJ", "assert_args", "join_device", "join_device_async", "join_wait", "generate_device", "generate_device_range",
+    "BPRO", "PRO", "join_materialize_device", "set_materialize", "set_gpus", "BPRH", "BPRHO", "BRJ", "PRH", "PRHO", "RJ", "assert_args", "join_device", "join_device_async", "join_wait", "join_wait_all", "generate_device", "generate_device_range",
     "generate_host", "nonunique_threshold", "create_relation_nonunique",
     "create_relation_nonunique_from_pk", "create_relation_fk_from_pk", "create_relation_zipf",
     "rand_stream", "reference_relations", "create_relation_zipf_device",
@@ -106,6 +106,8 @@ def lib() -> ctypes.CDLL:
                                              ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(_Stats)]
         L.hwbrj_join_wait.restype = ctypes.c_int
         L.hwbrj_join_wait.argtypes = [ctypes.c_void_p]
+        L.hwbrj_join_wait_all.restype = ctypes.c_int
+        L.hwbrj_join_wait_all.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
         L.hwbrj_join_device.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
                                         ctypes.c_uint64, ctypes.POINTER(_BloomArgs),
                                         ctypes.c_void_p, ctypes.POINTER(_Stats)]
@@ -437,6 +439,16 @@ def join_wait() -> Stats:
     st = _Stats()
     _err(lib().hwbrj_join_wait(ctypes.byref(st)), "hwbrj_join_wait")
     return Stats(**{n: getattr(st, n) for n, _ in _Stats._fields_})
+
+
+def join_wait_all(capacity: int = 256) -> list:
+    """Wait for the last enqueued join and return the Stats of EVERY join enqueued on this device
+    since the last join_wait / join_wait_all, oldest first (hwbrj_join_wait_all: each join keeps its
+    own counts in a device ring). Raises if more than `capacity` joins are pending."""
+    arr = (_Stats * max(1, capacity))()
+    n = ctypes.c_int(0)
+    _err(lib().hwbrj_join_wait_all(arr, capacity, ctypes.byref(n)), "hwbrj_join_wait_all")
+    return [Stats(**{f: getattr(arr[i], f) for f, _ in _Stats._fields_}) for i in range(n.value)]
 
 
 ALGO_PRO, ALGO_PRH, ALGO_PRHO = 0, 1, 2  # include/hwbrj.h HWBRJ_ALGO_* (per-partition join)

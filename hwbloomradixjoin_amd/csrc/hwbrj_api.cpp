@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <chrono>
 #include <mutex>
+#include <set>
 #include <string>
 #include <thread>
 #include <vector>
@@ -41,9 +42,11 @@ const char* hwbrj_version(void) {
         if (!d.empty()) k += (k.empty() ? "" : " ") + d;
         return k;
     }();
-    static std::mutex  mu;
-    static std::string v;
-    std::lock_guard<std::mutex> lk(mu);
+    // one immutable string per distinct hook state, never freed: a pointer returned earlier stays
+    // valid whatever hooks are set later
+    static std::mutex            mu;
+    static std::set<std::string> interned;
+    std::lock_guard<std::mutex>  lk(mu);
     std::string        k = base;
     const TestHooks&   h = test_hooks();
     auto add = [&](const std::string& w) { k += (k.empty() ? "" : " ") + w; };
@@ -52,8 +55,9 @@ const char* hwbrj_version(void) {
     if (h.bcast_nonroot) add("HWBRJ_HOOK_BCAST_NONROOT=" + std::to_string(h.bcast_nonroot));
     if (h.pj_plan_div) add("HWBRJ_HOOK_PJ_PLAN_DIV=" + std::to_string(h.pj_plan_div));
     if (h.pj_async_fail) add("HWBRJ_HOOK_PJ_ASYNC_FAIL=" + std::to_string(h.pj_async_fail));
-    v =std::string("hwbloomradixjoin_amd 0.5 (gfx950) src " HWBRJ_SRC_SHA) + (k.empty() ? "" : " knobs: " + k);
-    return v.c_str();
+    const std::string v = std::string("hwbloomradixjoin_amd 0.6 (gfx950) src " HWBRJ_SRC_SHA) +
+                          (k.empty() ? "" : " knobs: " + k);
+    return interned.insert(v).first->c_str();
 }
 
 int hwbrj_set_test_hook(int hook, int64_t value) {
@@ -208,6 +212,16 @@ int hwbrj_join_wait(hwbrj_stats_t* stats) {
     Engine* e = engine_for_current_device();
     if (!e) return 10;
     return e->wait(stats);
+}
+
+int hwbrj_join_wait_all(hwbrj_stats_t* stats, int capacity, int* n_joins) {
+    if (capacity < 0 || (capacity > 0 && !stats)) {
+        set_last_error("stats must hold capacity >= 0 entries");
+        return 2;
+    }
+    Engine* e = engine_for_current_device();
+    if (!e) return 10;
+    return e->wait_all(stats, capacity, n_joins);
 }
 
 // The materializing join: the partitioned pipeline carrying payloads (Engine::run_mat); the

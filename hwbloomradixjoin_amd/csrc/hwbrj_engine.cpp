@@ -323,8 +323,14 @@ void Engine::release() {
                       &pjIstart, &pjJobs, &ppoolR, &ppoolS, &rpay, &survpos, &dense2, &kkcnt, &xcnt_, &pjBsum, &pjBound, &pjWtot, &pjWscan, &pjTab2})
         b->release();
     for (DevBuf& b : xslot_) b.release();
+    if (pending_) (void) hipEventSynchronize(ev_[8]);  // (the ring's joins end before it is freed)
+    ring_drop();
+    jring_.release();
     have_filter_ = false;
 }
+
+// One join's result slot: 128 bytes of result words (read_join_counts), then k_join's partial sums
+static size_t ring_slot_bytes() { return 128 + join_sum_slots() * join_sum_stride() * 8; }
 
 static uint64_t region_cap(uint64_t n, uint32_t G, uint32_t F) {
     const uint64_t units = (n + 3) / 4;
@@ -451,7 +457,7 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     ok &= rjoin.ensure(sweeps_max * SLOT * 4) && rrun.ensure(2 * sweeps_max * NSUB * 4);
     ok &= surv.ensure(nseg * LS * 128) && survcnt.ensure(items_max * NSUB * 4) &&
           survoff.ensure(items_max * NSUB * 4);
-    ok &= small.ensure(128 + 64 * 128) && colR.ensure(F * 12) && colS.ensure(F * 12);  // u64 elems | u32 chunks
+    ok &= jring_.ensure(kJoinRing * ring_slot_bytes()) && colR.ensure(F * 12) && colS.ensure(F * 12);  // u64 elems | u32 chunks
     // jparts: nparts [NJ] | job_surv [NJ] | nextra; jtask: extra parts {job, part}
     // (job_surv is left zero by k_join_split for the NJ jobs it saw: a join with another NJ
     // clears the whole buffer, so no stale count of an earlier job layout is read)
@@ -471,9 +477,13 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     }
     if (alloc_only_) return 0;
     if (const int rc = pre(0)) return rc;
-    uint64_t* d_result   = small.as<uint64_t>();      // [0] matches
-    uint64_t* d_dcount   = small.as<uint64_t>() + 1;  // [1] dense survivor count (global mode)
-    uint64_t* d_filtered = small.as<uint64_t>() + 2;  // [2] S-tuples after filter
+    // this join's result slot (ring_take collects a full ring first)
+    uint32_t  rslot      = 0;
+    char*     sm         = (char*) ring_take(&rslot);
+    if (!sm) return 1;
+    uint64_t* d_result   = (uint64_t*) sm;      // [0] matches
+    uint64_t* d_dcount   = (uint64_t*) sm + 1;  // [1] dense survivor count (global mode)
+    uint64_t* d_filtered = (uint64_t*) sm + 2;  // [2] S-tuples after filter
 
     // zeroing (the reference callocs before its timer, :1583, :1601): the counts and the join's
     // extra-task count are zeroed by the R scatter's workgroup 0 (two memset dispatches less per
@@ -484,7 +494,7 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     ScatterParams sp{};
     sp.tabs = d_tabs_;
     sp.g    = g;
-    sp.zero_small = small.as<uint32_t>();  // (the R scatter only: cleared below)
+    sp.zero_small = (uint32_t*) sm;  // (the R scatter only: cleared below)
     sp.zero_word  = jparts.as<uint32_t>() + 2 * NJ;
 
     // S pass-1 and its lists (below; dev A/B HWBRJ_DEV_OVL: on a second stream, concurrent with
@@ -660,7 +670,7 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     pp.job_surv        = jparts.as<uint32_t>() + NJ;
     pp.surv_pos        = mat ? survpos.as<uint32_t>() : nullptr;
     pp.pack3           = pack3 ? 1u : 0u;
-    pp.fmt_cnt         = mat ? nullptr : small.as<uint32_t>() + 10;  // (u64 slot 5 of small: zeroed by the R scatter)
+    pp.fmt_cnt         = mat ? nullptr : (uint32_t*) sm + 10;  // (u64 word 5 of the slot: zeroed by the R scatter)
     const size_t   pl_lds = probe_lds_bytes(g, nullptr, mat != nullptr);
     const uint32_t PG = (uint32_t) cus_ * (uint32_t) std::max<size_t>(1, std::min<size_t>(2, 163840 / pl_lds));
     const bool dbg_on = dbg;  // dev-only phase stamps (HWBRJ_DBG)
@@ -691,7 +701,7 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     jp.log2NSUB        = g.log2NSUB;
     jp.hash_shift      = g.hash_shift;
     jp.bitmap          = (g.sub_shift > 0 && 32 - g.hash_shift <= join_bitmap_log2()) ? 1u : 0u;
-    jp.jsum            = (uint64_t*) ((char*) small.p + 128);  // 64 partial sums, one per 128-B line
+    jp.jsum            = (uint64_t*) (sm + 128);  // 64 partial sums, one per 128-B line
     jp.dbg             = dbg_on ? dbgJ.as<uint64_t>() : nullptr;
     jp.nparts          = jparts.as<uint32_t>();
     jp.extra           = jtask.as<uint2>();
@@ -745,6 +755,17 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     pending_stream_ = stream;
     have_filter_  = args != nullptr;
     last_g_       = g;
+    {
+        JoinRec r;
+        r.slot  = rslot;
+        r.args  = args != nullptr;
+        r.fmt   = pending_fmt_;
+        r.pack3 = pack3;
+        r.slots = !mat;
+        r.nS    = nS;
+        r.g     = g;
+        ring_push(r);
+    }
 
     if (dbg_on) {
         HWBRJ_CHECK(hipEventSynchronize(ev_[8]));
@@ -832,7 +853,7 @@ int Engine::enqueue_basic_kk(const uint2* dR, uint64_t nR, const uint2* dS, uint
     const uint64_t sweeps_max = LR / BSW + Fm + 1;
     ok &= rjoin.ensure(sweeps_max * SLOT * 4) && rrun.ensure(2 * sweeps_max * NSUB * 4);
     ok &= surv.ensure(LS * 128) && survcnt.ensure(items_max * NSUB * 4) && survoff.ensure(items_max * NSUB * 4);
-    ok &= small.ensure(128 + 64 * 128) && colR.ensure(Fm * 12) && colS.ensure(Fm * 12);
+    ok &= jring_.ensure(kJoinRing * ring_slot_bytes()) && colR.ensure(Fm * 12) && colS.ensure(Fm * 12);
     const bool jnew = jparts.bytes < (size_t) (2 * NJ + 1) * 4 || NJ != last_nj_;
     last_nj_ = NJ;
     ok &= jtask.ensure((size_t) join_extra_tasks() * 8) && jparts.ensure((size_t) (2 * NJ + 1) * 4);
@@ -844,10 +865,13 @@ int Engine::enqueue_basic_kk(const uint2* dR, uint64_t nR, const uint2* dS, uint
         return 4;
     }
     if (alloc_only_) return 0;
-    uint64_t* d_filtered = small.as<uint64_t>() + 2;
+    uint32_t  rslot      = 0;
+    char*     sm         = (char*) ring_take(&rslot);
+    if (!sm) return 1;
+    uint64_t* d_filtered = (uint64_t*) sm + 2;
     uint64_t* cnt        = kkcnt.as<uint64_t>();  // [j]: candidates after pass j (j < k - 1); [NC - 1]: dummy
     uint32_t* wgc[2]     = {(uint32_t*) (cnt + NC), (uint32_t*) (cnt + NC) + G};  // per-workgroup counts
-    HWBRJ_CHECK(hipMemsetAsync(small.p, 0, 64, stream));
+    HWBRJ_CHECK(hipMemsetAsync(sm, 0, 64, stream));
     HWBRJ_CHECK(hipMemsetAsync(kkcnt.p, 0, kkcnt.bytes, stream));
     if (jnew) HWBRJ_CHECK(hipMemsetAsync(jparts.p, 0, jparts.bytes, stream));
     HWBRJ_CHECK(hipMemsetAsync(jparts.as<uint32_t>() + 2 * NJ, 0, 4, stream));
@@ -1003,7 +1027,7 @@ int Engine::enqueue_basic_kk(const uint2* dR, uint64_t nR, const uint2* dS, uint
     jp.log2NSUB        = gj.log2NSUB;
     jp.hash_shift      = gj.hash_shift;
     jp.bitmap          = (gj.sub_shift > 0 && 32 - gj.hash_shift <= join_bitmap_log2()) ? 1u : 0u;
-    jp.jsum            = (uint64_t*) ((char*) small.p + 128);
+    jp.jsum            = (uint64_t*) (sm + 128);
     jp.nparts          = jparts.as<uint32_t>();
     jp.extra           = jtask.as<uint2>();
     jp.nextra          = jparts.as<uint32_t>() + 2 * NJ;
@@ -1025,6 +1049,15 @@ int Engine::enqueue_basic_kk(const uint2* dR, uint64_t nR, const uint2* dS, uint
     pending_stream_ = stream;
     have_filter_  = true;
     last_g_       = g;
+    {
+        JoinRec r;
+        r.slot  = rslot;
+        r.args  = true;
+        r.slots = true;
+        r.nS    = nS;
+        r.g     = g;
+        ring_push(r);
+    }
     return 0;
 }
 
@@ -1046,63 +1079,143 @@ int read_join_counts(const void* small, bool slots, hipStream_t stream, uint64_t
     return 0;
 }
 
-int Engine::wait(hwbrj_stats_t* st) {
+void* Engine::ring_take(uint32_t* slot) {
+    if (jr_.size() >= (size_t) kJoinRing && ring_collect()) return nullptr;
+    *slot    = jr_next_;
+    jr_next_ = (jr_next_ + 1) % kJoinRing;
+    return (char*) jring_.p + (size_t) *slot * ring_slot_bytes();
+}
+
+// The counts of every join in jr_ (all completed once ev_[8] has: they share the device's scratch,
+// so each ran after the one before), read in one copy of the ring, appended to jdone_.
+int Engine::ring_collect() {
+    if (jr_.empty()) return 0;
+    HWBRJ_CHECK(hipEventSynchronize(ev_[8]));
+    const size_t          SB = ring_slot_bytes();
+    std::vector<uint64_t> buf(kJoinRing * SB / 8);
+    // the slots in use are consecutive mod kJoinRing: one copy of [first, last], or of the ring
+    const uint32_t a = jr_.front().slot, z = jr_.back().slot;
+    const size_t   off = a <= z ? (size_t) a * SB : 0, len = a <= z ? (size_t) (z - a + 1) * SB : kJoinRing * SB;
+    HWBRJ_CHECK(hipMemcpy((char*) buf.data() + off, (char*) jring_.p + off, len, hipMemcpyDeviceToHost));
+    const size_t S = join_sum_slots(), W = join_sum_stride();
+    for (const JoinRec& r : jr_) {
+        const uint64_t* b = buf.data() + (size_t) r.slot * (SB / 8);
+        uint64_t        h[6];
+        for (int i = 0; i < 6; i++) h[i] = b[i];
+        if (r.slots)
+            for (size_t j = 0; j < S; j++) {
+                h[0] += b[16 + j * W];
+                h[3] += b[16 + j * W + 1];
+                h[4] += b[16 + j * W + 2];
+            }
+        if (r.fmt) pack3_hint_ = (uint32_t) h[5] == 0;  // (k_probe's count, ProbeParams::fmt_cnt)
+        const Geometry& g = r.g;
+        hwbrj_stats_t   st;
+        memset(&st, 0, sizeof(st));
+        st.filtered       = r.args ? h[2] : r.nS;
+        st.matches        = (int64_t) h[0];
+        st.mode           = g.mode;
+        st.format         = g.s_format;
+        st.partitions     = 1u << g.log2F;
+        st.subparts       = 1u << g.log2NSUB;
+        st.slice_segments = (g.mode == MODE_SLICE_BLOCK || g.mode == MODE_SLICE_BASIC) ? g.nseg : 1;
+        st.unstaged_items = r.fmt ? (uint32_t) h[5] : 0u;
+        st.join_keys      = !r.pack3 ? HWBRJ_JOIN_KEYS_32
+                            : st.unstaged_items ? HWBRJ_JOIN_KEYS_MIXED : HWBRJ_JOIN_KEYS_PACKED;
+        // (probe / join ticks: the synchronous joins' phase split, added by wait())
+        st.ms_join_probe  = (double) h[3];
+        st.ms_join        = (double) h[4];
+        jdone_.push_back(st);
+    }
+    jr_.clear();
+    return 0;
+}
+
+// Waits for the last join and collects every join since the last wait; the last one's phase times
+// (synchronous joins) are read from its events.
+static int wait_common(hwbrj_stats_t* last, bool phases, const hipEvent_t* ev, bool sfirst, bool surv_fused) {
+    float ms[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    if (phases) {  // (async joins: counts only)
+        hipEvent_t e[9];
+        for (int i = 0; i <= 8; i++) e[i] = ev[i];
+        if (surv_fused) e[7] = ev[6];
+        // phase i ends at boundary i and starts at boundary from[i] (S pass first: it starts the
+        // join, the R scatter starts after the S lists, the probe after the build)
+        static const int kFrom[2][9] = {{0, 0, 1, 2, 3, 4, 5, 6, 7}, {0, 5, 1, 2, 0, 4, 3, 6, 7}};
+        const int* from = kFrom[sfirst ? 1 : 0];
+        for (int i = 1; i <= 8; i++) HWBRJ_CHECK(hipEventElapsedTime(&ms[i], e[from[i]], e[i]));
+        HWBRJ_CHECK(hipEventElapsedTime(&ms[0], e[0], e[8]));
+    }
+    const double pt = last->ms_join_probe, jt = last->ms_join;  // (ticks, ring_collect)
+    last->ms_total      = ms[0];
+    last->ms_r_scatter  = ms[1];
+    last->ms_r_index    = ms[2];
+    last->ms_build      = ms[3];
+    last->ms_s_scatter  = ms[4];
+    last->ms_s_index    = ms[5];
+    last->ms_probe      = ms[6];
+    last->ms_surv       = ms[7];
+    last->ms_join       = ms[8];
+    // the probe share of the join's workgroup time (k_join's wall_clock64 sections)
+    last->ms_join_probe = jt > 0 ? ms[8] * pt / jt : 0.0;
+    return 0;
+}
+
+int Engine::wait_all(hwbrj_stats_t* st, int cap, int* n) {
     HWBRJ_CHECK(hipSetDevice(device_));
+    if (n) *n = 0;
     if (!pending_) {
+        ring_drop();
         set_last_error("no join has been enqueued");
         return 6;
     }
     HWBRJ_CHECK(hipEventSynchronize(ev_[8]));
     if (pending_rc_) {  // the last join stopped after some of its kernels (a failed broadcast)
+        ring_drop();
         set_last_error(pending_err_);
         return pending_rc_;
     }
-    const Geometry& g = last_g_;
-    const uint32_t  F = 1u << g.log2F, NSUB = 1u << g.log2NSUB;
-    const uint32_t  nseg = (g.mode == MODE_SLICE_BLOCK || g.mode == MODE_SLICE_BASIC) ? g.nseg : 1;
-    const uint64_t* d_result   = small.as<uint64_t>();      // (see enqueue)
-    const uint64_t* d_filtered = small.as<uint64_t>() + 2;
-    uint64_t small_h[6] = {0, 0, 0, 0, 0, 0};  // matches, dcount, filtered, probe ticks, join ticks, unstaged items
-    if (const int rc = read_join_counts(d_result, pending_slots_, own_stream_, small_h)) return rc;
-    if (pending_fmt_) pack3_hint_ = (uint32_t) small_h[5] == 0;  // (k_probe's count, ProbeParams::fmt_cnt)
-    (void) d_filtered;
-    const uint64_t matches = small_h[0], filtered = small_h[2];
-    if (st) {
-        memset(st, 0, sizeof(*st));
-        st->filtered       = pending_args_ ? filtered : pending_nS_;
-        st->matches        = (int64_t) matches;
-        st->mode           = g.mode;
-        st->format         = g.s_format;
-        st->partitions     = F;
-        st->subparts       = NSUB;
-        st->slice_segments = nseg;
-        float ms[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-        if (pending_ev_) {  // (async joins: counts only)
-            hipEvent_t e[9];
-            for (int i = 0; i <= 8; i++) e[i] = ev_[i];
-            if (surv_fused_) e[7] = ev_[6];
-            // phase i ends at boundary i and starts at boundary from[i] (S pass first: it starts the
-            // join, the R scatter starts after the S lists, the probe after the build)
-            static const int kFrom[2][9] = {{0, 0, 1, 2, 3, 4, 5, 6, 7}, {0, 5, 1, 2, 0, 4, 3, 6, 7}};
-            const int* from = kFrom[pending_sfirst_ ? 1 : 0];
-            for (int i = 1; i <= 8; i++) HWBRJ_CHECK(hipEventElapsedTime(&ms[i], e[from[i]], e[i]));
-            HWBRJ_CHECK(hipEventElapsedTime(&ms[0], e[0], e[8]));
+    if (const int rc = ring_collect()) return rc;
+    for (size_t i = 0; i < jdone_.size(); i++) {  // ticks -> ms (only the last has phase times)
+        if (i + 1 == jdone_.size()) {
+            if (const int rc = wait_common(&jdone_[i], pending_ev_, ev_, pending_sfirst_, surv_fused_)) return rc;
+        } else {
+            jdone_[i].ms_join_probe = jdone_[i].ms_join = 0;
         }
-        st->ms_total     = ms[0];
-        st->ms_r_scatter = ms[1];
-        st->ms_r_index   = ms[2];
-        st->ms_build     = ms[3];
-        st->ms_s_scatter = ms[4];
-        st->ms_s_index   = ms[5];
-        st->ms_probe     = ms[6];
-        st->ms_surv      = ms[7];
-        st->ms_join      = ms[8];
-        // the probe share of the join's workgroup time (k_join's wall_clock64 sections)
-        st->ms_join_probe = small_h[4] ? ms[8] * (double) small_h[3] / (double) small_h[4] : 0.0;
-        st->unstaged_items = pending_fmt_ ? (uint32_t) small_h[5] : 0u;
-        st->join_keys      = !pending_pack3_ ? HWBRJ_JOIN_KEYS_32
-                             : st->unstaged_items ? HWBRJ_JOIN_KEYS_MIXED : HWBRJ_JOIN_KEYS_PACKED;
     }
+    const size_t tot = jdone_.size();
+    if (tot) last_st_ = jdone_.back();
+    if (n) *n = (int) tot;
+    if (st)
+        for (size_t i = 0; i < tot && (int) i < cap; i++) st[i] = jdone_[i];
+    jdone_.clear();
+    if (st && (size_t) cap < tot) {
+        set_last_error("more joins than the stats array holds (the oldest were written)");
+        return 7;
+    }
+    return 0;
+}
+
+int Engine::wait(hwbrj_stats_t* st) {
+    HWBRJ_CHECK(hipSetDevice(device_));
+    if (!pending_) {
+        ring_drop();
+        set_last_error("no join has been enqueued");
+        return 6;
+    }
+    HWBRJ_CHECK(hipEventSynchronize(ev_[8]));
+    if (pending_rc_) {  // the last join stopped after some of its kernels (a failed broadcast)
+        ring_drop();
+        set_last_error(pending_err_);
+        return pending_rc_;
+    }
+    if (const int rc = ring_collect()) return rc;
+    if (!jdone_.empty()) {  // (else: the last join was collected before; its stats again)
+        last_st_ = jdone_.back();
+        jdone_.clear();
+        if (const int rc = wait_common(&last_st_, pending_ev_, ev_, pending_sfirst_, surv_fused_)) return rc;
+    }
+    if (st) *st = last_st_;
     return 0;
 }
 

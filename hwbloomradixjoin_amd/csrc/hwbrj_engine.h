@@ -48,6 +48,12 @@ class Engine {
     int  run_async(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
                    const bloom_filter_args_t* args, hipStream_t stream, int jkind = 0);
     int  wait(hwbrj_stats_t* st);
+    // Every join enqueued since the last wait / wait_all, oldest first, each with its own counts
+    // (they stay on the device in a ring of kJoinRing result slots, one per join; an enqueue that
+    // finds the ring full collects it on the host first). *n = the number of joins; 7 when it
+    // exceeds cap (the oldest cap are written).
+    static constexpr int kJoinRing = 64;
+    int  wait_all(hwbrj_stats_t* st, int cap, int* n);
     // Allocates every buffer a join of these inputs needs, without launching it (the host BPRO
     // stages this before its timed region, like the reference's allocations before its timer).
     int  reserve(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
@@ -197,6 +203,24 @@ class Engine {
     int          pending_rc_     = 0;   // nonzero: the pending join failed after enqueuing kernels
     std::string  pending_err_;
     bool         surv_fused_   = false;
+    // per-join results: join i writes its counts and k_join's partial sums into ring slot
+    // i mod kJoinRing (jring_), so every join of a back-to-back run can be checked, not only the
+    // last (the reference sums every thread's count per run, parallel_radix_join_bloom.c:1696-1707)
+    struct JoinRec {
+        uint32_t slot = 0;
+        bool     args = false, fmt = false, pack3 = false, slots = false;
+        uint64_t nS   = 0;
+        Geometry g{};
+    };
+    DevBuf                     jring_;
+    std::vector<JoinRec>       jr_;     // enqueued since the last wait, oldest first
+    std::vector<hwbrj_stats_t> jdone_;  // collected early (the ring was full), oldest first
+    uint32_t                   jr_next_ = 0;
+    hwbrj_stats_t              last_st_{};  // the last collected join (with its phase times)
+    void*        ring_take(uint32_t* slot);            // the next slot's bytes (jring_ grown first)
+    void         ring_push(const JoinRec& r) { jr_.push_back(r); }
+    int          ring_collect();                       // jr_ (completed) -> jdone_
+    void         ring_drop() { jr_.clear(); jdone_.clear(); }
     hipError_t   mark(int i, hipStream_t stream);  // ev_[i] when phase_ev_
     bool         alloc_only_   = false;  // reserve(): enqueue returns after its allocations
     int          enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,

@@ -796,6 +796,7 @@ int Engine::join_partitioned(const hwbrj_exchange_t* x, int rank, int world, con
     }
     if (rc7) return rc7;
     pending_ = false;
+    ring_drop();  // (single-GPU joins enqueued before it are no longer collected)
     have_filter_ = false;  // (the slices live in the caller's exchange buffer)
     last_nj_     = 0;      // job_surv holds this join's counts: the next enqueue clears the table
     if (st) {

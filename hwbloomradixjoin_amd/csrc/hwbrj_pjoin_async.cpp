@@ -26,6 +26,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <functional>
 #include <vector>
 
 #include "hwbrj_engine.h"
@@ -326,6 +327,26 @@ int Engine::join_partitioned_async(const hwbrj_exchange_t* xa, int rank, int wor
     uint64_t* rc2r     = rc2s + (uint64_t) W * NC;
     const int slot     = (int) (pj_seq_ % kPjDepth);
     if (pending_ && pending_stream_ != stream) PX_CHECK(hipStreamWaitEvent(stream, ev_[8], 0));
+    // An error return from here on leaves work of this join enqueued (on the join stream and, after
+    // the fork below, on the side stream): the side stream is joined back into the join stream and
+    // ev_[8] recorded after it, so every later join on this Engine (which shares these buffers)
+    // orders after that work. Disarmed where the join completes its enqueue.
+    bool forked = false;
+    struct Unwind {
+        std::function<void()> f;
+        ~Unwind() {
+            if (f) f();
+        }
+    } unwind;
+    unwind.f = [&] {
+        if (forked) (void) hipStreamWaitEvent(stream, ovl_ev_[1], 0);
+        (void) hipEventRecord(ev_[8], stream);
+        pending_        = true;
+        pending_stream_ = stream;
+        pending_rc_     = 6;
+        pending_err_    = "the last join was a partitioned join that failed: " + std::string(hwbrj_last_error());
+        ring_drop();
+    };
     PX_CHECK(hipEventRecord(pjEv_[2 * slot], stream));
     PX_CHECK(hipMemsetAsync(flag, 0, 8, stream));
     // this rank's own blocks are written by k_pjx_gather / k_pjx_surv_pack straight into the
@@ -390,6 +411,7 @@ int Engine::join_partitioned_async(const hwbrj_exchange_t* xa, int rank, int wor
         PX_CHECK(hipStreamWaitEvent(ovl_stream_, ovl_ev_[0], 0));
         s_pass(ovl_stream_);
         PX_CHECK(hipEventRecord(ovl_ev_[1], ovl_stream_));
+        forked = true;
     }
     if (!fail) {
         // ---- 1. R shard: partitions and the counts message
@@ -452,9 +474,10 @@ int Engine::join_partitioned_async(const hwbrj_exchange_t* xa, int rank, int wor
     }
     // ---- 5. S shard: partitions (unless on the side stream), probe, item tables, the counts message
     if (!fail) {
-        if (s_side)
+        if (s_side) {
             PX_CHECK(hipStreamWaitEvent(stream, ovl_ev_[1], 0));
-        else
+            forked = false;
+        } else
             s_pass(stream);
         ProbeParams pp{};
         pp.g               = g;
@@ -542,10 +565,12 @@ int Engine::join_partitioned_async(const hwbrj_exchange_t* xa, int rank, int wor
     PX_CHECK(hipEventRecord(pjEv_[2 * slot + 1], stream));
     PX_CHECK(hipEventRecord(ev_[8], stream));
     PX_CHECK(hipGetLastError());
+    unwind.f = nullptr;  // (enqueued: the state below replaces the unwinding)
     // single-GPU joins on this Engine order after it (ev_[8]); hwbrj_wait does not collect it
     pending_        = true;
     pending_stream_ = stream;
     pending_rc_     = 6;
+    ring_drop();
     pending_err_    = "the last join is a partitioned one: collect it with hwbrj_join_partitioned_wait";
     have_filter_    = false;
     last_nj_        = 0;

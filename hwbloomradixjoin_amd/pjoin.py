@@ -11,6 +11,7 @@ exchanges through the hwbrj_exchange_t callbacks; device buffers are torch tenso
 """
 from __future__ import annotations
 
+import collections
 import ctypes
 
 import numpy as np
@@ -197,25 +198,36 @@ def join_partitioned_rccl(R, S, nR_total: int, args=None) -> Stats:
     return Stats(**{n: getattr(st, n) for n, _ in _Stats._fields_})
 
 
+# What every enqueued async partitioned join reads until its wait returns: its R and S tensors and,
+# over the callbacks, the TorchExchange (its ctypes thunks and the device buffers of its exchanges;
+# a wait that reruns the join calls the thunks again). Held here, in call order, and released by
+# join_partitioned_wait, so a caller that drops its own references cannot free them early.
+_inflight = collections.deque()
+
+
 def join_partitioned_rccl_async(R, S, nR_total: int, args=None) -> None:
     """join_partitioned_rccl enqueued without host waits (hwbrj_join_partitioned_rccl_async): the
     exchanges are padded to a plan made by an earlier synchronous join of the same shapes (the first
     call runs synchronously and makes it). Collect with join_partitioned_wait, in call order; R and
-    S must stay alive and unchanged until then. A collective: every rank makes the same calls."""
+    S must stay unchanged until then (this module keeps them alive). A collective: every rank makes
+    the same calls."""
     _check_rel(R, S)
     a = args._c() if args is not None else None
     rc = lib().hwbrj_join_partitioned_rccl_async(_ptr(R), R.shape[0], int(nR_total), _ptr(S), S.shape[0],
                                                  ctypes.byref(a) if a is not None else None)
     _err(rc, "hwbrj_join_partitioned_rccl_async")
+    _inflight.append((R, S, None))
 
 
-def join_partitioned_async(R, S, nR_total: int, args=None, exchange=None) -> None:
+def join_partitioned_async(R, S, nR_total: int, args, exchange: "TorchExchange") -> None:
     """The async partitioned join over torch.distributed callbacks (hwbrj_join_partitioned_async):
     the same plan and padded layout as join_partitioned_rccl_async, with host-synchronous exchanges
-    (ranks may share a GPU: gloo). Collect with join_partitioned_wait; `exchange` (a TorchExchange)
-    must outlive the wait."""
+    (ranks may share a GPU: gloo). Collect with join_partitioned_wait. `exchange` is required (one
+    TorchExchange per rank, reused across joins); it, R and S are kept alive until the wait."""
+    if not isinstance(exchange, TorchExchange):
+        raise TypeError("join_partitioned_async needs the rank's TorchExchange (exchange=...)")
     _check_rel(R, S)
-    x = exchange or TorchExchange(R.device)
+    x = exchange
     a = args._c() if args is not None else None
     rc = lib().hwbrj_join_partitioned_async(ctypes.byref(x._c), x.rank, x.world, _ptr(R), R.shape[0],
                                             int(nR_total), _ptr(S), S.shape[0],
@@ -224,14 +236,18 @@ def join_partitioned_async(R, S, nR_total: int, args=None, exchange=None) -> Non
         e, x.error = x.error, None
         raise RuntimeError(f"hwbrj_join_partitioned_async: exchange failed: {e!r}") from e
     _err(rc, "hwbrj_join_partitioned_async")
-    return x
+    _inflight.append((R, S, x))
 
 
 def join_partitioned_wait() -> Stats:
     """The oldest enqueued async partitioned join's result (hwbrj_join_partitioned_wait); a join
     whose padded blocks overflowed on any rank is rerun synchronously here (same counts)."""
     st = _Stats()
-    _err(lib().hwbrj_join_partitioned_wait(ctypes.byref(st)), "hwbrj_join_partitioned_wait")
+    try:
+        _err(lib().hwbrj_join_partitioned_wait(ctypes.byref(st)), "hwbrj_join_partitioned_wait")
+    finally:
+        if _inflight:
+            _inflight.popleft()
     return Stats(**{n: getattr(st, n) for n, _ in _Stats._fields_})
 
 

@@ -166,6 +166,14 @@ int hwbrj_join_device_algo(const tuple_t * d_R, uint64_t nR, const tuple_t * d_S
 int hwbrj_join_device_async(const tuple_t * d_R, uint64_t nR, const tuple_t * d_S, uint64_t nS,
                             const bloom_filter_args_t * args, void * stream);
 int hwbrj_join_wait(hwbrj_stats_t * stats);
+/* Every join enqueued on this device since the last hwbrj_join_wait / hwbrj_join_wait_all (or
+ * synchronous join), oldest first, each with its own counts: stats[i] is join i's filtered /
+ * matches / mode / join_keys (ms_* only for the last one, and only if it was synchronous). The
+ * reference checks every run's count (src/parallel_radix_join_bloom.c:1696-1707 sums each thread's);
+ * here every join of a back-to-back run keeps its counts in a device ring of 64 result slots, and an
+ * enqueue that finds all 64 in use first collects them on the host (one wait). *n_joins = the
+ * number of joins; returns 7 when it exceeds capacity (the oldest `capacity` are written). */
+int hwbrj_join_wait_all(hwbrj_stats_t * stats, int capacity, int * n_joins);
 
 /* The join with result materialization (the reference's JOIN_RESULT_MATERIALIZE output,
  * src/parallel_radix_join_bloom.c:307-312): d_out[i] = {R.payload, S.payload} of every match, in

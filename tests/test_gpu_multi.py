@@ -426,17 +426,22 @@ def test_partitioned_async_failed_mode_world1(hw, cuda, orc, rccl1, hook):
 
 
 def test_bench_alt_watchdog_world1(hw):
-    """bench.py's alt_designs legs run under a watchdog (a collective that never completes on a
-    node must not cost the headline): with --alt-timeout far below what the legs take, rank 0 still
-    prints the headline line, its parity ok, with alt_designs marked by the timeout, and the run
-    exits 0."""
+    """bench.py's alt_designs legs each run under their own watchdog (a collective that never
+    completes on a node must not cost the headline, nor the legs before it): the bcast leg is made
+    to stall (HWBRJ_BENCH_HOOK_STALL_LEG). Rank 0 still prints the headline line, its parity ok, with
+    partitioned_async (the first leg) reported with the F3 counts, bcast named as the timed-out leg,
+    partitioned as not run, and the run exits non-zero (status 124 on the rank)."""
     g = GOLD["F3_grid"]
-    rc, out, err = torchrun(1, ["-r", g["r"], "-s", g["s"], "-m", g["m"], "--alt-timeout", "0.01"],
-                            {"HWBRJ_BENCH_DIST": "1"})
-    assert rc == 0, out[-2000:] + err[-3000:]
+    rc, out, err = torchrun(1, ["-r", g["r"], "-s", g["s"], "-m", g["m"], "--alt-timeout", "30"],
+                            {"HWBRJ_BENCH_DIST": "1", "HWBRJ_BENCH_HOOK_STALL_LEG": "bcast"})
+    assert rc not in (0, None), out[-2000:] + err[-3000:]
     line = last_json(out)
-    assert (line["parity"]["filtered"], line["parity"]["matches"]) == (g["rows"]["1024"][0], g["results"])
-    assert line["alt_designs"]["timeout_s"] == 0.01, line["alt_designs"]
+    want = [g["rows"]["1024"][0], g["results"]]
+    assert [line["parity"]["filtered"], line["parity"]["matches"]] == want
+    alt = line["alt_designs"]
+    assert alt["timed_out_leg"] == "bcast" and alt["timeout_s"] == 30 and alt["not_run"] == ["partitioned"], alt
+    assert alt["partitioned_async"]["sum"] == want, alt
+    assert "bcast" not in alt and "partitioned" not in alt, alt
 
 
 def test_partitioned_async_after_release_world1(hw, cuda, orc, rccl1):
@@ -471,14 +476,15 @@ def test_partitioned_async_after_release_world1(hw, cuda, orc, rccl1):
 @pytest.mark.parametrize("scen,world,flt", [("steady", 2, "blocked"), ("overflow", 2, "blocked"), ("shape", 2, "blocked"),
                                             ("fail1", 2, "blocked"), ("steady", 4, "blocked"), ("overflow", 4, "blocked"),
                                             ("steady", 2, "pro"), ("steady", 4, "sect")])
-def test_partitioned_async_ranks_shared_gpu(hw, scen, world, flt):
+def test_partitioned_async_ranks_shared_gpu(hw, orc, scen, world, flt):
     """The async partitioned join with two and four ranks (hwbrj_join_partitioned_async over
     torch.distributed gloo callbacks, every rank on the one GPU): the W > 1 parts of the padded layout -- destination
     blocks found among the block starts, two sources per owner table, survivor blocks per source --
     the plan max-reduced over the ranks, and the collective reruns: a plan too small (the flag set
     on a rank reruns the join on both), a shard that changes size on one rank only (the failed mode
     there), a rank forced into the failed mode. Counts summed over the ranks equal F3 (or, for the
-    changed shard, the synchronous join of the same shards)."""
+    changed shard, the oracle on the same shards). PRO and sectorized k = 2 are checked against the
+    oracle on the same relations (hwbrj.generate_host, the generator the ranks' shards come from)."""
     g = GOLD["F3_grid"]
     rc, out, err = torchrun(world, [scen, g["r"], g["s"], g["m"], flt], {}, timeout=300, script="pj_async_worker.py")
     assert rc == 0, out[-2000:] + err[-3000:]
@@ -488,16 +494,13 @@ def test_partitioned_async_ranks_shared_gpu(hw, scen, world, flt):
     n_async, reruns, flag, plan_joins = info[0]
     assert plan_joins == 1
     want = (g["rows"]["1024"][0], g["results"])
-    if flt != "blocked":  # (the single-GPU join of the same relations: the F3 rows hold blocked k = 1)
-        import torch
-        R = torch.empty((g["r"], 2), dtype=torch.int32, device="cuda")
-        S = torch.empty((g["s"], 2), dtype=torch.int32, device="cuda")
-        hw.generate_device_range(R, g["r"], 0, 2, g["r"], g["r"], 1.0, 12345)
-        hw.generate_device_range(S, g["s"], 0, 2, INT_MAX, g["r"], 0.01, 54321)
-        a = None if flt == "pro" else hw.BloomFilterArgs.from_flag("sectorized", g["m"], 2, 512)
-        st = hw.join_device(R, S, a)
-        want = (st.filtered, st.matches)
-        del R, S
+    R = S = None
+    if flt != "blocked" or scen == "shape":  # the oracle on the same relations (F3 holds blocked k = 1)
+        R = hw.generate_host(g["r"], 2, g["r"], g["r"], 1.0, 12345, 8)
+        S = hw.generate_host(g["s"], 2, INT_MAX, g["r"], 0.01, 54321, 8)
+    if flt != "blocked":
+        want = _ref_counts(orc, R, S, None if flt == "pro" else
+                           hw.BloomFilterArgs.from_flag("sectorized", g["m"], 2, 512))
     if scen == "steady":
         assert sums == [want] * 4 and (n_async, reruns) == (3, 0), out[-2000:]
     elif scen == "overflow":
@@ -505,6 +508,10 @@ def test_partitioned_async_ranks_shared_gpu(hw, scen, world, flt):
     elif scen == "fail1":
         assert sums == [want] * 2 and (n_async, reruns, flag) == (1, 1, 2), out[-2000:]
     else:
+        # rank 1's S shard lost its last 1000 rows (pj_async_worker.py "shape"): the oracle on them
+        lo, hi = hw.shard_range(g["s"], 1, world)
+        shaped = np.concatenate([S[:hi - 1000], S[hi:]])
+        got = _ref_counts(orc, R, shaped, hw.BloomFilterArgs(hw.BLOCKED, g["m"], 1, 1024))
         sync = [tuple(int(v) for v in l.split()[-2:]) for l in out.splitlines() if l.startswith("sync: ")]
-        assert sums[0] == want and sums[1] == sync[0] and sums[1] != want, out[-2000:]
+        assert sums[0] == want and sums[1] == got == sync[0] and sums[1] != want, out[-2000:]
         assert (n_async, reruns, flag) == (1, 1, 2), out[-2000:]

@@ -130,15 +130,16 @@ def test_joins_on_two_streams_are_ordered(hw, cuda):
         assert (st.filtered, st.matches) == (g["rows"]["basic"][1], g["results"])
         hw.join_device_async(R, S, a2, stream=s1)
         hw.join_device_async(R, S, a1, stream=s2)
-        st = hw.join_wait()
-        assert (st.filtered, st.matches) == (g["rows"]["1024"][0], g["results"])
+        sts = hw.join_wait_all()
+        assert [(st.filtered, st.matches) for st in sts] == [(g["rows"]["basic"][1], g["results"]),
+                                                             (g["rows"]["1024"][0], g["results"])]
 
 
 def test_back_to_back_joins_of_mixed_configs_on_one_stream(hw, cuda):
     """Async joins of different filter configurations back to back on one stream: no wait packet
     between them (stream order), the counts zeroed by each join's own first kernel (the R scatter's
     workgroup 0; the basic k >= 2 pipeline zeroes by memset), the job table cleared when its layout
-    changes. The last join's counts are its golden's."""
+    changes. Every join's counts (hwbrj_join_wait_all) are its golden's."""
     g = GOLD["F3_grid"]
     R = cuda.empty((g["r"], 2), dtype=cuda.int32, device="cuda")
     S = cuda.empty((g["s"], 2), dtype=cuda.int32, device="cuda")
@@ -152,8 +153,8 @@ def test_back_to_back_joins_of_mixed_configs_on_one_stream(hw, cuda):
     for seq in ((basic2, blocked, basic1), (blocked, basic1, basic2), (basic1, basic2, blocked), (blocked, blocked)):
         for a in seq:
             hw.join_device_async(R, S, a, stream=s1)
-        st = hw.join_wait()
-        assert (st.filtered, st.matches) == (want[id(seq[-1])], g["results"]), seq
+        sts = hw.join_wait_all()
+        assert [(st.filtered, st.matches) for st in sts] == [(want[id(a)], g["results"]) for a in seq], seq
     st = hw.join_device(R, S, basic1)
     assert (st.filtered, st.matches) == (want[id(basic1)], g["results"])
 

@@ -255,7 +255,7 @@ def test_repeatable_and_buffer_reuse(hw, cuda, f3):
 
 
 def test_async_joins_back_to_back(hw, cuda, f3):
-    """hwbrj_join_device_async x3 then hwbrj_join_wait: the last join's counts are the golden's.
+    """hwbrj_join_device_async x3 then hwbrj_join_wait_all: every join's counts are the golden's.
     Async joins record no phase events (counts only); a synchronous join after them measures its
     phases again."""
     g = GOLD["F3_grid"]
@@ -263,8 +263,9 @@ def test_async_joins_back_to_back(hw, cuda, f3):
     args = hw.BloomFilterArgs(hw.BLOCKED, g["m"], 1, 1024)
     for _ in range(3):
         hw.join_device_async(R, S, args)
-    st = hw.join_wait()
-    assert (st.filtered, st.matches) == (g["rows"]["1024"][0], g["results"])
+    sts = hw.join_wait_all()
+    assert [(st.filtered, st.matches) for st in sts] == [(g["rows"]["1024"][0], g["results"])] * 3
+    st = sts[-1]
     assert st.ms_total == 0 and st.ms_probe == 0
     st = hw.join_device(R, S, args)
     assert (st.filtered, st.matches) == (g["rows"]["1024"][0], g["results"])
