@@ -18,7 +18,7 @@ import numpy as np
 
 __all__ = [
     "BASIC", "BLOCKED", "SECTORIZED", "BloomFilterArgs", "Relation", "Result", "Stats",
-    "BPRO", "PRO", "join_materialize_device", "set_materialize", "set_gpus", "BPRH", "BPRHO", "BRJ", "PRH", "PRHO", "RJ", "assert_args", "join_device", "join_device_async", "join_wait", "join_wait_all", "generate_device", "generate_device_range",
+    "BPRO", "PRO", "join_materialize_device", "set_materialize", "set_gpus", "BPRH", "BPRHO", "BRJ", "PRH", "PRHO", "RJ", "assert_args", "join_device", "join_device_async", "join_wait", "join_wait_all", "set_async_timing", "generate_device", "generate_device_range",
     "generate_host", "nonunique_threshold", "create_relation_nonunique",
     "create_relation_nonunique_from_pk", "create_relation_fk_from_pk", "create_relation_zipf",
     "rand_stream", "reference_relations", "create_relation_zipf_device",
@@ -106,6 +106,8 @@ def lib() -> ctypes.CDLL:
                                              ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(_Stats)]
         L.hwbrj_join_wait.restype = ctypes.c_int
         L.hwbrj_join_wait.argtypes = [ctypes.c_void_p]
+        L.hwbrj_set_async_timing.restype = ctypes.c_int
+        L.hwbrj_set_async_timing.argtypes = [ctypes.c_int]
         L.hwbrj_join_wait_all.restype = ctypes.c_int
         L.hwbrj_join_wait_all.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
         L.hwbrj_join_device.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
@@ -439,6 +441,12 @@ def join_wait() -> Stats:
     st = _Stats()
     _err(lib().hwbrj_join_wait(ctypes.byref(st)), "hwbrj_join_wait")
     return Stats(**{n: getattr(st, n) for n, _ in _Stats._fields_})
+
+
+def set_async_timing(on: bool) -> None:
+    """hwbrj_set_async_timing: async joins time their S scatter on the side stream that runs it
+    (Stats.ms_s_scatter of every async join); off by default."""
+    _err(lib().hwbrj_set_async_timing(1 if on else 0), "hwbrj_set_async_timing")
 
 
 def join_wait_all(capacity: int = 256) -> list:

@@ -214,6 +214,13 @@ int hwbrj_join_wait(hwbrj_stats_t* stats) {
     return e->wait(stats);
 }
 
+int hwbrj_set_async_timing(int on) {
+    Engine* e = engine_for_current_device();
+    if (!e) return 10;
+    e->set_async_timing(on != 0);
+    return 0;
+}
+
 int hwbrj_join_wait_all(hwbrj_stats_t* stats, int capacity, int* n_joins) {
     if (capacity < 0 || (capacity > 0 && !stats)) {
         set_last_error("stats must hold capacity >= 0 entries");

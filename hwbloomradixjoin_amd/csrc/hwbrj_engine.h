@@ -54,6 +54,9 @@ class Engine {
     // exceeds cap (the oldest cap are written).
     static constexpr int kJoinRing = 64;
     int  wait_all(hwbrj_stats_t* st, int cap, int* n);
+    // async joins time their S scatter (the dominant kernel) with events on the side stream they
+    // run it on: stats ms_s_scatter of every collected join (include/hwbrj.h hwbrj_set_async_timing)
+    void set_async_timing(bool on) { async_timing_ = on; }
     // Allocates every buffer a join of these inputs needs, without launching it (the host BPRO
     // stages this before its timed region, like the reference's allocations before its timer).
     int  reserve(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
@@ -196,6 +199,7 @@ class Engine {
     // joins enqueued on it (a destroyed stream's handle can be reused by a new one).
     hipStream_t  pending_stream_ = nullptr;
     bool         pending_sfirst_ = false;  // the pending join ran its S pass first (phase boundaries)
+    bool         pending_fused_  = false;  // ... or both pass-1 scatters in one launch (HWBRJ_FUSE_SR)
     bool         pending_fmt_    = false;  // the pending join counted its unstaged probe items
     bool         pending_pack3_  = false;  // the pending join packed its join keys
     bool         pending_slots_  = false;  // the pending join's matches are in k_join's partial sums
@@ -208,7 +212,7 @@ class Engine {
     // last (the reference sums every thread's count per run, parallel_radix_join_bloom.c:1696-1707)
     struct JoinRec {
         uint32_t slot = 0;
-        bool     args = false, fmt = false, pack3 = false, slots = false;
+        bool     args = false, fmt = false, pack3 = false, slots = false, timed = false;
         uint64_t nS   = 0;
         Geometry g{};
     };
@@ -217,6 +221,8 @@ class Engine {
     std::vector<hwbrj_stats_t> jdone_;  // collected early (the ring was full), oldest first
     uint32_t                   jr_next_ = 0;
     hwbrj_stats_t              last_st_{};  // the last collected join (with its phase times)
+    bool                       async_timing_ = false;      // hwbrj_set_async_timing
+    hipEvent_t                 tev_[kJoinRing][2] = {};    // per slot: the async S scatter's start, end
     void*        ring_take(uint32_t* slot);            // the next slot's bytes (jring_ grown first)
     void         ring_push(const JoinRec& r) { jr_.push_back(r); }
     int          ring_collect();                       // jr_ (completed) -> jdone_
@@ -244,6 +250,7 @@ class Engine {
     DevBuf ppoolR, ppoolS, rpay, survpos;
     DevBuf dense2, kkcnt;  // basic k >= 2: the second dense candidate buffer, per-pass counts
     DevBuf jtask, jparts;  // join task table; parts per job (+ the task count)
+    DevBuf jfb;            // k_join_dma's fallback list (count, jobs)
     // partitioned join: owned partitions' lists, tables and received survivor descriptors
     DevBuf pjList, pjLstart, pjSweep, pjTab, pjRegion, pjTot, pjSoff, pjIbase, pjCnt, pjOff, pjIstart, pjJobs;
     DevBuf pjBsum, pjBound, pjWtot, pjWscan, pjTab2;  // device-side item tables (scans, bounds)

@@ -174,6 +174,12 @@ int hwbrj_join_wait(hwbrj_stats_t * stats);
  * enqueue that finds all 64 in use first collects them on the host (one wait). *n_joins = the
  * number of joins; returns 7 when it exceeds capacity (the oldest `capacity` are written). */
 int hwbrj_join_wait_all(hwbrj_stats_t * stats, int capacity, int * n_joins);
+/* on != 0: async joins bracket their S scatter (k_scatter_s, the dominant kernel) with timing
+ * events on the side stream that runs it beside the R side, and hwbrj_join_wait / _wait_all report
+ * its device time as ms_s_scatter of every async join (the other ms_* stay 0). For measuring the
+ * kernel in the schedule the back-to-back joins run (bench.py's roofline); off by default, so the
+ * timed joins carry no markers. */
+int hwbrj_set_async_timing(int on);
 
 /* The join with result materialization (the reference's JOIN_RESULT_MATERIALIZE output,
  * src/parallel_radix_join_bloom.c:307-312): d_out[i] = {R.payload, S.payload} of every match, in

@@ -176,3 +176,22 @@ def test_northstar_async_every_join(hw, cuda):
     assert [(s.filtered, s.matches) for s in hw.join_wait_all()] == [runs[0][1]] * 3
     del R, S
     cuda.cuda.empty_cache()
+
+
+def test_async_timing_of_the_s_scatter(hw, cuda, rels, expected):
+    """hwbrj_set_async_timing: every async join of a back-to-back run reports the device time of
+    its S scatter as it ran on the side stream (ms_s_scatter > 0, the other phases 0), counts
+    unchanged; off again, async joins report no phase time."""
+    _, dR, _, dSs = rels
+    a = mk(hw, CONFIGS[0])
+    hw.set_async_timing(True)
+    try:
+        for si in range(3):
+            hw.join_device_async(dR, dSs[si], a)
+        sts = hw.join_wait_all()
+    finally:
+        hw.set_async_timing(False)
+    assert [(s.filtered, s.matches) for s in sts] == [expected[0, si] for si in range(3)]
+    assert all(s.ms_s_scatter > 0 and s.ms_probe == 0 and s.ms_total == 0 for s in sts), sts
+    hw.join_device_async(dR, dSs[0], a)
+    assert hw.join_wait().ms_s_scatter == 0

@@ -13,7 +13,8 @@ for p in $(seq $P); do
     E=HWBRJ_AB_VARIANT=1
     if [ "$v" = tree ]; then L=""; elif [[ "$v" == *:*=* ]]; then L=tools/abl_so/libhwbrj_${v%%:*}.so; E=${v#*:};
     elif [[ "$v" == *=* ]]; then L=""; E=$v; else L=tools/abl_so/libhwbrj_$v.so; fi
-    timeout -k 10 240 env HWBRJ_LIB=$L $E python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-e2e $ABFLAGS > $OUT/$v.$p.log 2>&1 || { echo "BENCH_FAIL $v"; tail -5 $OUT/$v.$p.log; exit 1; }
+    BP=bench.py; n=${v%%:*}; [ -f tools/abl_so/${n}_py/bench.py ] && BP=tools/abl_so/${n}_py/bench.py  # (a revision's own bench)
+    timeout -k 10 240 env HWBRJ_LIB=$L $E python3 $BP --steps 20 --warmup 5 --no-cpu-baseline --no-e2e $ABFLAGS > $OUT/$v.$p.log 2>&1 || { echo "BENCH_FAIL $v"; tail -5 $OUT/$v.$p.log; exit 1; }
     tail -1 $OUT/$v.$p.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); ph=d['phase_ms']; print('$v', d['ms_per_step'], d['parity']['ok'], ' '.join(f'{k}={v:.4f}' for k,v in ph.items()))"
   done
 done
