@@ -318,7 +318,7 @@ void Engine::release() {
     for (DevBuf* b : {&poolR, &metaR, &usedR, &wgqcR, &wgqeR, &wgqoR, &lstartR, &estartR, &istartR,
                       &listR, &poolS, &metaS, &usedS, &wgqcS, &wgqeS, &wgqoS, &lstartS, &estartS,
                       &istartS, &listS, &slices, &bitmap, &rjoin, &rrun, &surv, &survcnt, &survoff,
-                      &dense, &small, &bpos, &colR, &colS, &mtab, &mcount, &jtask, &jparts, &jfb, &pjList,
+                      &dense, &small, &bpos, &colR, &colS, &mtab, &mcount, &jtask, &jparts, &pjList,
                       &pjLstart, &pjSweep, &pjTab, &pjRegion, &pjTot, &pjSoff, &pjIbase, &pjCnt, &pjOff,
                       &pjIstart, &pjJobs, &ppoolR, &ppoolS, &rpay, &survpos, &dense2, &kkcnt, &xcnt_, &pjBsum, &pjBound, &pjWtot, &pjWscan, &pjTab2})
         b->release();
@@ -463,8 +463,7 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     // clears the whole buffer, so no stale count of an earlier job layout is read)
     const bool jnew = jparts.bytes < (size_t) (2 * NJ + 1) * 4 || NJ != last_nj_;
     last_nj_ = NJ;
-    ok &= jtask.ensure((size_t) join_extra_tasks() * 8) && jparts.ensure((size_t) (2 * NJ + 1) * 4) &&
-          jfb.ensure((size_t) (NJ + 1) * 4);
+    ok &= jtask.ensure((size_t) join_extra_tasks() * 8) && jparts.ensure((size_t) (2 * NJ + 1) * 4);
     if (slice_mode) ok &= slices.ensure((uint64_t) F * nseg * g.seg_words * 4);
     if (g.mode == MODE_GLOBAL) ok &= bitmap.ensure(((g.m + 31) / 32) * 4) && dense.ensure(nS * 4);
     if (basic_kk) ok &= bpos.ensure(nRk * 4);
@@ -544,11 +543,7 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
         return 0;
     };
     HWBRJ_CHECK(mark(0, stream));
-    // Pass-1 of S and R in one launch, then both sides' plans and lists in one launch each
-    // (HWBRJ_FUSE_SR): the R workgroups fill the S scatter's tail instead of a kernel boundary.
-    const bool fuse = HWBRJ_FUSE_SR && !mat && !basic_kk && !bcast && g.mode != MODE_GLOBAL &&
-                      g.s_format == g.format && !dev_knobs().ovl && !dev_knobs().rfirst;
-    const bool ovl = !fuse && (dev_knobs().ovl || (HWBRJ_OVL_ASYNC && !phase_ev_)) && g.mode != MODE_GLOBAL && !basic_kk &&
+    const bool ovl = (dev_knobs().ovl || (HWBRJ_OVL_ASYNC && !phase_ev_)) && g.mode != MODE_GLOBAL && !basic_kk &&
                      !mat && !bcast;
     if (ovl) {  // S pass on the side stream (with phase events, its phases would show inside the R side's)
         if (!ovl_stream_) {
@@ -575,7 +570,7 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     // Cache still holds much of them. Not in the global mode (the R scatter's workgroup 0 zeroes the
     // dense count the S pass's global probe adds to) nor for basic k >= 2 (the R side borrows the
     // S-side buffers).
-    const bool s_first = !fuse && !ovl && !dev_knobs().rfirst && g.mode != MODE_GLOBAL && !basic_kk;
+    const bool s_first = !ovl && !dev_knobs().rfirst && g.mode != MODE_GLOBAL && !basic_kk;
     if (s_first)
         if (const int rc = s_pass(stream, true)) return rc;
     // ---------------------------------------------------------------- R: pass-1 (+ filter)
@@ -591,56 +586,14 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     sp.wgq_chunks = wgqcR.as<uint32_t>();
     sp.wgq_elems  = wgqeR.as<uint32_t>();
     sp.cap        = capR;
-    if (fuse) {
-        ScatterParams ss = sp;  // the S side (workgroups [0, G) of the launch)
-        ss.zero_small    = nullptr;
-        ss.zero_word     = nullptr;
-        ss.src           = dS;
-        ss.n             = nS;
-        ss.pool          = poolS.as<uint32_t>();
-        ss.meta          = metaS.as<uint32_t>();
-        ss.wg_used       = usedS.as<uint32_t>();
-        ss.wgq_chunks    = wgqcS.as<uint32_t>();
-        ss.wgq_elems     = wgqeS.as<uint32_t>();
-        ss.cap           = capS;
-        hipEvent_t* tev  = nullptr;  // (hwbrj_set_async_timing: the fused scatter, as timed joins run it)
-        if (async_timing_ && !phase_ev_) {
-            for (int i = 0; i < 2; i++)
-                if (!tev_[rslot][i]) HWBRJ_CHECK(hipEventCreateWithFlags(&tev_[rslot][i], hipEventDisableSystemFence));
-            tev = tev_[rslot];
-            HWBRJ_CHECK(hipEventRecord(tev[0], stream));
-        }
-        rtimed = tev != nullptr;
-        if (!launch_scatter_sr(ss, sp, G, G, stream)) {
-            set_last_error("internal: no fused scatter for this geometry");
-            return 1;
-        }
-        if (tev) HWBRJ_CHECK(hipEventRecord(tev[1], stream));
-        HWBRJ_CHECK(mark(4, stream));
-        const PlanArgs pS{wgqcS.as<uint32_t>(), wgqeS.as<uint32_t>(), G, g.log2F, wgqoS.as<uint32_t>(),
-                          colS.as<uint32_t>() + 2 * F, colS.as<uint64_t>()};
-        const PlanArgs pR{wgqcR.as<uint32_t>(), wgqeR.as<uint32_t>(), G, g.log2F, wgqoR.as<uint32_t>(),
-                          colR.as<uint32_t>() + 2 * F, colR.as<uint64_t>()};
-        launch_plan2(pS, pR, stream);
-        const ListFillArgs lS{metaS.as<uint32_t>(), usedS.as<uint32_t>(), capS, g.log2F, wgqoS.as<uint32_t>(),
-                              colS.as<uint32_t>() + 2 * F, colS.as<uint64_t>(), CH, nseg, lstartS.as<uint32_t>(),
-                              estartS.as<uint64_t>(), istartS.as<uint32_t>(), listS.as<uint32_t>()};
-        const ListFillArgs lR{metaR.as<uint32_t>(), usedR.as<uint32_t>(), capR, g.log2F, wgqoR.as<uint32_t>(),
-                              colR.as<uint32_t>() + 2 * F, colR.as<uint64_t>(), (uint32_t) BSW, 1,
-                              lstartR.as<uint32_t>(), estartR.as<uint64_t>(), istartR.as<uint32_t>(),
-                              listR.as<uint32_t>()};
-        launch_list_fill2(lS, G, lR, G, stream);
-        HWBRJ_CHECK(mark(5, stream));
-    } else {
-        launch_scatter(sp, SRC_TUPLES, SIDE_R, G, stream);
-        HWBRJ_CHECK(mark(1, stream));
-        launch_plan(wgqcR.as<uint32_t>(), wgqeR.as<uint32_t>(), G, g.log2F, wgqoR.as<uint32_t>(),
-                    colR.as<uint32_t>() + 2 * F, colR.as<uint64_t>(), stream);
-        launch_list_fill(metaR.as<uint32_t>(), usedR.as<uint32_t>(), capR, g.log2F, wgqoR.as<uint32_t>(),
-                         colR.as<uint32_t>() + 2 * F, colR.as<uint64_t>(), (uint32_t) BSW, 1, lstartR.as<uint32_t>(),
-                         estartR.as<uint64_t>(), istartR.as<uint32_t>(), listR.as<uint32_t>(), G, stream);
-        HWBRJ_CHECK(mark(2, stream));
-    }
+    launch_scatter(sp, SRC_TUPLES, SIDE_R, G, stream);
+    HWBRJ_CHECK(mark(1, stream));
+    launch_plan(wgqcR.as<uint32_t>(), wgqeR.as<uint32_t>(), G, g.log2F, wgqoR.as<uint32_t>(),
+                colR.as<uint32_t>() + 2 * F, colR.as<uint64_t>(), stream);
+    launch_list_fill(metaR.as<uint32_t>(), usedR.as<uint32_t>(), capR, g.log2F, wgqoR.as<uint32_t>(),
+                     colR.as<uint32_t>() + 2 * F, colR.as<uint64_t>(), (uint32_t) BSW, 1, lstartR.as<uint32_t>(),
+                     estartR.as<uint64_t>(), istartR.as<uint32_t>(), listR.as<uint32_t>(), G, stream);
+    HWBRJ_CHECK(mark(2, stream));
     sp.ppool      = nullptr;
     sp.zero_small = nullptr;
     sp.zero_word  = nullptr;
@@ -660,7 +613,7 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     bp.out_pay     = mat ? rpay.as<uint32_t>() : nullptr;
     // 3-byte join keys from build / probe to k_join, unless the last join this Engine waited for had
     // probe items too large for the stage (their 32-bit survivor runs make the join read two formats,
-    // k_join_rest): a performance hint only, both paths give the same counts
+    // k_join_mixed): a performance hint only, both paths give the same counts
     const bool pack3 = !mat && join_pack3(g) && pack3_hint_;
     bp.pack3       = pack3 ? 1u : 0u;
     // the broadcast: rank 0 builds the slices, the other ranks only sub-partition R for the join
@@ -710,7 +663,7 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
         HWBRJ_CHECK(hipStreamWaitEvent(stream, ovl_ev_[1], 0));
         HWBRJ_CHECK(mark(4, stream));
         HWBRJ_CHECK(mark(5, stream));
-    } else if (!s_first && !fuse) {
+    } else if (!s_first) {
         if (const int rc = s_pass(stream, true)) return rc;
     }
     ProbeParams pp{};
@@ -770,7 +723,6 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     jp.r_pack3         = pack3 ? 1u : 0u;
     jp.fmt_cnt         = pp.fmt_cnt;
     jp.timing          = phase_ev_ ? 1u : 0u;  // (back-to-back joins: counts only)
-    jp.fb              = jfb.as<uint32_t>();   // (k_join_dma's fallback list, bitmap launches)
     if (mat) {
         // (k_join_split, which leaves job_surv zero for the next join, does not run here)
         HWBRJ_CHECK(hipMemsetAsync(jparts.as<uint32_t>() + NJ, 0, (size_t) NJ * 4, stream));
@@ -809,7 +761,6 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     pending_nS_   = nS;
     pending_ev_   = phase_ev_;
     pending_sfirst_ = s_first;
-    pending_fused_  = fuse;
     pending_fmt_    = pp.fmt_cnt != nullptr;
     pending_pack3_  = pack3;
     pending_slots_  = !mat;
@@ -918,8 +869,7 @@ int Engine::enqueue_basic_kk(const uint2* dR, uint64_t nR, const uint2* dS, uint
     ok &= jring_.ensure(kJoinRing * ring_slot_bytes()) && colR.ensure(Fm * 12) && colS.ensure(Fm * 12);
     const bool jnew = jparts.bytes < (size_t) (2 * NJ + 1) * 4 || NJ != last_nj_;
     last_nj_ = NJ;
-    ok &= jtask.ensure((size_t) join_extra_tasks() * 8) && jparts.ensure((size_t) (2 * NJ + 1) * 4) &&
-          jfb.ensure((size_t) (NJ + 1) * 4);
+    ok &= jtask.ensure((size_t) join_extra_tasks() * 8) && jparts.ensure((size_t) (2 * NJ + 1) * 4);
     ok &= slices.ensure((uint64_t) F * nseg * g.seg_words * 4) && (g.k <= G || bpos.ensure(nRk * 4));
     const uint32_t NC = (g.k + 64) & ~63u;  // pass counters [0, k - 1) + the dummy [NC - 1]
     ok &= dense.ensure(G * rw * 4) && dense2.ensure(G * rw * 4) && kkcnt.ensure(NC * 8 + 2 * G * 4);
@@ -1097,7 +1047,6 @@ int Engine::enqueue_basic_kk(const uint2* dR, uint64_t nR, const uint2* dS, uint
     jp.jkind           = (uint32_t) jkind;
     jp.split_surv      = test_hooks().join_split;
     jp.timing          = phase_ev_ ? 1u : 0u;
-    jp.fb              = jfb.as<uint32_t>();
     launch_join(jp, NJ, jparts.as<uint32_t>() + NJ, stream);
     HWBRJ_CHECK(hipEventRecord(ev_[8], stream));
     HWBRJ_CHECK(hipGetLastError());
@@ -1107,7 +1056,6 @@ int Engine::enqueue_basic_kk(const uint2* dR, uint64_t nR, const uint2* dS, uint
     pending_nS_   = nS;
     pending_ev_   = phase_ev_;
     pending_sfirst_ = false;
-    pending_fused_  = false;
     pending_fmt_    = false;
     pending_pack3_  = false;
     pending_slots_  = true;
@@ -1203,21 +1151,17 @@ int Engine::ring_collect() {
 
 // Waits for the last join and collects every join since the last wait; the last one's phase times
 // (synchronous joins) are read from its events.
-static int wait_common(hwbrj_stats_t* last, bool phases, const hipEvent_t* ev, bool sfirst, bool surv_fused,
-                       bool fused) {
+static int wait_common(hwbrj_stats_t* last, bool phases, const hipEvent_t* ev, bool sfirst, bool surv_fused) {
     float ms[9] = {0, 0, 0, 0, (float) last->ms_s_scatter, 0, 0, 0, 0};  // (async: the timed S scatter only)
     if (phases) {  // (async joins: counts only)
         hipEvent_t e[9];
         for (int i = 0; i <= 8; i++) e[i] = ev[i];
         if (surv_fused) e[7] = ev[6];
         // phase i ends at boundary i and starts at boundary from[i] (S pass first: it starts the
-        // join, the R scatter starts after the S lists, the probe after the build; fused pass-1:
-        // both scatters are the s_scatter phase, both sides' lists the s_index phase, -1 = none)
-        static const int kFrom[3][9] = {{0, 0, 1, 2, 3, 4, 5, 6, 7}, {0, 5, 1, 2, 0, 4, 3, 6, 7},
-                                        {0, -1, -1, 5, 0, 4, 3, 6, 7}};
-        const int* from = kFrom[fused ? 2 : sfirst ? 1 : 0];
-        for (int i = 1; i <= 8; i++)
-            if (from[i] >= 0) HWBRJ_CHECK(hipEventElapsedTime(&ms[i], e[from[i]], e[i]));
+        // join, the R scatter starts after the S lists, the probe after the build)
+        static const int kFrom[2][9] = {{0, 0, 1, 2, 3, 4, 5, 6, 7}, {0, 5, 1, 2, 0, 4, 3, 6, 7}};
+        const int* from = kFrom[sfirst ? 1 : 0];
+        for (int i = 1; i <= 8; i++) HWBRJ_CHECK(hipEventElapsedTime(&ms[i], e[from[i]], e[i]));
         HWBRJ_CHECK(hipEventElapsedTime(&ms[0], e[0], e[8]));
     }
     const double pt = last->ms_join_probe, jt = last->ms_join;  // (ticks, ring_collect)
@@ -1252,7 +1196,7 @@ int Engine::wait_all(hwbrj_stats_t* st, int cap, int* n) {
     if (const int rc = ring_collect()) return rc;
     for (size_t i = 0; i < jdone_.size(); i++) {  // ticks -> ms (only the last has phase times)
         if (i + 1 == jdone_.size()) {
-            if (const int rc = wait_common(&jdone_[i], pending_ev_, ev_, pending_sfirst_, surv_fused_, pending_fused_)) return rc;
+            if (const int rc = wait_common(&jdone_[i], pending_ev_, ev_, pending_sfirst_, surv_fused_)) return rc;
         } else {
             jdone_[i].ms_join_probe = jdone_[i].ms_join = 0;  // (the ticks: not phase times)
         }
@@ -1287,7 +1231,7 @@ int Engine::wait(hwbrj_stats_t* st) {
     if (!jdone_.empty()) {  // (else: the last join was collected before; its stats again)
         last_st_ = jdone_.back();
         jdone_.clear();
-        if (const int rc = wait_common(&last_st_, pending_ev_, ev_, pending_sfirst_, surv_fused_, pending_fused_)) return rc;
+        if (const int rc = wait_common(&last_st_, pending_ev_, ev_, pending_sfirst_, surv_fused_)) return rc;
     }
     if (st) *st = last_st_;
     return 0;

@@ -199,7 +199,6 @@ class Engine {
     // joins enqueued on it (a destroyed stream's handle can be reused by a new one).
     hipStream_t  pending_stream_ = nullptr;
     bool         pending_sfirst_ = false;  // the pending join ran its S pass first (phase boundaries)
-    bool         pending_fused_  = false;  // ... or both pass-1 scatters in one launch (HWBRJ_FUSE_SR)
     bool         pending_fmt_    = false;  // the pending join counted its unstaged probe items
     bool         pending_pack3_  = false;  // the pending join packed its join keys
     bool         pending_slots_  = false;  // the pending join's matches are in k_join's partial sums
@@ -250,7 +249,6 @@ class Engine {
     DevBuf ppoolR, ppoolS, rpay, survpos;
     DevBuf dense2, kkcnt;  // basic k >= 2: the second dense candidate buffer, per-pass counts
     DevBuf jtask, jparts;  // join task table; parts per job (+ the task count)
-    DevBuf jfb;            // k_join_dma's fallback list (count, jobs)
     // partitioned join: owned partitions' lists, tables and received survivor descriptors
     DevBuf pjList, pjLstart, pjSweep, pjTab, pjRegion, pjTot, pjSoff, pjIbase, pjCnt, pjOff, pjIstart, pjJobs;
     DevBuf pjBsum, pjBound, pjWtot, pjWscan, pjTab2;  // device-side item tables (scans, bounds)

@@ -51,9 +51,6 @@ inline bool join_pack3(const Geometry& g) { return HWBRJ_PACK3 != 0 && g.sub_shi
 #ifndef HWBRJ_OVL_ASYNC
 #define HWBRJ_OVL_ASYNC 1
 #endif
-#ifndef HWBRJ_FUSE_SR
-#define HWBRJ_FUSE_SR 0  // 1: pass-1 of S and R in one launch (k_scatter_sr, k_plan2, k_list_fill2)
-#endif
 #ifndef HWBRJ_PJ_OVL
 #define HWBRJ_PJ_OVL 1  // async partitioned joins: the S shard's partitioning on a second stream
 #endif
@@ -135,8 +132,6 @@ struct JoinParams {
     const uint32_t* fmt_cnt;      // ProbeParams::fmt_cnt (the launch's survivor-run formats), or nullptr
     uint32_t        timing;       // 1: accumulate the probe / total ticks (result[3], result[4]) for
                                   // ms_join_probe (synchronous joins; 0: one count add per workgroup)
-    uint32_t*       fb;           // [1 + jobs]: count, then the jobs k_join_dma leaves to k_join_rest;
-                                  // nullptr: no k_join_dma (k_join runs every job)
 };
 
 // The materializing join (k_join_mat): R codes + payloads of the build sweeps, survivors + their
@@ -182,34 +177,6 @@ size_t scatter_lds_bytes(uint32_t log2F);
 size_t scatter_pay_lds_bytes(uint32_t log2F);  // (ScatterParams::ppool set)
 enum { SIDE_R = 0, SIDE_S = 1 };  // which relation a scatter partitions (kernel name; S uses g.s_format)
 void   launch_scatter(const ScatterParams& p, int src, int side, uint32_t grid, hipStream_t st);
-// pass-1 of S (workgroups [0, GS)) and R ([GS, GS + GR)) in one launch (tuples, one geometry, no
-// payloads, S words in the R format); false (nothing launched) otherwise
-bool   launch_scatter_sr(const ScatterParams& s, const ScatterParams& r, uint32_t GS, uint32_t GR, hipStream_t st);
-// k_plan's and k_list_fill's arguments, for the launches of both sides at once
-struct PlanArgs {
-    const uint32_t* wgq_chunks;
-    const uint32_t* wgq_elems;
-    uint32_t        G, log2F;
-    uint32_t*       wgq_off;
-    uint32_t*       colc;
-    uint64_t*       cole;
-};
-struct ListFillArgs {
-    const uint32_t* meta;
-    const uint32_t* wg_used;
-    uint64_t        cap;
-    uint32_t        log2F;
-    const uint32_t* wgq_off;
-    const uint32_t* colc;
-    const uint64_t* cole;
-    uint32_t        CH, nseg;
-    uint32_t*       list_start;
-    uint64_t*       elem_start;
-    uint32_t*       item_start;
-    uint32_t*       list;
-};
-bool   launch_plan2(const PlanArgs& a, const PlanArgs& b, hipStream_t st);
-void   launch_list_fill2(const ListFillArgs& a, uint32_t ga, const ListFillArgs& b, uint32_t gb, hipStream_t st);
 // k_plan: per-(wg, q) list offsets + per-partition chunk / element totals (colc, cole);
 // k_list_fill: scans the totals into list / element / item starts [F + 1] and fills the lists.
 void   launch_list_fill(const uint32_t* meta, const uint32_t* wg_used, uint64_t cap,

@@ -582,7 +582,7 @@ struct ScRaw {  // one round's raw loads of this thread (tuples: keys only; code
 // LDS: static CRC nibble table (512 B, at 0, so its row offsets are immediates); dynamic (words):
 // stage F x 32 | 64 dummy slots | fill F + 4 | ncb 2F | flq F | misc 8 (per-partition totals: registers of the plan thread)
 template <int SRC, int MODE, int FMT, int SAUX = HWBRJ_SC_SAUX>
-__device__ __forceinline__ void scatter_body(const ScatterParams& P, const uint32_t wgi, const uint32_t Gi) {
+__device__ __forceinline__ void scatter_body(const ScatterParams& P) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     __shared__ uint32_t crc_tab[128];
     constexpr int NL = SRC == SRC_TUPLES ? kScE / 2 : kScE / 4;  // uint4 loads per thread per round
@@ -609,13 +609,13 @@ __device__ __forceinline__ void scatter_body(const ScatterParams& P, const uint3
         crc_tab[tid] = v;
     }
     if (tid < 8) misc[tid] = 0;
-    if (wgi == 0 && P.zero_small && tid < 16) P.zero_small[tid] = 0;
-    if (wgi == 0 && P.zero_word && tid == 0) *P.zero_word = 0;
+    if (blockIdx.x == 0 && P.zero_small && tid < 16) P.zero_small[tid] = 0;
+    if (blockIdx.x == 0 && P.zero_word && tid == 0) *P.zero_word = 0;
 
-    if (P.dbg && tid == 0) P.dbg[wgi * 8 + 6] = __builtin_amdgcn_s_memrealtime();  // dev-only: start
+    if (P.dbg && tid == 0) P.dbg[blockIdx.x * 8 + 6] = __builtin_amdgcn_s_memrealtime();  // dev-only: start
     const uint64_t n     = P.n_dev ? *P.n_dev : P.n;
     const uint64_t units = (n + 3) >> 2;
-    const uint64_t G = Gi, wg = wgi;
+    const uint64_t G = gridDim.x, wg = blockIdx.x;
     uint64_t       e0  = 4 * (wg * units / G);
     const uint64_t e1r = 4 * ((wg + 1) * units / G);
     const uint64_t e1  = e1r < n ? e1r : n;
@@ -1268,19 +1268,17 @@ constexpr uint32_t kPlanCols  = HWBRJ_PLANCOLS;
 constexpr uint32_t kPlanRGs   = 1024 / kPlanCols;   // row groups per block
 constexpr uint32_t kPlanMaxRG = 512 / kPlanRGs;     // rows per row group: G <= 512 scatter workgroups
 
-__device__ __forceinline__ void plan_body(const PlanArgs& A, const uint32_t blk) {
-    const uint32_t* __restrict__ wgq_chunks = A.wgq_chunks;
-    const uint32_t* __restrict__ wgq_elems  = A.wgq_elems;
-    uint32_t* __restrict__       wgq_off    = A.wgq_off;
-    uint32_t* __restrict__       colc       = A.colc;
-    uint64_t* __restrict__       cole       = A.cole;
-    const uint32_t               G = A.G, log2F = A.log2F;
+__global__ __launch_bounds__(1024) void k_plan(const uint32_t* __restrict__ wgq_chunks,
+                                               const uint32_t* __restrict__ wgq_elems, uint32_t G,
+                                               uint32_t log2F, uint32_t* __restrict__ wgq_off,
+                                               uint32_t* __restrict__ colc,
+                                               uint64_t* __restrict__ cole) {
     __shared__ uint32_t tc[16][kPlanCols];  // per wave and column: chunk sum of its row groups
     __shared__ uint64_t te[16][kPlanCols];
     const uint32_t F = 1u << log2F;
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const uint32_t cl = threadIdx.x % kPlanCols, rg = threadIdx.x / kPlanCols;
-    const uint32_t col = blk * kPlanCols + cl;
+    const uint32_t col = blockIdx.x * kPlanCols + cl;
     const bool     okc = col < F;
     const uint32_t RG  = (G + kPlanRGs - 1) / kPlanRGs;
     const uint32_t r0  = min(G, rg * RG), r1 = min(G, r0 + RG);
@@ -1327,13 +1325,6 @@ __device__ __forceinline__ void plan_body(const PlanArgs& A, const uint32_t blk)
     }
 }
 
-__global__ __launch_bounds__(1024) void k_plan(PlanArgs A) { plan_body(A, blockIdx.x); }
-// both sides' scans in one launch: blocks [0, nbA) side A, the rest side B
-__global__ __launch_bounds__(1024) void k_plan2(PlanArgs A, PlanArgs B, uint32_t nbA) {
-    if (blockIdx.x < nbA) plan_body(A, blockIdx.x);
-    else plan_body(B, blockIdx.x - nbA);
-}
-
 // One block per scatter region: every chunk of the region gets its slot in its partition's list
 // (slots of (wg, q) start at list_start[q] + wgq_off[wg][q]). The region's metas are taken in
 // batches of kLfBatch, counting-sorted by partition in LDS and written out as contiguous runs per
@@ -1346,19 +1337,17 @@ constexpr uint32_t kLfPer     = HWBRJ_LFPER;
 constexpr uint32_t kLfBatch   = kLfThreads * kLfPer;
 static_assert(kLfBatch <= (1u << 17), "batch-local index in 17 bits of a packed entry");
 
-__device__ __forceinline__ void list_fill_body(const ListFillArgs& A, const uint32_t wg) {
-    const uint32_t* __restrict__ meta       = A.meta;
-    const uint32_t* __restrict__ wg_used    = A.wg_used;
-    const uint64_t               cap        = A.cap;
-    const uint32_t               log2F      = A.log2F;
-    const uint32_t* __restrict__ wgq_off    = A.wgq_off;
-    const uint32_t* __restrict__ colc       = A.colc;
-    const uint64_t* __restrict__ cole       = A.cole;
-    const uint32_t               CH         = A.CH, nseg = A.nseg;
-    uint32_t* __restrict__       list_start = A.list_start;
-    uint64_t* __restrict__       elem_start = A.elem_start;
-    uint32_t* __restrict__       item_start = A.item_start;
-    uint32_t* __restrict__       list       = A.list;
+__global__ __launch_bounds__(kLfThreads) void k_list_fill(const uint32_t* __restrict__ meta,
+                                                          const uint32_t* __restrict__ wg_used,
+                                                          uint64_t cap, uint32_t log2F,
+                                                          const uint32_t* __restrict__ wgq_off,
+                                                          const uint32_t* __restrict__ colc,
+                                                          const uint64_t* __restrict__ cole,
+                                                          uint32_t CH, uint32_t nseg,
+                                                          uint32_t* __restrict__ list_start,
+                                                          uint64_t* __restrict__ elem_start,
+                                                          uint32_t* __restrict__ item_start,
+                                                          uint32_t* __restrict__ list) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const uint32_t F    = 1u << log2F;
     // sorted batch entries, packed: partition | (count - 1) << 10 | batch-local index << 15
@@ -1370,6 +1359,7 @@ __device__ __forceinline__ void list_fill_body(const ListFillArgs& A, const uint
     uint32_t*      dcur = cur + F;            // [F] cur - off: the entry sorted to pos goes to list[dcur[q] + pos]
     uint32_t*      wtot = dcur + F;           // [16] wave totals of the scan
     const uint32_t tid  = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t wg   = blockIdx.x;
     {
         // exclusive scans over the F <= 1024 partitions of the column totals (k_plan): list starts
         // (every block), element and probe-item starts (block 0 publishes all three)
@@ -1474,13 +1464,6 @@ __device__ __forceinline__ void list_fill_body(const ListFillArgs& A, const uint
         }
         __syncthreads();
     }
-}
-
-__global__ __launch_bounds__(kLfThreads) void k_list_fill(ListFillArgs A) { list_fill_body(A, blockIdx.x); }
-// both sides' lists in one launch: blocks [0, GA) side A's regions, the rest side B's
-__global__ __launch_bounds__(kLfThreads) void k_list_fill2(ListFillArgs A, ListFillArgs B, uint32_t GA) {
-    if (blockIdx.x < GA) list_fill_body(A, blockIdx.x);
-    else list_fill_body(B, blockIdx.x - GA);
 }
 
 // ======================================================== chunk-walking helpers (8 lanes)
@@ -2415,10 +2398,9 @@ __global__ __launch_bounds__(256) void k_join_split(const uint32_t* __restrict__
                                                      uint32_t log2NSUB, uint32_t NJ, uint32_t split,
                                                      uint32_t* __restrict__ nparts,
                                                      uint2* __restrict__ extra, uint32_t* nextra,
-                                                     uint64_t* __restrict__ jsum, uint32_t* __restrict__ fb) {
+                                                     uint64_t* __restrict__ jsum) {
     if (blockIdx.x == 0 && threadIdx.x < kJoinSumSlots)
         for (int w = 0; w < 3; w++) jsum[threadIdx.x * kJoinSumStride + w] = 0;
-    if (blockIdx.x == 0 && threadIdx.x == 0 && fb) fb[0] = 0;
     const uint32_t job = blockIdx.x * blockDim.x + threadIdx.x;  // one thread per job
     if (job >= NJ) return;
     const uint32_t q = job >> log2NSUB, items = item_start[q + 1] - item_start[q];
@@ -2453,7 +2435,7 @@ struct JoinShared {
 
 template <bool MIXED>
 __device__ __forceinline__ void join_job(const JoinParams& P, const uint32_t blk, JoinShared& L, uint64_t& cnt_acc,
-                                         uint64_t& tp_acc, const int64_t forced_job = -1) {
+                                         uint64_t& tp_acc) {
     uint32_t* const tab   = L.tab;
     uint64_t* const dbase = L.dbase;
     uint32_t* const dcnt  = L.dcnt;
@@ -2471,9 +2453,7 @@ __device__ __forceinline__ void join_job(const JoinParams& P, const uint32_t blk
     // consecutive jobs -- the 16 subs of a partition run on one XCD, where the lines their runs
     // share (adjacent sub runs in every sweep slot and item region) are fetched into its L2 once
     if (HWBRJ_JXCD && blk < P.jobs && (P.jobs & 7u) == 0) job = (blk & 7u) * (P.jobs >> 3) + (blk >> 3);
-    if (forced_job >= 0) {               // (k_join_rest: part 0 of a job k_join_dma left to this path)
-        job = (uint32_t) forced_job;
-    } else if (blk >= P.jobs) {          // extra workgroups: further parts of skewed jobs
+    if (blk >= P.jobs) {                 // extra workgroups: further parts of skewed jobs
         const uint32_t e = blk - P.jobs;
         if (e >= min(*P.nextra, kJoinExtra)) return;
         const uint2 x = P.extra[e];
@@ -2524,7 +2504,7 @@ __device__ __forceinline__ void join_job(const JoinParams& P, const uint32_t blk
     // packed when their probe item was staged (bit 31 of surv_off). P.fmt_cnt counts the unstaged
     // items: with none (or no pack3 at all) every run of the launch has one format, whose stride,
     // shift and mask are uniform (k_join); otherwise the survivor runs are mixed and read with a
-    // per-run format (k_join_rest: only where probe items overflow their stage), R runs packed.
+    // per-run format (k_join_mixed: only where probe items overflow their stage), R runs packed.
     // Loads stay raw until used (key()): ALU work on a conditionally loaded value would make the
     // wave wait for it at once.
     constexpr uint64_t kPk = 1ull << 63;
@@ -2903,365 +2883,23 @@ __device__ __forceinline__ void join_finish(const JoinParams& P, uint64_t cnt, u
 __global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
     __shared__ JoinShared L;
     const bool mixed = __builtin_amdgcn_readfirstlane(P.r_pack3 && P.fmt_cnt && *P.fmt_cnt ? 1u : 0u) != 0;
-    if (mixed) return;  // (k_join_rest's launch)
+    if (mixed) return;  // (k_join_mixed's launch)
     const uint64_t t_start = P.timing ? wall_clock64() : 0;
     uint64_t       cnt = 0, t_probe = 0;
     join_job<false>(P, blockIdx.x, L, cnt, t_probe);
     join_finish(P, cnt, t_probe, t_start);
 }
 
-// The jobs k_join does not run (persistent, a small grid): every job of a launch with survivor runs
-// of both formats (MIXED), or, after k_join_dma (P.fb), the jobs it left (duplicate R keys, more
-// runs or bytes than its LDS holds) and the further parts of skewed jobs. Empty (~5 us) otherwise.
-__global__ __launch_bounds__(kJoinThreads) void k_join_rest(JoinParams P) {
+__global__ __launch_bounds__(kJoinThreads) void k_join_mixed(JoinParams P) {
     __shared__ JoinShared L;
-    const bool mixed = P.r_pack3 && P.fmt_cnt && *P.fmt_cnt;
-    if (!mixed && !P.fb) return;
+    if (!(P.r_pack3 && P.fmt_cnt && *P.fmt_cnt)) return;
     const uint64_t t_start = P.timing ? wall_clock64() : 0;
     uint64_t       cnt = 0, t_probe = 0;
-    if (mixed) {
-        for (uint32_t b = blockIdx.x; b < P.jobs + kJoinExtra; b += gridDim.x) {
-            __syncthreads();  // the previous job's LDS reads are done
-            join_job<true>(P, b, L, cnt, t_probe);
-        }
-    } else {
-        const uint32_t nfb = P.fb[0], nx = min(*P.nextra, kJoinExtra);
-        if (nfb + nx == 0) return;
-        for (uint32_t b = blockIdx.x; b < nfb + nx; b += gridDim.x) {
-            __syncthreads();
-            if (b < nfb) join_job<false>(P, 0, L, cnt, t_probe, (int64_t) P.fb[1 + b]);
-            else join_job<false>(P, P.jobs + (b - nfb), L, cnt, t_probe);
-        }
+    for (uint32_t b = blockIdx.x; b < P.jobs + kJoinExtra; b += gridDim.x) {
+        __syncthreads();  // the previous job's LDS reads are done
+        join_job<true>(P, b, L, cnt, t_probe);
     }
     join_finish(P, cnt, t_probe, t_start);
-}
-
-// ===================================================== K10d: the join's bitmap jobs by LDS-DMA
-// Persistent, one 1024-thread workgroup per CU, for launches whose jobs take the bitmap path
-// (P.bitmap, bucket chaining's role, one key format). A job's runs -- its R runs (one per build
-// sweep of q) and its survivor runs (one per probe item) -- are copied into LDS by LDS-DMA
-// (global_load_lds_dwordx4: whole 16-byte blocks, one 1 KiB wave-instruction per 64 blocks, no
-// VGPRs), and read back from LDS as keys. Two job buffers: while job t is tested, job t + 1's
-// runs are in flight, and the descriptors of job t + 2 (two dependent loads: the job's partition
-// tables, then its run counts and offsets) are loaded one and two jobs ahead, so the memory pipe
-// is fed across the job boundaries that k_join's 4-workgroups-per-CU scheme leaves idle (DESIGN
-// s9, round 5: one dword per key at 3-byte strides capped its load phases at ~4 TB/s). Every
-// barrier while a DMA is in flight is a raw s_barrier with lgkmcnt(0): __syncthreads() would
-// drain the DMA (vmcnt(0)). Jobs it cannot take (duplicate R keys, > kJdMaxR / kJdMaxS runs, more
-// than kJdSlots blocks) go to P.fb for k_join_rest, with the further parts of skewed jobs.
-#ifndef HWBRJ_JDMA
-#define HWBRJ_JDMA 0  // 1: k_join_dma for bitmap launches (measured slower, DESIGN s9: not the default)
-#endif
-#ifndef HWBRJ_ABL_JD
-#define HWBRJ_ABL_JD 0  // dev ablation (results invalid): 1 no DMA (no fallback), 2 no job compute, 3 neither
-#endif
-constexpr int      kJdThreads = 1024;
-constexpr int      kJdWaves   = kJdThreads / 64;
-constexpr uint32_t kJdSlots   = 3584;  // 16-byte blocks of one job's runs (56 KiB)
-constexpr uint32_t kJdMaxR    = 64, kJdMaxS = 256, kJdRuns = kJdMaxR + kJdMaxS;
-struct JdDesc {
-    uint32_t gblk[kJdRuns];      // the run's first 16-byte block in r_codes / surv
-    uint16_t pre[kJdRuns + 1];   // its first block in the job buffer (exclusive scan of the blocks)
-    uint16_t cnt[kJdRuns];       // keys
-    uint8_t  head[kJdRuns];      // byte of its first key in the first block
-    uint32_t nr, ns, nrk, job;   // R runs, survivor runs, R keys, the job (ok: nr + ns > 0)
-};
-struct JdShared {
-    uint32_t tab[kJoinWords];               // bitmap (32 KiB)
-    uint4    buf[2][kJdSlots + 1];          // job buffers (+1: a key's second dword stays inside)
-    uint8_t  info[2][kJdSlots];             // per block: byte of its first key | keys starting in it << 4
-    JdDesc   d[2];
-    uint32_t wtot[kJdWaves];                // scan / reduction totals
-    uint32_t bits;                          // set bits of the job's bitmap
-};
-size_t join_dma_lds_bytes() { return sizeof(JdShared); }
-
-// One global_load_lds_dwordx4: 16 bytes per active lane into LDS at lds_byte + 16 * lane (M0 the
-// wave-uniform base). Issued as asm: the compiler's wait insertion treats the builtin as an LDS write
-// of unknown extent and makes every later LDS access wait for it (vmcnt(0)), which would drain the
-// next job's copy at the first bitmap write; here the kernel orders its buffers itself (vmcnt(0) and
-// a barrier before a buffer is read, a barrier after its last read before it is refilled). M0 is the
-// compiler's: saved and restored around the load (cdna_hip_programming.md's LDS-DMA recipe).
-__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_byte) {
-    uint32_t keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep)
-                 : "v"(gsrc), "s"(lds_byte)
-                 : "memory");
-}
-
-__device__ __forceinline__ void jd_barrier() {  // (DMA in flight survives it)
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-}
-
-// A job's header: the uniform tables of its partition (first of the two dependent descriptor loads)
-struct JdHdr {
-    int64_t  job = -1;
-    uint32_t w0 = 0, w1 = 0, qi0 = 0, i0 = 0, i1 = 0, lq0 = 0, npc = 1;
-};
-// A thread's run of a job (the second load): R run t (t < nRd) or survivor run t - nRd
-struct JdRun {
-    uint32_t cnt = 0, off = 0;
-    uint64_t e0 = 0;
-};
-
-__global__ __launch_bounds__(kJdThreads) void k_join_dma(JoinParams P) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t jd_lds[];
-    JdShared&      L   = *(JdShared*) jd_lds;
-    const bool     mixed = __builtin_amdgcn_readfirstlane(P.r_pack3 && P.fmt_cnt && *P.fmt_cnt ? 1u : 0u) != 0;
-    if (mixed) return;  // (k_join_rest)
-    const int      tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const uint32_t NSUB = 1u << P.log2NSUB, J = P.jobs, G = gridDim.x, b = blockIdx.x;
-    const bool     rpk  = P.r_pack3 != 0;
-    const uint32_t kst  = rpk ? 3u : 4u, ksh = rpk ? 0u : P.hash_shift, kmk = rpk ? 0xFFFFFFu : 0xFFFFFFFFu;
-    const uint8_t* const r8 = (const uint8_t*) P.r_codes;
-    const uint8_t* const s8 = (const uint8_t*) P.surv;
-    const uint64_t t_start = P.timing ? wall_clock64() : 0;
-    uint64_t       t_probe = 0, cnt = 0;
-    // the t-th job of this workgroup: XCD-aware (workgroups b, b + 8, ... run on one XCD and take
-    // neighbouring jobs, so a partition's subs share that XCD's L2 lines of their adjacent runs)
-    const bool     xcd = (J & 7u) == 0 && (G & 7u) == 0;
-    auto job_at = [&](uint32_t t) -> int64_t {
-        if (xcd) {
-            const uint32_t per = J >> 3, i = (b >> 3) + (G >> 3) * t;
-            return i < per ? (int64_t) ((b & 7u) * per + i) : -1;
-        }
-        const uint64_t j = (uint64_t) b + (uint64_t) G * t;
-        return j < J ? (int64_t) j : -1;
-    };
-    auto load_hdr = [&](uint32_t t) -> JdHdr {
-        JdHdr h;
-        h.job = job_at(t);
-        if (h.job < 0) return h;
-        const uint32_t job = (uint32_t) h.job, q = job >> P.log2NSUB;
-        h.w0  = P.r_sweep_start[q];
-        h.w1  = P.r_sweep_start[q + 1];
-        h.qi0 = P.item_start[q];
-        const uint32_t qi1 = P.item_start[q + 1], np = P.nparts[job];
-        h.i0  = h.qi0;  // (part 0; k_join_rest takes the further parts)
-        h.i1  = h.qi0 + (uint32_t) ((uint64_t) (qi1 - h.qi0) / np);
-        h.lq0 = P.item_base ? 0u : P.list_start[q];
-        h.npc = (qi1 - h.qi0) / P.nseg;  // probe pieces of q (items are segment-major)
-        return h;
-    };
-    auto load_run = [&](const JdHdr& h) -> JdRun {
-        JdRun r;
-        if (h.job < 0) return r;
-        const uint32_t s = (uint32_t) h.job & (NSUB - 1u);
-        const uint32_t nRd = h.w1 - h.w0, nSd = h.i1 - h.i0;
-        if (nRd > kJdMaxR || nSd > kJdMaxS) return r;  // (not this kernel's job)
-        if ((uint32_t) tid < nRd) {
-            const uint64_t x = (uint64_t) (h.w0 + tid) * NSUB + s;
-            r.cnt = P.r_cnt[x];
-            r.off = P.r_off[x];
-        } else if ((uint32_t) tid < nRd + nSd) {
-            const uint32_t it = h.i0 + (tid - nRd);
-            const uint64_t x  = (uint64_t) it * NSUB + s;
-            r.cnt = P.surv_cnt[x];
-            r.off = P.surv_off[x];
-            if (P.item_base) {
-                r.e0 = P.item_base[it];
-            } else {
-                const uint32_t local = it - h.qi0;
-                const uint32_t seg = local / h.npc, piece = local - seg * h.npc;
-                r.e0 = (uint64_t) seg * P.surv_seg_stride + (uint64_t) (h.lq0 + piece * P.CH) * 32;
-            }
-        }
-        return r;
-    };
-    // E1: job h's descriptors into d[bi] (its runs' layout in the buffer: a block scan over the
-    // threads, one per run); jobs this kernel does not take go to P.fb. Two barriers.
-    auto describe_job = [&](const JdHdr& h, const JdRun& r, int bi) {
-        JdDesc&        D   = L.d[bi];
-        const uint32_t nRd = h.job >= 0 ? h.w1 - h.w0 : 0u, nSd = h.job >= 0 ? h.i1 - h.i0 : 0u;
-        const bool     take = h.job >= 0 && nRd <= kJdMaxR && nSd <= kJdMaxS && nRd > 0 && nSd > 0;
-        const bool     mine = take && (uint32_t) tid < nRd + nSd;
-        uint64_t       tb = 0;
-        uint32_t       nblk = 0;
-        if (mine) {
-            if ((uint32_t) tid < nRd) {
-                tb = rpk ? (uint64_t) (h.w0 + tid) * P.slot * 4u + (uint64_t) r.off * 3u
-                         : ((uint64_t) (h.w0 + tid) * P.slot + r.off) * 4u;
-            } else {
-                const uint64_t off = r.off & 0x7FFFFFFFu;  // (one format per launch: bit 31 = rpk)
-                tb = rpk ? r.e0 * 4u + off * 3u : (r.e0 + off) * 4u;
-            }
-            nblk = r.cnt ? (uint32_t) (((tb & 15u) + (uint64_t) r.cnt * kst + 15u) >> 4) : 0u;
-        }
-        const uint32_t inc = wave_incl_scan_dpp(nblk);
-        if (lane == 63) L.wtot[wave] = inc;
-        jd_barrier();
-        uint32_t base = 0, tot = 0;
-#pragma unroll
-        for (int w = 0; w < kJdWaves; w++) {
-            const uint32_t x = L.wtot[w];
-            base += w < wave ? x : 0u;
-            tot += x;
-        }
-        const bool fits = take && tot <= kJdSlots;  // (uniform)
-        if (fits && mine) {
-            D.gblk[tid] = (uint32_t) (tb >> 4);
-            D.pre[tid]  = (uint16_t) (base + inc - nblk);
-            D.cnt[tid]  = (uint16_t) r.cnt;
-            D.head[tid] = (uint8_t) (tb & 15u);
-            if ((uint32_t) tid == nRd + nSd - 1) D.pre[tid + 1] = (uint16_t) (base + inc);
-        }
-        if (wave == 0) {  // (nRd <= 64: every R run is in wave 0) the job's R keys
-            const uint32_t t = __builtin_amdgcn_readlane(wave_incl_scan_dpp(mine && (uint32_t) tid < nRd ? r.cnt : 0u), 63);
-            if (lane == 0) {
-                D.nrk = t;
-                D.nr  = fits ? nRd : 0u;
-                D.ns  = fits ? nSd : 0u;
-                D.job = h.job >= 0 ? (uint32_t) h.job : 0u;
-                L.bits = 0;
-                if (!fits && h.job >= 0 && nRd > 0 && nSd > 0) {  // (empty jobs count nothing)
-                    const uint32_t k = atomicAdd(&P.fb[0], 1u);
-                    P.fb[1 + k] = (uint32_t) h.job;
-                }
-            }
-        }
-        jd_barrier();  // (wtot read by every wave; d[bi] complete)
-    };
-    // E2: the DMA of a described job: wave w copies runs w, w + 16, ...: 64 blocks per
-    // wave-instruction, lane-linear into the buffer; each lane also records its block's keys (the
-    // byte of the first key that starts in it and how many start in it), so the job is processed
-    // block by block, every thread independent of the runs
-    auto dma_job = [&](int bi) {
-        const JdDesc&  D  = L.d[bi];
-        const uint32_t nr = D.nr, nn = D.nr + D.ns;  // (uniform)
-        const uint32_t buf = (uint32_t) (uintptr_t) (const __attribute__((address_space(3))) uint4*) L.buf[bi];
-        uint8_t* const inf = L.info[bi];
-        for (uint32_t k = wave; k < nn; k += kJdWaves) {
-            const uint32_t p0 = __builtin_amdgcn_readfirstlane(D.pre[k]);  // (wave-uniform)
-            const uint32_t n  = __builtin_amdgcn_readfirstlane(D.pre[k + 1]) - p0;
-            const uint32_t h = D.head[k], c = D.cnt[k];
-            const uint8_t* src = (k < nr ? r8 : s8) + (uint64_t) D.gblk[k] * 16u;
-            for (uint32_t c0 = 0; c0 < n; c0 += 64) {
-                const uint32_t i = c0 + lane;
-                if (i < n) {
-                    glds16(src + (uint64_t) i * 16u, buf + (p0 + c0) * 16u);
-                    // keys o with h + kst o in [16 i, 16 i + 16): o in [ceil((16 i - h) / kst), ceil((16 i + 16 - h) / kst))
-                    const uint32_t lo = 16u * i, hi = lo + 16u;
-                    auto cdiv = [&](uint32_t x) -> uint32_t {  // ceil(x / kst), x < 2^16
-                        return rpk ? ((x + 2u) * 0xAAABu) >> 17 : (x + 3u) >> 2;
-                    };
-                    const uint32_t o0 = lo > h ? cdiv(lo - h) : 0u;
-                    const uint32_t o1 = min(c, cdiv(hi - h));
-                    const uint32_t nk = o1 > o0 ? o1 - o0 : 0u;
-                    inf[p0 + i] = (uint8_t) ((h + kst * o0 - lo) | (nk << 4));
-                }
-            }
-        }
-    };
-    // C: job in buffer bi (landed): bitmap, R bits, duplicate check, survivor tests. Every thread
-    // takes whole 16-byte blocks (R runs' blocks first, then the survivor runs'): the keys starting
-    // in a block are read from its 4 dwords and the next block's first (a key may end there).
-    auto run_job = [&](int bi) {
-        const JdDesc&  D  = L.d[bi];
-        const uint32_t nr = D.nr, ns = D.ns;  // (uniform)
-        if (nr + ns == 0) return;
-        const uint32_t nbR = D.pre[nr], nb = D.pre[nr + ns];
-        const uint4* const  bq  = L.buf[bi];
-        const uint8_t* const inf = L.info[bi];
-        constexpr uint32_t kVmask = kJoinWords * 32u - 1u;  // (keys are < 2^18: bounded anyway)
-        // the keys starting in block q through op(key)
-        auto block_keys = [&](uint32_t q, auto&& op) {
-            const uint32_t f = inf[q], nk = f >> 4, a0 = f & 15u;
-            if (!nk) return;
-            const uint4    v  = bq[q];
-            const uint32_t v4 = ((const uint32_t*) bq)[4 * q + 4];
-#pragma unroll
-            for (uint32_t j = 0; j < 6; j++) {
-                if (j < nk) {
-                    const uint32_t a = a0 + j * kst, w = a >> 2;
-                    const uint32_t x0 = w == 0 ? v.x : w == 1 ? v.y : w == 2 ? v.z : v.w;
-                    uint32_t       x;
-                    if (rpk) {
-                        const uint32_t x1 = w == 0 ? v.y : w == 1 ? v.z : w == 2 ? v.w : v4;
-                        x = __builtin_amdgcn_alignbit(x1, x0, (a & 3u) * 8u) & 0xFFFFFFu;
-                    } else {
-                        x = (x0 >> ksh) & kmk;
-                    }
-                    op(x & kVmask);
-                }
-            }
-        };
-        for (uint32_t i = tid; i < kJoinWords / 4; i += kJdThreads) ((uint4*) L.tab)[i] = make_uint4(0, 0, 0, 0);
-        jd_barrier();
-        for (uint32_t q = tid; q < nbR; q += kJdThreads)
-            block_keys(q, [&](uint32_t x) {
-                __hip_atomic_fetch_or(&L.tab[x >> 5], 1u << (x & 31u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            });
-        jd_barrier();
-        {
-            uint32_t pc = 0;
-            for (uint32_t i = tid; i < kJoinWords / 4; i += kJdThreads) {
-                const uint4 v = ((const uint4*) L.tab)[i];
-                pc += __builtin_popcount(v.x) + __builtin_popcount(v.y) + __builtin_popcount(v.z) + __builtin_popcount(v.w);
-            }
-            pc = __builtin_amdgcn_readlane(wave_incl_scan_dpp(pc), 63);
-            if (lane == 0 && pc) atomicAdd(&L.bits, pc);
-        }
-        jd_barrier();
-        if (L.bits != D.nrk) {  // duplicate R keys (uniform): k_join_rest's hash path
-            if (tid == 0 && !(HWBRJ_ABL_JD & 1)) {
-                const uint32_t k = atomicAdd(&P.fb[0], 1u);
-                P.fb[1 + k] = D.job;
-            }
-            if (!(HWBRJ_ABL_JD & 1)) return;
-        }
-        const uint64_t tm = P.timing ? wall_clock64() : 0;
-        uint32_t       c32 = 0;
-        for (uint32_t q = nbR + tid; q < nb; q += kJdThreads)
-            block_keys(q, [&](uint32_t x) { c32 += (L.tab[x >> 5] >> (x & 31u)) & 1u; });
-        cnt += c32;
-        if (P.timing) t_probe += wall_clock64() - tm;
-    };
-
-    // Pipeline. At the top of iteration t (after vmcnt(0)): job t's runs are in buffer t & 1,
-    // job t + 1's run descriptors and job t + 2's header are in registers. Then: describe job t + 1,
-    // load job t + 2's run descriptors and job t + 3's header, start job t + 1's DMA (into the
-    // buffer job t - 1 used), and run job t: job t + 1's runs land while job t is tested.
-    JdHdr h1 = load_hdr(0);
-    {
-        const JdRun r0 = load_run(h1);
-        const JdHdr h2 = load_hdr(1);
-        describe_job(h1, r0, 0);
-        dma_job(0);
-        h1 = h2;
-    }
-    JdRun r1 = load_run(h1);   // job t + 1's runs
-    JdHdr h2 = load_hdr(2);    // job t + 2's header
-    for (uint32_t t = 0; job_at(t) >= 0; t++) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // job t's DMA, the descriptors above
-        jd_barrier();
-        const int bi = (int) (t & 1u), bn = bi ^ 1;
-        describe_job(h1, r1, bn);
-        r1 = load_run(h2);
-        h1 = h2;
-        h2 = load_hdr(t + 3);
-        if (!(HWBRJ_ABL_JD & 1)) dma_job(bn);
-        if (!(HWBRJ_ABL_JD & 2)) run_job(bi);
-        jd_barrier();  // (buffer bi and d[bi] are free for job t + 2)
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    // the workgroup's matches (and, P.timing, its probe / total ticks) into one partial sum
-    cnt = wave_sum_u64(cnt);
-    __syncthreads();
-    __shared__ uint64_t wsum64[kJdWaves];
-    if (lane == 0) wsum64[wave] = cnt;
-    __syncthreads();
-    if (tid != 0) return;
-    uint64_t tt = 0;
-    for (int w = 0; w < kJdWaves; w++) tt += wsum64[w];
-    uint64_t* slot = &P.jsum[(blockIdx.x % kJoinSumSlots) * kJoinSumStride];
-    if (tt) atomicAdd((unsigned long long*) slot, (unsigned long long) tt);
-    if (P.timing) {
-        if (t_probe) atomicAdd((unsigned long long*) (slot + 1), (unsigned long long) t_probe);
-        atomicAdd((unsigned long long*) (slot + 2), (unsigned long long) (wall_clock64() - t_start));
-    }
 }
 
 // ============================================================ K10m: the materializing join
@@ -4426,44 +4064,9 @@ void launch_copy_bw(const void* src, void* dst, uint64_t bytes, int grid, hipStr
 }
 
 template <int SRC, int MODE, int FMT>
-__global__ __launch_bounds__(kScThreads) void k_scatter_r(ScatterParams P) {
-    scatter_body<SRC, MODE, FMT, HWBRJ_SC_SAUX_R>(P, blockIdx.x, gridDim.x);
-}
+__global__ __launch_bounds__(kScThreads) void k_scatter_r(ScatterParams P) { scatter_body<SRC, MODE, FMT, HWBRJ_SC_SAUX_R>(P); }
 template <int SRC, int MODE, int FMT>
-__global__ __launch_bounds__(kScThreads) void k_scatter_s(ScatterParams P) {
-    scatter_body<SRC, MODE, FMT>(P, blockIdx.x, gridDim.x);
-}
-// Pass-1 of both relations in one launch (the reference partitions R, then S, between barriers:
-// src/parallel_radix_join_bloom.c:1139-1171): workgroups [0, GS) partition S, [GS, grid) R. The
-// dispatcher hands out workgroups in order, so S's take every CU first and R's start on the CUs S's
-// leave, filling the S scatter's tail (its workgroups end over a ~0.1 ms spread) instead of
-// waiting for a kernel boundary.
-template <int SRC, int MODE, int FMT>
-__global__ __launch_bounds__(kScThreads) void k_scatter_sr(ScatterParams S, ScatterParams R, uint32_t GS) {
-    if (blockIdx.x < GS) scatter_body<SRC, MODE, FMT>(S, blockIdx.x, GS);
-    else scatter_body<SRC, MODE, FMT, HWBRJ_SC_SAUX_R>(R, blockIdx.x - GS, gridDim.x - GS);
-}
-
-template <int SRC, int MODE, int FMT>
-static void scatter_sr_inst(const ScatterParams& s, const ScatterParams& r, uint32_t GS, uint32_t GR, hipStream_t st) {
-    const size_t lds = scatter_lds_bytes(s.g.log2F);
-    (void) hipFuncSetAttribute((const void*) &k_scatter_sr<SRC, MODE, FMT>, hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds);
-    k_scatter_sr<SRC, MODE, FMT><<<GS + GR, kScThreads, lds, st>>>(s, r, GS);
-}
-
-bool launch_scatter_sr(const ScatterParams& s, const ScatterParams& r, uint32_t GS, uint32_t GR, hipStream_t st) {
-    const Geometry& g = s.g;
-    if (s.ppool || r.ppool || g.log2F != r.g.log2F || g.mode != r.g.mode || g.s_format != g.format) return false;
-    switch (g.mode) {
-        case MODE_SLICE_BLOCK:
-            if (g.format == FMT_PACKED) scatter_sr_inst<SRC_TUPLES, MODE_SLICE_BLOCK, FMT_PACKED>(s, r, GS, GR, st);
-            else scatter_sr_inst<SRC_TUPLES, MODE_SLICE_BLOCK, FMT_CODE>(s, r, GS, GR, st);
-            return true;
-        case MODE_SLICE_BASIC: scatter_sr_inst<SRC_TUPLES, MODE_SLICE_BASIC, FMT_CODE>(s, r, GS, GR, st); return true;
-        case MODE_NOBLOOM: scatter_sr_inst<SRC_TUPLES, MODE_NOBLOOM, FMT_CODE>(s, r, GS, GR, st); return true;
-        default: return false;
-    }
-}
+__global__ __launch_bounds__(kScThreads) void k_scatter_s(ScatterParams P) { scatter_body<SRC, MODE, FMT>(P); }
 
 template <int SRC, int MODE, int FMT>
 static void scatter_inst(const ScatterParams& p, int side, uint32_t grid, hipStream_t st) {
@@ -4529,29 +4132,15 @@ void launch_list_fill(const uint32_t* meta, const uint32_t* wg_used, uint64_t ca
                       uint32_t* item_start, uint32_t* list, uint32_t grid, hipStream_t st) {
     const size_t lds = (kLfBatch + 4 * (1u << log2F) + 16) * sizeof(uint32_t);
     (void) hipFuncSetAttribute((const void*) &k_list_fill, hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds);
-    const ListFillArgs A{meta, wg_used, cap, log2F, wgq_off, colc, cole, CH, nseg, list_start, elem_start, item_start, list};
-    k_list_fill<<<grid, kLfThreads, lds, st>>>(A);
-}
-
-void launch_list_fill2(const ListFillArgs& a, uint32_t ga, const ListFillArgs& b, uint32_t gb, hipStream_t st) {
-    const size_t lds = (kLfBatch + 4 * (1u << std::max(a.log2F, b.log2F)) + 16) * sizeof(uint32_t);
-    (void) hipFuncSetAttribute((const void*) &k_list_fill2, hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds);
-    k_list_fill2<<<ga + gb, kLfThreads, lds, st>>>(a, b, ga);
+    k_list_fill<<<grid, kLfThreads, lds, st>>>(meta, wg_used, cap, log2F, wgq_off, colc, cole, CH,
+                                               nseg, list_start, elem_start, item_start, list);
 }
 
 bool launch_plan(const uint32_t* wgq_chunks, const uint32_t* wgq_elems, uint32_t G, uint32_t log2F,
                  uint32_t* wgq_off, uint32_t* colc, uint64_t* cole, hipStream_t st) {
     if (G > kPlanRGs * kPlanMaxRG) return false;
     const uint32_t F = 1u << log2F;
-    const PlanArgs A{wgq_chunks, wgq_elems, G, log2F, wgq_off, colc, cole};
-    k_plan<<<(F + kPlanCols - 1) / kPlanCols, 1024, 0, st>>>(A);
-    return true;
-}
-
-bool launch_plan2(const PlanArgs& a, const PlanArgs& b, hipStream_t st) {
-    if (a.G > kPlanRGs * kPlanMaxRG || b.G > kPlanRGs * kPlanMaxRG) return false;
-    const uint32_t na = ((1u << a.log2F) + kPlanCols - 1) / kPlanCols, nb = ((1u << b.log2F) + kPlanCols - 1) / kPlanCols;
-    k_plan2<<<na + nb, 1024, 0, st>>>(a, b, na);
+    k_plan<<<(F + kPlanCols - 1) / kPlanCols, 1024, 0, st>>>(wgq_chunks, wgq_elems, G, log2F, wgq_off, colc, cole);
     return true;
 }
 
@@ -4654,30 +4243,14 @@ void launch_probe(const ProbeParams& p0, uint32_t grid, hipStream_t st) {
 
 uint32_t probe_chunks_per_item() { return kProbeCH; }
 
-// The join of one launch: k_join_split, then either k_join_dma (bitmap launches with a fallback
-// list, P.fb: one persistent workgroup per CU) or k_join (one workgroup per job), then k_join_rest
-// (the mixed-format launches; after k_join_dma the jobs it left and the further parts of skewed jobs).
 void launch_join(const JoinParams& p0, uint32_t jobs, uint32_t* job_surv, hipStream_t st) {
     JoinParams p = p0;
     p.jobs       = jobs;
-    const bool dma = HWBRJ_JDMA && p.fb && p.bitmap && p.jkind == 0;
-    if (!dma) p.fb = nullptr;
     const uint32_t split = p.split_surv ? p.split_surv : kJoinTaskSurv;
     k_join_split<<<(jobs + 255) / 256, 256, 0, st>>>(p.item_start, job_surv, p.log2NSUB, jobs, split,
-                                                     p.nparts, p.extra, p.nextra, p.jsum, p.fb);
-    if (dma) {
-        static const int cus = [] {
-            int dev = 0, n = 256;
-            if (hipGetDevice(&dev) == hipSuccess) (void) hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
-            return n;
-        }();
-        const size_t lds = join_dma_lds_bytes();
-        (void) hipFuncSetAttribute((const void*) &k_join_dma, hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds);
-        k_join_dma<<<(uint32_t) cus, kJdThreads, lds, st>>>(p);
-    } else {
-        k_join<<<jobs + kJoinExtra, kJoinThreads, 0, st>>>(p);
-    }
-    k_join_rest<<<std::min<uint32_t>(jobs + kJoinExtra, 1024u), kJoinThreads, 0, st>>>(p);
+                                                     p.nparts, p.extra, p.nextra, p.jsum);
+    k_join<<<jobs + kJoinExtra, kJoinThreads, 0, st>>>(p);
+    k_join_mixed<<<std::min<uint32_t>(jobs + kJoinExtra, 1024u), kJoinThreads, 0, st>>>(p);
 }
 
 uint32_t join_extra_tasks() { return kJoinExtra; }
@@ -4735,8 +4308,6 @@ const char* kernel_build_knobs() {
         num("HWBRJ_JFW", HWBRJ_JFW, 5);
         num("HWBRJ_JBM", HWBRJ_JBM, 18);
         num("HWBRJ_OVL_ASYNC", HWBRJ_OVL_ASYNC, 1);
-        num("HWBRJ_FUSE_SR", HWBRJ_FUSE_SR, 0);
-        num("HWBRJ_JDMA", HWBRJ_JDMA, 0);
         num("HWBRJ_PJ_OVL", HWBRJ_PJ_OVL, 1);
         num("HWBRJ_ABL_PROBE", HWBRJ_ABL_PROBE, 0);
         num("HWBRJ_PCO", HWBRJ_PCO, 1);
