@@ -85,13 +85,14 @@ def parse():
     return ap.parse_args()
 
 
-JOIN_KEY_NAMES = {0: "32-bit codes", 1: "3-byte keys (pack3)", 2: "mixed (3-byte, unstaged items 32-bit)"}
+JOIN_KEY_NAMES = {0: "32-bit codes", 1: "packed keys", 2: "mixed (packed, unstaged items 32-bit)"}
 
 
 def join_key_bytes(st) -> float:
     """Bytes per join key between build/probe and k_join, as the join ran them (hwbrj_stats_t
-    join_keys): 3 for 3-byte keys (the mixed format's unstaged runs are a small share), else 4."""
-    return 3.0 if st.join_keys in (1, 2) else 4.0
+    join_keys, join_key_bits): join_key_bits / 8 for packed keys (the mixed format's unstaged runs
+    are a small share; 18 bits at the north star), else 4."""
+    return st.join_key_bits / 8.0 if st.join_keys in (1, 2) else 4.0
 
 
 def modeled_bytes(nR: int, nS: int, filtered: int, m: int, word_bytes: float, key_bytes: float = 4.0) -> dict:
@@ -326,7 +327,8 @@ def headline_line(a, hw, torch, dist, rank, world, dR, dS, args, st, last, sums,
                 "launch_ms": round(dev_ms, 4),
                 "modeled_bytes": modeled_bytes(nR, nS, st.filtered, a.bloom_size if args else 0,
                                                word_bytes, join_key_bytes(last)),
-                "join_keys": {"format": JOIN_KEY_NAMES.get(last.join_keys), "unstaged_items": last.unstaged_items,
+                "join_keys": {"format": JOIN_KEY_NAMES.get(last.join_keys), "bits": last.join_key_bits,
+                              "unstaged_items": last.unstaged_items,
                               "what": "the key format the timed joins handed to k_join (the last one's "
                                       "hwbrj_stats_t.join_keys)"},
                 "pmc_source": os.path.relpath(a.pmc_json, ROOT) if pm else None,

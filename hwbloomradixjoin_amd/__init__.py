@@ -59,7 +59,8 @@ class _Stats(ctypes.Structure):  # include/hwbrj.h hwbrj_stats_t
                     (n, ctypes.c_double) for n in (
                         "ms_total", "ms_r_scatter", "ms_r_index", "ms_build", "ms_s_scatter",
                         "ms_s_index", "ms_probe", "ms_surv", "ms_join", "ms_join_probe")] + [
-                    ("join_keys", ctypes.c_int), ("unstaged_items", ctypes.c_uint32)]
+                    ("join_keys", ctypes.c_int), ("unstaged_items", ctypes.c_uint32),
+                    ("join_key_bits", ctypes.c_uint32)]
 
 # hwbrj_stats_t.join_keys (include/hwbrj.h): the key format between the build / probe and the join
 JOIN_KEYS_32, JOIN_KEYS_PACKED, JOIN_KEYS_MIXED = 0, 1, 2
@@ -327,6 +328,7 @@ class Stats:
     ms_join_probe: float
     join_keys: int = 0       # JOIN_KEYS_32 / _PACKED / _MIXED
     unstaged_items: int = 0  # probe items whose survivors overflowed the LDS stage
+    join_key_bits: int = 32  # bits per packed join key (18 at the north star, 24, or 32: codes)
 
 
 class Relation:

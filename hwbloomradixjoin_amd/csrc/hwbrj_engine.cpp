@@ -614,8 +614,9 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     // 3-byte join keys from build / probe to k_join, unless the last join this Engine waited for had
     // probe items too large for the stage (their 32-bit survivor runs make the join read two formats,
     // k_join_mixed): a performance hint only, both paths give the same counts
-    const bool pack3 = !mat && join_pack3(g) && pack3_hint_;
-    bp.pack3       = pack3 ? 1u : 0u;
+    const bool     pack3 = !mat && join_pack3(g) && pack3_hint_;
+    const uint32_t kbits = pack3 ? join_key_bits(g) : 0u;  // 18 at the north star
+    bp.kbits       = kbits;
     // the broadcast: rank 0 builds the slices, the other ranks only sub-partition R for the join
     // and receive them over RCCL (HWBRJ_HOOK_BCAST_NONROOT: this rank takes the non-root side, for
     // tests at world 1; value 2 zeroes the slices first, so the counts show whether k_build wrote any)
@@ -681,7 +682,7 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     pp.filtered        = d_filtered;
     pp.job_surv        = jparts.as<uint32_t>() + NJ;
     pp.surv_pos        = mat ? survpos.as<uint32_t>() : nullptr;
-    pp.pack3           = pack3 ? 1u : 0u;
+    pp.kbits           = kbits;
     pp.fmt_cnt         = mat ? nullptr : (uint32_t*) sm + 10;  // (u64 word 5 of the slot: zeroed by the R scatter)
     const size_t   pl_lds = probe_lds_bytes(g, nullptr, mat != nullptr);
     const uint32_t PG = (uint32_t) cus_ * (uint32_t) std::max<size_t>(1, std::min<size_t>(2, 163840 / pl_lds));
@@ -720,7 +721,7 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     jp.nextra          = jparts.as<uint32_t>() + 2 * NJ;
     jp.jkind           = (uint32_t) jkind;
     jp.split_surv      = test_hooks().join_split;  // (tests: force the skew split)
-    jp.r_pack3         = pack3 ? 1u : 0u;
+    jp.r_kbits         = kbits;
     jp.fmt_cnt         = pp.fmt_cnt;
     jp.timing          = phase_ev_ ? 1u : 0u;  // (back-to-back joins: counts only)
     if (mat) {
@@ -762,7 +763,6 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     pending_ev_   = phase_ev_;
     pending_sfirst_ = s_first;
     pending_fmt_    = pp.fmt_cnt != nullptr;
-    pending_pack3_  = pack3;
     pending_slots_  = !mat;
     pending_stream_ = stream;
     have_filter_  = args != nullptr;
@@ -772,7 +772,7 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
         r.slot  = rslot;
         r.args  = args != nullptr;
         r.fmt   = pending_fmt_;
-        r.pack3 = pack3;
+        r.kbits = kbits;
         r.slots = !mat;
         r.timed = rtimed;
         r.nS    = nS;
@@ -1057,7 +1057,6 @@ int Engine::enqueue_basic_kk(const uint2* dR, uint64_t nR, const uint2* dS, uint
     pending_ev_   = phase_ev_;
     pending_sfirst_ = false;
     pending_fmt_    = false;
-    pending_pack3_  = false;
     pending_slots_  = true;
     pending_stream_ = stream;
     have_filter_  = true;
@@ -1133,8 +1132,9 @@ int Engine::ring_collect() {
         st.subparts       = 1u << g.log2NSUB;
         st.slice_segments = (g.mode == MODE_SLICE_BLOCK || g.mode == MODE_SLICE_BASIC) ? g.nseg : 1;
         st.unstaged_items = r.fmt ? (uint32_t) h[5] : 0u;
-        st.join_keys      = !r.pack3 ? HWBRJ_JOIN_KEYS_32
+        st.join_keys      = !r.kbits ? HWBRJ_JOIN_KEYS_32
                             : st.unstaged_items ? HWBRJ_JOIN_KEYS_MIXED : HWBRJ_JOIN_KEYS_PACKED;
+        st.join_key_bits  = r.kbits ? r.kbits : 32u;
         // (probe / join ticks: the synchronous joins' phase split, added by wait())
         st.ms_join_probe  = (double) h[3];
         st.ms_join        = (double) h[4];

@@ -200,9 +200,8 @@ class Engine {
     hipStream_t  pending_stream_ = nullptr;
     bool         pending_sfirst_ = false;  // the pending join ran its S pass first (phase boundaries)
     bool         pending_fmt_    = false;  // the pending join counted its unstaged probe items
-    bool         pending_pack3_  = false;  // the pending join packed its join keys
     bool         pending_slots_  = false;  // the pending join's matches are in k_join's partial sums
-    bool         pack3_hint_     = true;   // the last waited join had none: 3-byte join keys pay
+    bool         pack3_hint_     = true;   // the last waited join had none: packed join keys pay
     int          pending_rc_     = 0;   // nonzero: the pending join failed after enqueuing kernels
     std::string  pending_err_;
     bool         surv_fused_   = false;
@@ -211,7 +210,8 @@ class Engine {
     // last (the reference sums every thread's count per run, parallel_radix_join_bloom.c:1696-1707)
     struct JoinRec {
         uint32_t slot = 0;
-        bool     args = false, fmt = false, pack3 = false, slots = false, timed = false;
+        bool     args = false, fmt = false, slots = false, timed = false;
+        uint32_t kbits = 0;  // packed join-key bits (0: 32-bit codes)
         uint64_t nS   = 0;
         Geometry g{};
     };

@@ -37,13 +37,21 @@ struct ScatterParams {
     const CrcTables* tabs;
 };
 
-// 3-byte join keys between the build / probe and the join (BuildParams::pack3): on when the
-// join key v = code >> hash_shift fits 24 bits and the run formats are private to k_join (not the
+// Packed join keys between the build / probe and the join (BuildParams::kbits): on when the join
+// key v = code >> hash_shift fits 24 bits and the run formats are private to k_join (not the
 // materializing join, which reads codes, nor the partitioned join, which ships survivor words).
+// Keys are a bit stream of kbits-bit fields: 18 bits when hash_shift = 14 (the bitmap path's keys,
+// every north-star job: 16 keys per 9 dwords), else 24 (4 keys per 12 bytes); 0 = 32-bit codes.
 #ifndef HWBRJ_PACK3
 #define HWBRJ_PACK3 1
 #endif
+#ifndef HWBRJ_PACK18
+#define HWBRJ_PACK18 1  // 0: 24-bit keys for the hash_shift = 14 launches too (A/B)
+#endif
 inline bool join_pack3(const Geometry& g) { return HWBRJ_PACK3 != 0 && g.sub_shift > 0 && g.hash_shift >= 8; }
+inline uint32_t join_key_bits(const Geometry& g) {
+    return !join_pack3(g) ? 0u : (HWBRJ_PACK18 && g.hash_shift == 14) ? 18u : 24u;
+}
 
 // Joins enqueued without phase events (hwbrj_join_device_async: the timed back-to-back joins) run
 // their S pass on a second stream beside the R side, joined before the probe (A/B: 0 = one stream,
@@ -71,8 +79,9 @@ struct BuildParams {
     const uint32_t*  ppool;       // payloads of pool's words (materialization), or nullptr
     uint32_t*        out_pay;     // [sweeps][kBSlot]: the payloads of out_codes (ppool set)
     uint32_t         no_slices;   // 1: join runs only (the slices arrive by broadcast from rank 0)
-    uint32_t         pack3;       // 1: out_codes hold 3-byte join keys (code >> hash_shift), 4 per
-                                  // 12 bytes from the slot's byte 0 (hash_shift >= 8; not PAY)
+    uint32_t         kbits;       // 18 / 24: out_codes hold the slot's keys (code >> hash_shift) as a
+                                  // stream of kbits-bit fields from its byte 0 (join_key_bits; not
+                                  // PAY); 0: 32-bit codes
 };
 
 struct ProbeParams {
@@ -95,10 +104,11 @@ struct ProbeParams {
     uint32_t*        wg_cnt;      // k_probe_bitj: words appended to workgroup w's region
                                   // (surv + w * surv_seg_stride)
     uint64_t*        dbg;         // dev-only: per-workgroup phase cycles (HWBRJ_DBG), or nullptr
-    uint32_t         pack3;       // 1: staged items store 3-byte join keys (code >> hash_shift), 3
-                                  // bytes per key from the item region's byte 0, flagged by bit 31 of
-                                  // their surv_off entries (unstaged items keep 32-bit codes)
-    uint32_t*        fmt_cnt;     // pack3: += the unstaged items (zeroed by the R scatter), or nullptr
+    uint32_t         kbits;       // 18 / 24: staged items store their join keys (code >> hash_shift)
+                                  // as a stream of kbits-bit fields from the item region's byte 0,
+                                  // flagged by bit 31 of their surv_off entries (unstaged items keep
+                                  // 32-bit codes); 0: 32-bit codes
+    uint32_t*        fmt_cnt;     // kbits: += the unstaged items (zeroed by the R scatter), or nullptr
 };
 
 struct JoinParams {
@@ -127,8 +137,8 @@ struct JoinParams {
                                   // table, PRO), 1 histogram join (PRH), 2 + 16-byte compares (PRHO)
     const uint64_t* item_base;    // [items] survivor region of each item (partitioned multi-GPU
                                   // join: received runs), or nullptr (k_probe's item regions)
-    uint32_t        r_pack3;      // 1: r_codes hold 3-byte join keys (BuildParams::pack3); survivor
-                                  // runs say so per item (bit 31 of surv_off)
+    uint32_t        r_kbits;      // 18 / 24: r_codes hold packed join keys (BuildParams::kbits), and so
+                                  // do the survivor runs flagged by bit 31 of surv_off; 0: codes
     const uint32_t* fmt_cnt;      // ProbeParams::fmt_cnt (the launch's survivor-run formats), or nullptr
     uint32_t        timing;       // 1: accumulate the probe / total ticks (result[3], result[4]) for
                                   // ms_join_probe (synchronous joins; 0: one count add per workgroup)

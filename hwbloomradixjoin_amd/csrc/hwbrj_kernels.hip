@@ -82,7 +82,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, uin
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int) bytes, 0x00020000);
 }
 
-// 3-byte join keys (pack3): the join needs only v = code >> hash_shift, < 2^24 when hash_shift >= 8
+// 24-bit join keys (pack3): the join needs only v = code >> hash_shift, < 2^24 when hash_shift >= 8
 // (18 bits at the north star), so the build's R runs and the probe's staged survivor runs store
 // 4 keys per 12 bytes -- 25 % fewer bytes written there and read back by the join. Key i of a run
 // at byte b is the low 24 bits of the (unaligned) dword at b + 3 i; the last key's dword ends
@@ -91,6 +91,41 @@ typedef unsigned int v3u __attribute__((ext_vector_type(3)));
 __device__ __forceinline__ v3u pack3x4(v4u v, uint32_t sh) {
     const uint32_t a = v.x >> sh, b = v.y >> sh, c = v.z >> sh, d = v.w >> sh;
     return v3u{a | (b << 24), (b >> 8) | (c << 16), (c >> 16) | (d << 8)};
+}
+// 18-bit join keys (hash_shift = 14, every bitmap-path launch; join_key_bits): key i of a run at
+// bit b is bits [b + 18 i, b + 18 i + 18) of the stream, read as the dword at byte (b + 18 i) >> 3
+// shifted right by (b + 18 i) & 7 (18 + 7 < 32 bits). 25 % fewer bytes than 24-bit keys (north
+// star: 0.19 GB of R keys and as much of survivors, each written by k_build / k_probe and read back
+// by k_join). A writer builds dword d of the stream from the three codes that overlap it, read from
+// the LDS stage they are sorted in (c[ka + 1], c[ka + 2] may lie past the last key: they only fill
+// bits past the stream's end), so no thread holds more than its four output dwords.
+__device__ __forceinline__ uint32_t pack18_dword(const uint32_t* c, uint32_t d, uint32_t sh) {
+    const uint32_t p = 32u * d, ka = p / 18u, s = p - 18u * ka;
+    const uint32_t k0 = (c[ka] >> sh) & 0x3FFFFu, k1 = (c[ka + 1] >> sh) & 0x3FFFFu, k2 = (c[ka + 2] >> sh) & 0x3FFFFu;
+    return (k0 >> s) | (k1 << (18u - s)) | (s > 4u ? k2 << (36u - s) : 0u);
+}
+__device__ __forceinline__ v4u pack18_quad(const uint32_t* c, uint32_t i, uint32_t sh) {  // dwords 4i .. 4i + 3
+    return v4u{pack18_dword(c, 4 * i, sh), pack18_dword(c, 4 * i + 1, sh), pack18_dword(c, 4 * i + 2, sh),
+               pack18_dword(c, 4 * i + 3, sh)};
+}
+// The same stream from 16 codes held in registers (4 quads) into 9 dwords: the build's form (its
+// copy-out has registers to spare and measured faster this way than with the LDS reads above; the
+// probe's has not: 16 live codes spill it)
+__device__ __forceinline__ void pack18x16(const v4u* q, uint32_t sh, uint32_t out[9]) {
+    uint64_t acc = 0;
+    int      nb = 0, d = 0;
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const v4u      v = q[k >> 2];
+        const uint32_t c = (k & 3) == 0 ? v.x : (k & 3) == 1 ? v.y : (k & 3) == 2 ? v.z : v.w;
+        acc |= (uint64_t) ((c >> sh) & 0x3FFFFu) << nb;
+        nb += 18;
+        if (nb >= 32) {
+            out[d++] = (uint32_t) acc;
+            acc >>= 32;
+            nb -= 32;
+        }
+    }
 }
 typedef uint32_t u32_unaligned __attribute__((aligned(1)));
 
@@ -1673,7 +1708,17 @@ __global__ __launch_bounds__(1024) void k_build(BuildParams P) {
                 nsw++;
                 __syncthreads();  // B3: the sweep is sorted
                 uint32_t* __restrict__ dst = P.out_codes + (uint64_t) sw * kBSlot;
-                if (!PAY && P.pack3) {  // 3-byte keys: one 12-byte store per 4 codes (uniform)
+                if (!PAY && P.kbits == 18) {  // 18-bit keys: 36 bytes per 16 codes (uniform)
+                    const uint32_t i = tid;   // (kBSlot / 16 groups: threads below 256)
+                    if (i < kBSlot / 16) {
+                        uint32_t o[9];
+                        pack18x16((const v4u*) stage + 4 * i, g.hash_shift, o);
+                        const auto rd = buf_rsrc(dst, (tot + 15u) / 16u * 36u);  // (inside the slot)
+                        __builtin_amdgcn_raw_buffer_store_b128(v4u{o[0], o[1], o[2], o[3]}, rd, i * 36u, 0, 0);
+                        __builtin_amdgcn_raw_buffer_store_b128(v4u{o[4], o[5], o[6], o[7]}, rd, i * 36u + 16u, 0, 0);
+                        __builtin_amdgcn_raw_buffer_store_b32(o[8], rd, i * 36u + 32u, 0, 0);
+                    }
+                } else if (!PAY && P.kbits) {  // 24-bit keys: one 12-byte store per 4 codes (uniform)
                     const uint32_t i = tid;  // kBSlot / 4 == blockDim.x quads
                     const v4u      v = ((const v4u*) stage)[i];
                     __builtin_amdgcn_raw_buffer_store_b96(pack3x4(v, g.hash_shift), buf_rsrc(dst, (tot + 3u) / 4u * 12u),
@@ -1819,7 +1864,8 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
     constexpr uint32_t kNoItem = 0x80000000u;
     uint32_t  prev_total = 0, prev_it = kNoItem, prev_buf = 0, subc_v = 0, subo_v = 0, prev_q = 0;
     uint32_t* prev_out   = P.surv;
-    const bool pk3       = !PAY && P.pack3 != 0;  // 3-byte join keys for staged items
+    const bool pk3       = !PAY && P.kbits != 0;  // packed join keys for staged items
+    const bool pk18      = pk3 && P.kbits == 18;
     bool       prev_pk   = false;  // the previous item's run is staged and stored as 3-byte keys
     uint32_t   n_unst    = 0;      // items of this workgroup too large for the stage (32-bit runs)
     auto copy_out = [&]() {
@@ -1836,7 +1882,14 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
                 __builtin_amdgcn_raw_buffer_store_b128(src[j], ro, i * 16, 0, 0);
                 __builtin_amdgcn_raw_buffer_store_b128(src[hp / 4 + j], rp, i * 16, 0, 0);
             }
-        } else if (prev_pk) {  // 3-byte keys: 12 bytes per staged quad (whole quads: the item
+        } else if (prev_pk && pk18) {  // 18-bit keys: one 16-byte store per 4 stream dwords (whole
+                                       // quads: the region holds round_up(total, 4) words, more)
+            const uint32_t nq = ((prev_total * 18u + 31u) / 32u + 3u) / 4u;
+            const auto     rp = buf_rsrc(prev_out, nq * 16u);
+            const uint32_t* c = (const uint32_t*) src;
+            for (uint32_t i = tid; i < nq; i += NT)
+                __builtin_amdgcn_raw_buffer_store_b128(pack18_quad(c, i, g.hash_shift), rp, i * 16u, 0, HWBRJ_PCO_AUX);
+        } else if (prev_pk) {  // 24-bit keys: 12 bytes per staged quad (whole quads: the item
                                // region holds round_up(total, 4) words, more than these bytes)
             const auto rp3 = buf_rsrc(prev_out, (prev_total + 3u) / 4u * 12u);
 #pragma unroll
@@ -2433,7 +2486,9 @@ struct JoinShared {
     uint32_t dupflag, npieces;
 };
 
-template <bool MIXED>
+// KW: the launch's packed key width, 18 / 24 (every run packed), 32 (every run 32-bit codes), or 0
+// (P.r_kbits at run time: the mixed launches, k_join_mixed)
+template <bool MIXED, int KW = 0>
 __device__ __forceinline__ void join_job(const JoinParams& P, const uint32_t blk, JoinShared& L, uint64_t& cnt_acc,
                                          uint64_t& tp_acc) {
     uint32_t* const tab   = L.tab;
@@ -2464,7 +2519,7 @@ __device__ __forceinline__ void join_job(const JoinParams& P, const uint32_t blk
     const uint32_t w0 = P.r_sweep_start[q], w1 = P.r_sweep_start[q + 1];
     const uint32_t qi0 = P.item_start[q], qi1 = P.item_start[q + 1];  // q's items (segment-major)
     const uint32_t np  = P.nparts[job];
-    const bool     rpk = P.r_pack3 != 0;
+    const bool     rpk = KW ? KW != 32 : P.r_kbits != 0;
     const uint32_t i0  = qi0 + (uint32_t) ((uint64_t) (qi1 - qi0) * part / np);
     const uint32_t i1  = qi0 + (uint32_t) ((uint64_t) (qi1 - qi0) * (part + 1) / np);
     if (w1 == w0 || i1 == i0) return;
@@ -2498,17 +2553,24 @@ __device__ __forceinline__ void join_job(const JoinParams& P, const uint32_t blk
         (void) k;
 #endif
     };
-    // Run formats. A run is addressed by a tagged byte offset tb from its array's base: bit 63 set =
-    // 3-byte keys (pack3), key o the low 24 bits of the unaligned dword at tb + 3 o; else 32-bit
-    // codes at tb + 4 o, key = code >> sh. R runs share one format (the build's); survivor runs are
+    // Run formats. A run is addressed by a tag tb from its array's base: bit 63 set = packed keys
+    // (P.r_kbits = kw bits each: 18 or 24), tb their bit address, key o the kw bits at tb + kw o
+    // (the unaligned dword at byte (tb + kw o) >> 3, shifted by (tb + kw o) & 7); else 32-bit codes at
+    // byte tb + 4 o, key = code >> sh. R runs share one format (the build's); survivor runs are
     // packed when their probe item was staged (bit 31 of surv_off). P.fmt_cnt counts the unstaged
-    // items: with none (or no pack3 at all) every run of the launch has one format, whose stride,
+    // items: with none (or no packing at all) every run of the launch has one format, whose width,
     // shift and mask are uniform (k_join); otherwise the survivor runs are mixed and read with a
     // per-run format (k_join_mixed: only where probe items overflow their stage), R runs packed.
     // Loads stay raw until used (key()): ALU work on a conditionally loaded value would make the
     // wave wait for it at once.
+    // Packed runs are tagged by their bit address in the stream (bit 63 set): key o at bit
+    // tb + kw o, read as the dword at byte (tb + kw o) >> 3 shifted by (tb + kw o) & 7; code runs by
+    // their byte address, key o the code at tb + 4 o shifted by hash_shift.
     constexpr uint64_t kPk = 1ull << 63;
-    const uint32_t kst = rpk ? 3u : 4u, ksh = rpk ? 0u : sh, kmk = rpk ? 0xFFFFFFu : 0xFFFFFFFFu;
+    const uint32_t kw = KW ? (uint32_t) KW : rpk ? P.r_kbits : 32u, kw7 = kw & 7u;
+    const uint32_t ksh = rpk ? 0u : sh, kmk = rpk ? (1u << kw) - 1u : 0xFFFFFFFFu;
+    // (24-bit keys start on byte boundaries: a run's tb & 7 is 0, key o at byte 3 o)
+    constexpr bool kB8 = KW == 24 || KW == 32;
     const uint8_t* const r8 = (const uint8_t*) P.r_codes;
     const uint8_t* const s8 = (const uint8_t*) P.surv;
     using SideR = std::integral_constant<int, 0>;
@@ -2516,24 +2578,32 @@ __device__ __forceinline__ void join_job(const JoinParams& P, const uint32_t blk
     // R run of (sweep, sub) at key offset off of the sweep's slot; survivor run at key offset off of
     // the item region at element e0 (regions and slots keep their 4-byte-per-key sizes)
     auto rtag = [&](uint32_t sweep, uint32_t off) -> uint64_t {
-        return rpk ? kPk | ((uint64_t) sweep * P.slot * 4u + (uint64_t) off * 3u) : ((uint64_t) sweep * P.slot + off) * 4u;
+        return rpk ? kPk | ((uint64_t) sweep * P.slot * 32u + (uint64_t) off * kw) : ((uint64_t) sweep * P.slot + off) * 4u;
     };
     auto stag = [&](uint64_t e0, uint32_t offw) -> uint64_t {
         const uint64_t off = offw & 0x7FFFFFFFu;
-        return (offw >> 31) ? kPk | (e0 * 4u + off * 3u) : (e0 + off) * 4u;
+        return (offw >> 31) ? kPk | (e0 * 32u + off * kw) : (e0 + off) * 4u;
     };
     auto ldv = [&](auto side_c, uint64_t tb, uint32_t o) -> uint32_t {
         constexpr int SIDE = decltype(side_c)::value;
-        uint32_t      st   = kst;
-        if constexpr (MIXED) st = (tb & kPk) ? 3u : 4u;
-        return *(const u32_unaligned*) ((SIDE == 0 ? r8 : s8) + (tb & ~kPk) + o * st);
+        bool          pk   = rpk;
+        if constexpr (MIXED) pk = (tb & kPk) != 0;
+        // (the run's byte base once per run, the key's byte inside it in 32 bits)
+        const uint8_t* rb = (SIDE == 0 ? r8 : s8) + (pk ? (tb & ~kPk) >> 3 : tb);
+        const uint32_t ob = pk ? (kB8 ? (kw >> 3) * o : (((uint32_t) tb & 7u) + kw * o) >> 3) : 4u * o;
+        return *(const u32_unaligned*) (rb + ob);
     };
-    auto key = [&](auto side_c, uint32_t x, bool pk) -> uint32_t {  // (side_c: as ldv's, unused)
+    // the key of raw word x = key o of a run whose tag has low bits b7 (tb & 7 of a packed run, 0
+    // else). Only o mod 8 matters (kw o mod 8), and every caller's o is its lane plus a multiple of
+    // 64: callers pass the lane, so the shift is one value per run and lane, not one per key.
+    auto key = [&](auto side_c, uint32_t x, bool pk, uint32_t b7, uint32_t o) -> uint32_t {  // (side_c: as ldv's, unused)
         (void) side_c;
-        if constexpr (MIXED) return pk ? x & 0xFFFFFFu : x >> sh;
+        if constexpr (MIXED) return pk ? (x >> ((b7 + kw7 * o) & 7u)) & kmk : x >> sh;
         (void) pk;
-        return (x >> ksh) & kmk;
+        if constexpr (kB8) return (x >> ksh) & kmk;
+        return (x >> (((b7 + kw7 * o) & 7u) + ksh)) & kmk;
     };
+    auto b7_of = [&](uint64_t tb) -> uint32_t { return !kB8 && (tb & kPk) ? (uint32_t) tb & 7u : 0u; };
     // The words [from, n) of one run (long runs: high-selectivity survivors, large R runs), with
     // kJoinTailU loads in flight per lane instead of one dependent load per iteration.
     auto tail_run = [&](auto side_c, uint64_t bb, uint32_t from, uint32_t n, auto&& op) {
@@ -2546,7 +2616,7 @@ __device__ __forceinline__ void join_job(const JoinParams& P, const uint32_t blk
             }
 #pragma unroll
             for (int u = 0; u < (int) kJoinTailU; u++)
-                if (o + 64u * u < n) op(key(side_c, v[u], (bb & kPk) != 0));
+                if (o + 64u * u < n) op(key(side_c, v[u], (bb & kPk) != 0, b7_of(bb), lane));  // (from: a multiple of 64)
         }
     };
     // Every word of runs [da, db) of a descriptor batch through op(word): a wave per run, RUNS runs
@@ -2555,13 +2625,14 @@ __device__ __forceinline__ void join_job(const JoinParams& P, const uint32_t blk
                     const uint64_t* nb, uint32_t da, uint32_t db, auto&& op) {
         constexpr int RUNS = decltype(runs_c)::value, WPL = decltype(wpl_c)::value;
         for (uint32_t d = da + wave; d < db; d += kJoinWaves * RUNS) {
-            uint32_t v[RUNS][WPL], n[RUNS], pkm = 0;  // pkm bit r: run r holds 3-byte keys
+            uint32_t v[RUNS][WPL], n[RUNS], pkm = 0, b7m = 0;  // pkm bit r: run r packed; b7m: its tb & 7
 #pragma unroll
             for (int r = 0; r < RUNS; r++) {
                 const uint32_t dd = d + r * kJoinWaves;
                 n[r]              = dd < db ? nc[dd] : 0u;
                 const uint64_t bb = dd < db ? nb[dd] : 0ull;
                 pkm |= (uint32_t) (bb >> 63) << r;
+                b7m |= b7_of(bb) << (3 * r);
 #pragma unroll
                 for (int j = 0; j < WPL; j++) {
                     const uint32_t o = lane + 64u * j;
@@ -2572,7 +2643,7 @@ __device__ __forceinline__ void join_job(const JoinParams& P, const uint32_t blk
             for (int r = 0; r < RUNS; r++) {
 #pragma unroll
                 for (int j = 0; j < WPL; j++)
-                    if (lane + 64u * j < n[r]) op(key(side_c, v[r][j], (pkm >> r) & 1u));
+                    if (lane + 64u * j < n[r]) op(key(side_c, v[r][j], (pkm >> r) & 1u, (b7m >> (3 * r)) & 7u, lane));
                 if (n[r] > 64u * WPL) {
                     const uint64_t bb = nb[d + r * kJoinWaves];
                     tail_run(side_c, bb, 64u * WPL, n[r], op);
@@ -2667,6 +2738,7 @@ __device__ __forceinline__ void join_job(const JoinParams& P, const uint32_t blk
 #endif
         constexpr int FS = HWBRJ_JFS, FSW = HWBRJ_JSW;  // survivor runs per wave loaded with R's
         uint32_t rv[FR][FW], rn[FR], sv[FS][FSW], sn[FS], spk = 0;  // spk bit r: survivor run r packed
+        uint32_t r7m = 0, s7m = 0;  // tb & 7 of the packed runs (3 bits per run)
 #pragma unroll
         for (int r = 0; r < FR; r++) {
             const uint32_t dd = wave + r * kJoinWaves;
@@ -2675,6 +2747,7 @@ __device__ __forceinline__ void join_job(const JoinParams& P, const uint32_t blk
             rn[r] = 0;  // dev ablation (results invalid)
 #endif
             const uint64_t bb = dd < nRd ? rbase[dd] : 0ull;
+            r7m |= b7_of(bb) << (3 * r);
 #pragma unroll
             for (int j = 0; j < FW; j++) {
                 const uint32_t o = lane + 64u * j;
@@ -2690,6 +2763,7 @@ __device__ __forceinline__ void join_job(const JoinParams& P, const uint32_t blk
 #endif
             const uint64_t bb = dd < nSd ? dbase[dd] : 0ull;
             spk |= (uint32_t) (bb >> 63) << r;
+            s7m |= b7_of(bb) << (3 * r);
 #pragma unroll
             for (int j = 0; j < FSW; j++) {
                 const uint32_t o = lane + 64u * j;
@@ -2703,7 +2777,7 @@ __device__ __forceinline__ void join_job(const JoinParams& P, const uint32_t blk
         for (int r = 0; r < FR; r++) {
 #pragma unroll
             for (int j = 0; j < FW; j++)
-                if (lane + 64u * j < rn[r]) set(key(SideR{}, rv[r][j], rpk));
+                if (lane + 64u * j < rn[r]) set(key(SideR{}, rv[r][j], rpk, (r7m >> (3 * r)) & 7u, lane));
             if (rn[r] > 64u * FW) {  // (rare) longer run
                 const uint64_t bb = rbase[wave + r * kJoinWaves];
                 tail_run(SideR{}, bb, 64u * FW, rn[r], set);
@@ -2730,7 +2804,7 @@ __device__ __forceinline__ void join_job(const JoinParams& P, const uint32_t blk
             for (int r = 0; r < FS; r++) {
 #pragma unroll
                 for (int j = 0; j < FSW; j++)
-                    if (lane + 64u * j < sn[r]) test(key(SideS{}, sv[r][j], (spk >> r) & 1u));
+                    if (lane + 64u * j < sn[r]) test(key(SideS{}, sv[r][j], (spk >> r) & 1u, (s7m >> (3 * r)) & 7u, lane));
                 if (sn[r] > 64u * FSW) {
                     const uint64_t bb = dbase[wave + r * kJoinWaves];
                     tail_run(SideS{}, bb, 64u * FSW, sn[r], test);
@@ -2880,19 +2954,20 @@ __device__ __forceinline__ void join_finish(const JoinParams& P, uint64_t cnt, u
     }
 }
 
+template <int KW>
 __global__ __launch_bounds__(kJoinThreads) void k_join(JoinParams P) {
     __shared__ JoinShared L;
-    const bool mixed = __builtin_amdgcn_readfirstlane(P.r_pack3 && P.fmt_cnt && *P.fmt_cnt ? 1u : 0u) != 0;
+    const bool mixed = __builtin_amdgcn_readfirstlane(P.r_kbits && P.fmt_cnt && *P.fmt_cnt ? 1u : 0u) != 0;
     if (mixed) return;  // (k_join_mixed's launch)
     const uint64_t t_start = P.timing ? wall_clock64() : 0;
     uint64_t       cnt = 0, t_probe = 0;
-    join_job<false>(P, blockIdx.x, L, cnt, t_probe);
+    join_job<false, KW>(P, blockIdx.x, L, cnt, t_probe);
     join_finish(P, cnt, t_probe, t_start);
 }
 
 __global__ __launch_bounds__(kJoinThreads) void k_join_mixed(JoinParams P) {
     __shared__ JoinShared L;
-    if (!(P.r_pack3 && P.fmt_cnt && *P.fmt_cnt)) return;
+    if (!(P.r_kbits && P.fmt_cnt && *P.fmt_cnt)) return;
     const uint64_t t_start = P.timing ? wall_clock64() : 0;
     uint64_t       cnt = 0, t_probe = 0;
     for (uint32_t b = blockIdx.x; b < P.jobs + kJoinExtra; b += gridDim.x) {
@@ -4249,7 +4324,10 @@ void launch_join(const JoinParams& p0, uint32_t jobs, uint32_t* job_surv, hipStr
     const uint32_t split = p.split_surv ? p.split_surv : kJoinTaskSurv;
     k_join_split<<<(jobs + 255) / 256, 256, 0, st>>>(p.item_start, job_surv, p.log2NSUB, jobs, split,
                                                      p.nparts, p.extra, p.nextra, p.jsum);
-    k_join<<<jobs + kJoinExtra, kJoinThreads, 0, st>>>(p);
+    // (one key width per launch: k_join's key reads are compile-time for it)
+    if (p.r_kbits == 18) k_join<18><<<jobs + kJoinExtra, kJoinThreads, 0, st>>>(p);
+    else if (p.r_kbits == 24) k_join<24><<<jobs + kJoinExtra, kJoinThreads, 0, st>>>(p);
+    else k_join<32><<<jobs + kJoinExtra, kJoinThreads, 0, st>>>(p);
     k_join_mixed<<<std::min<uint32_t>(jobs + kJoinExtra, 1024u), kJoinThreads, 0, st>>>(p);
 }
 
@@ -4299,6 +4377,7 @@ const char* kernel_build_knobs() {
         num("HWBRJ_JT", HWBRJ_JT, 256);
         num("HWBRJ_JXCD", HWBRJ_JXCD, 1);
         num("HWBRJ_PACK3", HWBRJ_PACK3, 1);
+        num("HWBRJ_PACK18", HWBRJ_PACK18, 1);
         num("HWBRJ_JRR", HWBRJ_JRR, 4);
         num("HWBRJ_JRW", HWBRJ_JRW, 4);
         num("HWBRJ_JSR", HWBRJ_JSR, 8);

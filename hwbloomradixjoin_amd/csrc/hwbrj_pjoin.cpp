@@ -801,6 +801,7 @@ int Engine::join_partitioned(const hwbrj_exchange_t* x, int rank, int world, con
     last_nj_     = 0;      // job_surv holds this join's counts: the next enqueue clears the table
     if (st) {
         memset(st, 0, sizeof(*st));
+        st->join_key_bits  = 32;  // (survivor words travel as codes)
         st->filtered       = args ? small_h[2] : nS;
         st->matches        = (int64_t) small_h[0];
         st->mode           = g.mode;

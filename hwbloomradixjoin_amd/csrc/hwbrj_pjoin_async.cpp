@@ -629,6 +629,7 @@ int Engine::join_partitioned_wait(hwbrj_stats_t* st) {
         st->subparts       = G.NSUB;
         st->slice_segments = G.nseg;
         st->join_keys      = HWBRJ_JOIN_KEYS_32;
+        st->join_key_bits  = 32;
         float ms           = 0;  // the join's device time: its first to its last operation on the stream
         PX_CHECK(hipEventElapsedTime(&ms, pjEv_[2 * e.slot], pjEv_[2 * e.slot + 1]));
         st->ms_total = ms;

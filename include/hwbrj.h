@@ -137,11 +137,13 @@ typedef struct hwbrj_stats_t {
     double   ms_join_probe; /* the survivor-probing share of ms_join (k_join's probe sections),
                                printed as PROBE-TIME-USECS; synchronous joins only (0 for async) */
     /* The key format between the build / probe and the join ("Join keys"):
-     * HWBRJ_JOIN_KEYS_32 32-bit codes, _PACKED 3-byte keys, _MIXED 3-byte keys with the survivor
+     * HWBRJ_JOIN_KEYS_32 32-bit codes, _PACKED packed keys (join_key_bits each), _MIXED packed keys with the survivor
      * runs of unstaged probe items in 32-bit codes. It follows the last waited join on the device
      * (after a join with unstaged items the next one does not pack). */
     int      join_keys;
     uint32_t unstaged_items; /* probe items whose survivors overflowed the probe's LDS stage */
+    uint32_t join_key_bits;  /* bits per packed join key: 18 (the bitmap path's keys, hash_shift 14;
+                                the north star), 24, or 32 for 32-bit codes */
 } hwbrj_stats_t;
 enum { HWBRJ_JOIN_KEYS_32 = 0, HWBRJ_JOIN_KEYS_PACKED = 1, HWBRJ_JOIN_KEYS_MIXED = 2 };
 

@@ -54,9 +54,10 @@ def test_stats_layout_matches_header(hw, tmp_path):
     import ctypes
     src = tmp_path / "st.c"
     src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "hwbrj.h"\nint main(void) {\n'
-                   '  printf("%zu %zu %zu %zu %d %d %d\\n", sizeof(hwbrj_stats_t), offsetof(hwbrj_stats_t, '
+                   '  printf("%zu %zu %zu %zu %zu %d %d %d\\n", sizeof(hwbrj_stats_t), offsetof(hwbrj_stats_t, '
                    'ms_join_probe), offsetof(hwbrj_stats_t, join_keys), offsetof(hwbrj_stats_t, '
-                   'unstaged_items), HWBRJ_JOIN_KEYS_32, HWBRJ_JOIN_KEYS_PACKED, HWBRJ_JOIN_KEYS_MIXED);\n'
+                   'unstaged_items), offsetof(hwbrj_stats_t, join_key_bits), HWBRJ_JOIN_KEYS_32, '
+                   'HWBRJ_JOIN_KEYS_PACKED, HWBRJ_JOIN_KEYS_MIXED);\n'
                    '  return 0;\n}\n')
     exe = tmp_path / "st"
     subprocess.run(["gcc", "-std=gnu11", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"),
@@ -65,7 +66,8 @@ def test_stats_layout_matches_header(hw, tmp_path):
                                           check=True).stdout.split()]
     S = hw._Stats
     assert got == [ctypes.sizeof(S), S.ms_join_probe.offset, S.join_keys.offset,
-                   S.unstaged_items.offset, hw.JOIN_KEYS_32, hw.JOIN_KEYS_PACKED, hw.JOIN_KEYS_MIXED]
+                   S.unstaged_items.offset, S.join_key_bits.offset, hw.JOIN_KEYS_32, hw.JOIN_KEYS_PACKED,
+                   hw.JOIN_KEYS_MIXED]
 
 
 def test_host_hashes_match_reference_kats(hw):
@@ -202,15 +204,17 @@ def test_bench_uses_pmc_traffic_only_for_the_profiled_library(tmp_path, hw):
 
 def test_bench_modeled_join_key_bytes():
     """modeled_bytes prices the join's runs at the key format the join reported
-    (hwbrj_stats_t.join_keys): 3 bytes per key for packed and mixed runs, else 4."""
+    (hwbrj_stats_t.join_keys, join_key_bits): join_key_bits / 8 bytes per key for packed and mixed
+    runs (2.25 for the north star's 18-bit keys), else 4."""
     import importlib.util
     from types import SimpleNamespace as NS
     spec = importlib.util.spec_from_file_location("bench", os.path.join(ROOT, "bench.py"))
     bench = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(bench)
-    assert bench.join_key_bytes(NS(join_keys=1)) == 3.0  # packed (the north star)
-    assert bench.join_key_bytes(NS(join_keys=2)) == 3.0  # mixed
-    assert bench.join_key_bytes(NS(join_keys=0)) == 4.0  # 32-bit codes
+    assert bench.join_key_bytes(NS(join_keys=1, join_key_bits=18)) == 2.25  # packed (the north star)
+    assert bench.join_key_bytes(NS(join_keys=1, join_key_bits=24)) == 3.0
+    assert bench.join_key_bytes(NS(join_keys=2, join_key_bits=18)) == 2.25  # mixed
+    assert bench.join_key_bytes(NS(join_keys=0, join_key_bits=32)) == 4.0  # 32-bit codes
     mb = bench.modeled_bytes(10, 20, 5, 0, 4.0, 3.0)
     assert mb["join_codes_R"] == 60.0 and mb["survivors"] == 30.0
 

@@ -529,5 +529,44 @@ def test_join_key_formats_across_launches(hw, cuda, orc):
         st = hw.join_device(dR, dS, args)
         assert (st.filtered, st.matches) == (filt, res), (name, st)
         assert st.join_keys == keys, (name, st)
+        # 18-bit keys whenever packed (hash_shift 14 at F = 1024, 16 subs), else 32-bit codes
+        assert st.join_key_bits == (32 if keys == hw.JOIN_KEYS_32 else 18), (name, st)
         # unstaged items: some in every mid join (packed or not), none in a lo join
         assert (st.unstaged_items > 0) == (name == "mid"), (name, st)
+
+
+@pytest.mark.parametrize("cfg,bits", [(("blocked", 1 << 24, 1, 1024), 18), (("sectorized", 1 << 24, 2, 512), 18),
+                                      (("blocked", 1 << 24, 1, 1 << 17), 24), (("blocked", 1 << 22, 2, 1 << 15), 24),
+                                      (None, 18)], ids=str)
+def test_join_key_widths(hw, cuda, orc, cfg, bits):
+    """The packed join-key width follows the geometry (join_key_bits): 18 bits where the join keys are
+    v = code >> 14 (F = 1024 with 16 subs, or fewer partitions with 2^(14 - log2F) subs: the bitmap
+    path's keys), 24 bits where fewer subs leave wider keys (m / B = 128 blocks: F = 128 partitions
+    of 2 subs, hash_shift 8, the hash-table path), each counted as the oracle counts, synchronously
+    and through back-to-back async joins (both widths in one run). (A join whose probe items
+    overflowed their stage turns packing off for the next one: the first join of each side may run
+    32-bit codes, the ones after it pack.)"""
+    rng = np.random.default_rng(bits + (cfg[1] if cfg else 0))
+    nR, nS = 1000003, 6000011
+    Rk = rng.permutation(nR).astype(np.int64) + 1
+    Sk = rng.integers(1, 40 * nR, size=nS)
+    R = np.stack([Rk.astype(np.int32), np.arange(nR, dtype=np.int32)], 1)
+    S = np.stack([Sk.astype(np.int32), np.arange(nS, dtype=np.int32)], 1)
+    args = mk(hw, cfg)
+    if args is None:
+        res, filt, _ = orc.bpro(R, S, 8, 0, 0, 0, 0, use_bloom=False)
+    else:
+        res, filt, _ = orc.bpro(R, S, 8, args.variant, args.m, args.k, args.B)
+    dR, dS = to_dev(cuda, R), to_dev(cuda, S)
+    for _ in range(2):
+        st = hw.join_device(dR, dS, args)
+        assert (st.filtered, st.matches) == (filt, res), st
+    assert st.join_key_bits == bits and st.unstaged_items == 0, st
+    other = (hw.BloomFilterArgs(hw.BLOCKED, 1 << 24, 1, 1 << 17) if bits == 18
+             else hw.BloomFilterArgs(hw.BLOCKED, 1 << 24, 1, 1024))
+    ost = hw.join_device(dR, dS, other)
+    for a in (args, other, args):
+        hw.join_device_async(dR, dS, a)
+    sts = hw.join_wait_all()
+    assert [(x.filtered, x.matches) for x in sts] == [(filt, res), (ost.filtered, ost.matches), (filt, res)]
+    assert {sts[0].join_key_bits, sts[1].join_key_bits} == {18, 24}, sts
