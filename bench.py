@@ -25,6 +25,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import statistics
 import os
 import sys
 import threading
@@ -319,7 +320,7 @@ def headline_line(a, hw, torch, dist, rank, world, dR, dS, args, st, last, sums,
     # its ms in the timed joins' own schedule (S scatter on the side stream beside the R side; the
     # frac below uses it), the one-stream synchronous joins' phase time beside it
     use_async = dom == "s_scatter" and len(async_sc) > 0
-    dom_ms = sum(async_sc) / len(async_sc) if use_async else dom_ms_sync
+    dom_ms = statistics.median(async_sc) if use_async else dom_ms_sync  # (median: one slow join of K moves a mean)
     word_bytes = 2.75 if st.format == 2 else 4.0  # FMT_C22: 22-bit S words (88-byte chunks)
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": peak, "unit": "GB/s",
                 "frac": round(achieved / peak, 4), "traffic": traffic,
@@ -339,9 +340,10 @@ def headline_line(a, hw, torch, dist, rank, world, dR, dS, args, st, last, sums,
                              "probe": "k_probe", "build": "k_build", "join": "k_join"}[dom],
                     "ms": round(dom_ms, 4), "algorithmic_bytes": dom_alg,
                     "schedule": ("async two-stream joins (the timed schedule): S scatter events on its side "
-                                 f"stream, mean of {len(async_sc)} back-to-back joins" if use_async else
+                                 f"stream, median of {len(async_sc)} back-to-back joins" if use_async else
                                  "synchronous one-stream joins (phase events)"),
                     "ms_async_min_max": [round(min(async_sc), 4), round(max(async_sc), 4)] if use_async else None,
+                    "ms_async_mean": round(statistics.mean(async_sc), 4) if use_async else None,
                     "ms_sync_phase": round(dom_ms_sync, 4),
                     "achieved": round(dom_alg / (dom_ms * 1e-3) / 1e9, 1) if dom_alg else None,
                     "frac": round(dom_alg / (dom_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if dom_alg else None,
