@@ -321,7 +321,7 @@ def headline_line(a, hw, torch, dist, rank, world, dR, dS, args, st, last, sums,
     # frac below uses it), the one-stream synchronous joins' phase time beside it
     use_async = dom == "s_scatter" and len(async_sc) > 0
     dom_ms = statistics.median(async_sc) if use_async else dom_ms_sync  # (median: one slow join of K moves a mean)
-    word_bytes = 2.75 if st.format == 2 else 4.0  # FMT_C22: 22-bit S words (88-byte chunks)
+    word_bytes = 4.0  # S partition words (4 bytes in every format)
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": peak, "unit": "GB/s",
                 "frac": round(achieved / peak, 4), "traffic": traffic,
                 "algorithmic_bytes": alg_bytes, "launch": "one full join (every kernel of BPRO)",

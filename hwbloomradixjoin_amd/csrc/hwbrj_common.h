@@ -102,7 +102,6 @@ enum Mode : int {
 enum Format : int {
     FMT_CODE   = 0,  // element word = code = crc32c(42, key) (MODE_SLICE_BASIC: bmix(key))
     FMT_PACKED = 1,  // blocked, log2B <= log2F: (first bit-in-block) | (code >> log2F) << log2B (low bits: the slice bit)
-    FMT_C22    = 2,  // S side, blocked, log2F = 10: the 22-bit code >> 10 alone, 32 elements packed
                      // into a 22-dword (88-byte) chunk; the probe recomputes the bit-in-block from
                      // the key (inverse CRC + CrapWow)
 };
@@ -144,8 +143,6 @@ enum Kind : int {
                            // the word, the key (for the rest) is recovered only for those that pass
     KIND_BASIC_KK    = 5,  // basic, k >= 2: the first bit from the LDS slice, bits 2..k of the
                            // candidates from the global bitmap (slices = its transpose)
-    KIND_BLOCK_Z1    = 6,  // blocked/sectorized, k = 1, FMT_C22 S words (key recovered per word)
-    KIND_BLOCK_ZK    = 7,  // blocked/sectorized, k >= 2, FMT_C22 S words
 };
 
 constexpr uint32_t kMaxLog2F     = 10;

@@ -181,11 +181,9 @@ bool plan_geometry(const bloom_filter_args_t* a, uint64_t nR, Geometry* g, std::
             g->seg_words  = std::max<uint32_t>(4, g->seg_bits / 32);
         }
         if (g->mode == MODE_SLICE_BLOCK && ilog2u(B) <= g->log2F) g->format = FMT_PACKED;
-        // S partitions: FMT_C22 (22-bit words in 88-byte chunks) is a dev A/B (HWBRJ_DEV_C22): it cuts
-        // the S traffic by 2.6 GB per join, but the probe's per-word key recovery costs more than
-        // that saves
+        // S partitions use R's word format (the 22-bit S words of round 2, FMT_C22, cut 2.6 GB of
+        // S traffic but cost more in the probe's key recovery: removed in round 6)
         g->s_format = g->format;
-        if (!mat && g->mode == MODE_SLICE_BLOCK && g->log2F == 10 && dev_knobs().c22) g->s_format = FMT_C22;
         if (g->mode == MODE_SLICE_BLOCK || g->mode == MODE_SLICE_BASIC) g->log2seg = ilog2u(g->seg_bits);
         if (a->variant != BASIC) {
             g->log2B    = ilog2u(B);
@@ -251,7 +249,6 @@ const DevKnobs& dev_knobs() {
         };
         d.kk1       = getenv("HWBRJ_DEV_KK1") != nullptr;
         d.kk_gather = getenv("HWBRJ_DEV_KK_GATHER") != nullptr;
-        d.c22       = getenv("HWBRJ_DEV_C22") != nullptr;
         d.noxcd     = getenv("HWBRJ_DEV_NOXCD") != nullptr;
         d.dbg       = getenv("HWBRJ_DBG") != nullptr;
         d.maxf      = u("HWBRJ_DEV_MAXF");
@@ -272,7 +269,6 @@ std::string dev_knobs_string() {
     auto add = [&](const std::string& w) { r += (r.empty() ? "" : " ") + w; };
     if (d.kk1) add("HWBRJ_DEV_KK1");
     if (d.kk_gather) add("HWBRJ_DEV_KK_GATHER");
-    if (d.c22) add("HWBRJ_DEV_C22");
     if (d.noxcd) add("HWBRJ_DEV_NOXCD");
     if (d.dbg) add("HWBRJ_DBG");
     if (d.maxf) add("HWBRJ_DEV_MAXF=" + std::to_string(d.maxf));

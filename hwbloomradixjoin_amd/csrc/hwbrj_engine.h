@@ -16,7 +16,7 @@ namespace hwbrj {
 
 // Picks mode / partitioning / slice geometry for a filter configuration (DESIGN.md "Modes").
 // Returns false (and sets *err) for configurations outside the reference's contract.
-// mat: the materializing pipeline's geometry (no FMT_C22 S words; join jobs sized for its hash
+// mat: the materializing pipeline's geometry (join jobs sized for its hash
 // table, k_join_mat).
 bool plan_geometry(const bloom_filter_args_t* args, uint64_t nR, Geometry* g, std::string* err,
                    bool mat = false);

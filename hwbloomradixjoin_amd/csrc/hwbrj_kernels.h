@@ -294,7 +294,6 @@ const char* kernel_build_knobs();
 struct DevKnobs {
     bool     kk1 = false;        // HWBRJ_DEV_KK1: basic k = 1 on the bit-pass pipeline
     bool     kk_gather = false;  // HWBRJ_DEV_KK_GATHER: basic k >= 2 by global-slice gathers
-    bool     c22 = false;        // HWBRJ_DEV_C22: 22-bit S words (FMT_C22)
     bool     noxcd = false;      // HWBRJ_DEV_NOXCD: k_join_mat without XCD-aware job order
     bool     dbg = false;        // HWBRJ_DBG: in-kernel phase stamps (a -DHWBRJ_STAMPS build)
     uint32_t maxf = 0;           // HWBRJ_DEV_MAXF: cap on the partition count F

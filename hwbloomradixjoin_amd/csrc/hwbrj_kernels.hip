@@ -171,12 +171,7 @@ __device__ __forceinline__ Loc locate(uint32_t w, const Geometry& g, const uint3
         return L;
     }
     uint32_t lb;
-    if (KIND == KIND_BLOCK_Z1 || KIND == KIND_BLOCK_ZK) {  // FMT_C22: the key from the code
-        const uint32_t key = code_key(inv, decode_k<KIND>(w, q, g));
-        lb  = w & g.lbmask;
-        L.h = crapwow(kSeed, key) & (g.B - 1u);
-        L.y = (key + kSeed) & (g.B - 1u);
-    } else if (KIND == KIND_BLOCK_PK1 || KIND == KIND_BLOCK_PKK) {
+    if (KIND == KIND_BLOCK_PK1 || KIND == KIND_BLOCK_PKK) {
         lb  = (w >> g.log2B) & g.lbmask;  // (code >> log2F) & (nblocks/F - 1)
         L.h = w & (g.B - 1u);             // crapwow(key) & (B-1), stored by the scatter
         L.y = KIND == KIND_BLOCK_PKK ? (code_key(inv, decode_k<KIND>(w, q, g)) + kSeed) & (g.B - 1u) : 0u;
@@ -195,7 +190,7 @@ __device__ __forceinline__ Loc locate(uint32_t w, const Geometry& g, const uint3
 // SET: add the key's bits (ds_or); otherwise test them (src/bloom_filter.c:73-111 per variant).
 template <int KIND, bool SET>
 __device__ __forceinline__ bool apply_bits(const Loc& L, const Geometry& g, uint32_t* slice) {
-    if (KIND == KIND_BASIC_K1 || KIND == KIND_BASIC_KK || KIND == KIND_BLOCK_PK1 || KIND == KIND_BLOCK_Z1) {
+    if (KIND == KIND_BASIC_K1 || KIND == KIND_BASIC_KK || KIND == KIND_BLOCK_PK1) {
         const uint32_t b = L.base + L.h;
         if (SET) {
             atomicOr(slice + (b >> 5), 1u << (b & 31u));
@@ -226,7 +221,6 @@ __device__ __forceinline__ bool apply_bits(const Loc& L, const Geometry& g, uint
 template <int KIND>
 __device__ __forceinline__ uint32_t decode_k(uint32_t w, uint32_t q, const Geometry& g) {
     if (KIND == KIND_BLOCK_PK1 || KIND == KIND_BLOCK_PKK) return ((w >> g.log2B) << g.log2F) | q;  // drops the h bits
-    if (KIND == KIND_BLOCK_Z1 || KIND == KIND_BLOCK_ZK) return (w << g.log2F) | q;
     return w;
 }
 
@@ -489,27 +483,6 @@ __device__ __forceinline__ uint32_t crc_nib(const uint32_t* tab, uint32_t key) {
     return __builtin_amdgcn_bitop3_b32(a, c, t6 ^ t7, 0x96);
 }
 
-// The key of FMT_C22 word w of partition q (log2F = 10): code = w << 10 | q, key = finv(code) ^ 42
-// from the inverse nibble table at LDS address 0 (row offsets are immediates, reads conflict-free
-// as in crc_nib). Rows 0 and 1 (code bits 0..7 = q's low byte) and the seed are the partition's
-// constant cq = z_const(tab, q).
-__device__ __forceinline__ uint32_t z_const(const uint32_t* tab, uint32_t q) {
-    return tab[q & 15u] ^ tab[16u + ((q >> 4) & 15u)] ^ kSeed;
-}
-
-__device__ __forceinline__ uint32_t z_key(const uint32_t* tab, uint32_t w, uint32_t q, uint32_t cq) {
-    const char*    b = (const char*) tab;
-    const uint32_t c = (w << 10) | (q & 0x300u);
-    const uint32_t y = c & 0x0F0F0F0Fu, z = c & 0xF0F0F0F0u;
-    auto T = [&](uint32_t off) { return *(const uint32_t*) (b + off); };
-    const uint32_t t2 = T(byte_sh2<1, false>(y) + 128), t3 = T(byte_sh2<1, true>(z) + 192);
-    const uint32_t t4 = T(byte_sh2<2, false>(y) + 256), t5 = T(byte_sh2<2, true>(z) + 320);
-    const uint32_t t6 = T(byte_sh2<3, false>(y) + 384), t7 = T(byte_sh2<3, true>(z) + 448);
-    const uint32_t a = __builtin_amdgcn_bitop3_b32(t2, t3, t4, 0x96);
-    const uint32_t d = __builtin_amdgcn_bitop3_b32(t5, t6, t7, 0x96);
-    return a ^ d ^ cq;
-}
-
 template <int SRC, int MODE, int FMT>
 __device__ __forceinline__ void sc_word_lds0(uint32_t x, const Geometry& g, const uint32_t* tab,
                                              uint32_t& w, uint32_t& q) {
@@ -538,9 +511,6 @@ __device__ __forceinline__ void sc_word_lds0(uint32_t x, const Geometry& g, cons
         // the key (mixed, bmix): the join compares words, and nothing downstream needs the CRC
         q = mod_m(crapwow(kSeed, key), (uint32_t) g.m) & F1;
         w = bmix(key);
-    } else if (MODE == MODE_SLICE_BLOCK && FMT == FMT_C22) {
-        q = code & F1;  // log2F = 10: the word is the remaining 22 code bits, nothing else
-        w = code >> 10;
     } else if (MODE == MODE_SLICE_BLOCK && FMT == FMT_PACKED) {
         q = code & F1;
 #ifdef HWBRJ_ABL_NOCRAP
@@ -552,55 +522,6 @@ __device__ __forceinline__ void sc_word_lds0(uint32_t x, const Geometry& g, cons
         q = code & F1;
         w = code;
     }
-}
-
-// FMT_C22 chunks: element i (< 2^22) of a 32-element chunk at bits 22 i .. 22 i + 21 of its 22
-// dwords (88 bytes). Eight lanes write a chunk: lane l8 packs elements 4 l8 .. 4 l8 + 3 (88 bits
-// at bit 88 l8); with j = l8 & 3 the payload starts s = 88 j mod 32 = {0, 24, 16, 8} bits into
-// dword h * 11 + {0, 2, 5, 8}[j] of its half h = l8 >> 2. The lane owns dwords h * 11 + 3 j ..
-// (3 of them, 2 for j = 3); the dword it shares with lane l8 - 1 is completed there (DPP).
-struct C22Out {
-    uint32_t o0, o1, o2;  // owned dwords (o2 unused for j = 3)
-    uint32_t word;        // first owned dword index inside the chunk
-    bool     has2;        // o2 is owned (j < 3)
-};
-
-__device__ __forceinline__ C22Out c22_pack(uint32_t e0, uint32_t e1, uint32_t e2, uint32_t e3, uint32_t l8) {
-    const uint32_t j = l8 & 3u, s = (24u * j) & 31u;
-    const uint32_t P0 = e0 | (e1 << 22), P1 = (e1 >> 10) | (e2 << 12), P2 = (e2 >> 20) | (e3 << 2);
-    const uint32_t X0 = P0 << s;
-    const uint32_t X1 = s ? (P1 << s) | (P0 >> (32u - s)) : P1;
-    const uint32_t X2 = s ? (P2 << s) | (P1 >> (32u - s)) : P2;
-    const uint32_t X3 = s ? (P2 >> (32u - s)) : 0u;
-    // head: this lane's share of the previous lane's last dword; take the next lane's head
-    const uint32_t head = s ? X0 : 0u;
-    const uint32_t nxt  = (uint32_t) __builtin_amdgcn_update_dpp(0, (int) head, 0x101, 0xf, 0xf, false);  // row_shl:1
-    C22Out r;
-    r.o0   = s ? X1 : X0;
-    r.o1   = s ? X2 : X1;
-    r.o2   = (s ? X3 : X2) | nxt;
-    r.word = (l8 >> 2) * 11u + 3u * j;
-    r.has2 = j < 3u;
-    return r;
-}
-
-// The 4 elements of lane l8 from the 4 dwords at dword (l8 >> 2) * 11 + {0, 2, 5, 8}[l8 & 3]
-// of a FMT_C22 chunk (c22_load_dword gives that offset).
-__device__ __forceinline__ uint32_t c22_load_dword(uint32_t l8) {
-    const uint32_t j = l8 & 3u;
-    return (l8 >> 2) * 11u + ((11u * j) >> 2);
-}
-
-__device__ __forceinline__ uint4 c22_unpack(uint4 W, uint32_t l8) {
-    const uint32_t j = l8 & 3u, s = (24u * j) & 31u;
-    constexpr uint32_t M = (1u << 22) - 1u;
-    const uint32_t b1 = s + 22u, b2 = s + 44u, b3 = s + 66u;
-    uint4 e;
-    e.x = __builtin_amdgcn_alignbit(W.y, W.x, s) & M;
-    e.y = (b1 < 32u ? __builtin_amdgcn_alignbit(W.y, W.x, b1) : __builtin_amdgcn_alignbit(W.z, W.y, b1 - 32u)) & M;
-    e.z = (b2 < 64u ? __builtin_amdgcn_alignbit(W.z, W.y, b2 - 32u) : __builtin_amdgcn_alignbit(W.w, W.z, b2 - 64u)) & M;
-    e.w = __builtin_amdgcn_alignbit(W.w, W.z, b3 - 64u) & M;
-    return e;
 }
 
 template <int SRC>
@@ -659,7 +580,7 @@ __device__ __forceinline__ void scatter_body(const ScatterParams& P) {
         e0  = wg * P.seg_stride;
         len = __builtin_amdgcn_readfirstlane(P.seg_cnt[wg]);
     }
-    constexpr uint32_t CW = FMT == FMT_C22 ? 22u : 32u;  // dwords per chunk
+    constexpr uint32_t CW = 32u;  // dwords per chunk
     uint32_t* __restrict__ pool = P.pool + wg * P.cap * CW;
     uint32_t* __restrict__ meta = P.meta + wg * P.cap;
     constexpr uint32_t EB = SRC == SRC_TUPLES ? 8u : 4u;  // bytes per element
@@ -735,21 +656,10 @@ __device__ __forceinline__ void scatter_body(const ScatterParams& P) {
             const uint32_t l8 = k & 7;
             const uint32_t cb = ncb[(par ^ 1u) * F + qq] & kCbMask;
             const v4u      v  = *(const v4u*) &stage[qq * 32 + l8 * 4];
-            if (FMT == FMT_C22) {
-                const C22Out o = c22_pack(v.x, v.y, v.z, v.w, l8);
-                const uint32_t d = cb * 22u + o.word;
-                typedef unsigned int v2u __attribute__((ext_vector_type(2)));
-                v2u o01;
-                o01.x = o.o0;
-                o01.y = o.o1;
-                __builtin_amdgcn_raw_buffer_store_b64(o01, rpool, ok ? d * 4 : kOob, 0, 0);
-                __builtin_amdgcn_raw_buffer_store_b32(o.o2, rpool, ok && o.has2 ? (d + 2) * 4 : kOob, 0, 0);
-            } else {
 #ifdef HWBRJ_ABL_NOSTORE
             if (v.x == 0x12345678u && v.y == 0x9abcdef0u)  // dev ablation: practically never stores
 #endif
             __builtin_amdgcn_raw_buffer_store_b128(v, rpool, ok ? (cb * 32 + l8 * 4) * 4 : kOob, 0, SAUX);
-            }
             __builtin_amdgcn_raw_buffer_store_b32(qq | (32u << 16), rmeta, ok && l8 == 0 ? cb * 4 : kOob, 0, 0);
         };
 #pragma unroll
@@ -795,17 +705,8 @@ __device__ __forceinline__ void scatter_body(const ScatterParams& P) {
                 const uint32_t cb = ncb[(par ^ 1u) * F + qq], nch = cb >> kCbBits;
                 const bool     st = sl >= nch * 32;
                 stage[ok && st ? qq * 32 + sl - nch * 32 : dummy] = pw[j];
-                if (FMT == FMT_C22) {  // into the zeroed packed chunk: two adds of disjoint bits
-                    const uint32_t bit = (sl & 31u) * 22u, sh = bit & 31u;
-                    const uint32_t d   = ((cb & kCbMask) + (sl >> 5)) * 22u + (bit >> 5);
-                    const bool     go  = ok && !st;
-                    __builtin_amdgcn_raw_ptr_buffer_atomic_add_i32((int) (pw[j] << sh), rpool, go ? d * 4 : kOob, 0, 0);
-                    __builtin_amdgcn_raw_ptr_buffer_atomic_add_i32((int) (sh > 10u ? pw[j] >> (32u - sh) : 0u), rpool,
-                                                                   go && sh > 10u ? (d + 1) * 4 : kOob, 0, 0);
-                } else {
-                    const uint32_t po = ((cb & kCbMask) + (sl >> 5)) * 128 + (sl & 31u) * 4;
-                    __builtin_amdgcn_raw_buffer_store_b32(pw[j], rpool, ok && !st ? po : kOob, 0, 0);
-                }
+                const uint32_t po = ((cb & kCbMask) + (sl >> 5)) * 128 + (sl & 31u) * 4;
+                __builtin_amdgcn_raw_buffer_store_b32(pw[j], rpool, ok && !st ? po : kOob, 0, 0);
             }
         }
     };
@@ -908,11 +809,7 @@ __device__ __forceinline__ void scatter_body(const ScatterParams& P) {
                 fill[qq]          = f & 31u;
                 my_tch[pp] += nch;
                 my_tel[pp] += nch * 32;
-                for (uint32_t c = 1; c < nch; c++) {  // direct chunks
-                    meta[cb + c] = qq | (32u << 16);
-                    if (FMT == FMT_C22)  // filled by atomic adds after the next barriers
-                        for (uint32_t d = 0; d < 22u; d++) pool[(cb + c) * 22u + d] = 0u;
-                }
+                for (uint32_t c = 1; c < nch; c++) meta[cb + c] = qq | (32u << 16);  // direct chunks
             }
         }
         stamp(4);
@@ -960,15 +857,7 @@ __device__ __forceinline__ void scatter_body(const ScatterParams& P) {
             const uint32_t qq = k >> 3, l8 = k & 7;
             const bool     ok = fill[qq] > 0;
             const v4u      v  = *(const v4u*) &stage[qq * 32 + l8 * 4];
-            if (FMT == FMT_C22) {
-                const C22Out   o = c22_pack(v.x, v.y, v.z, v.w, l8);
-                const uint32_t d = ncb[qq] * 22u + o.word;
-                __builtin_amdgcn_raw_buffer_store_b32(o.o0, rpool, ok ? d * 4 : kOob, 0, 0);
-                __builtin_amdgcn_raw_buffer_store_b32(o.o1, rpool, ok ? (d + 1) * 4 : kOob, 0, 0);
-                __builtin_amdgcn_raw_buffer_store_b32(o.o2, rpool, ok && o.has2 ? (d + 2) * 4 : kOob, 0, 0);
-            } else {
-                __builtin_amdgcn_raw_buffer_store_b128(v, rpool, ok ? (ncb[qq] * 32 + l8 * 4) * 4 : kOob, 0, 0);
-            }
+            __builtin_amdgcn_raw_buffer_store_b128(v, rpool, ok ? (ncb[qq] * 32 + l8 * 4) * 4 : kOob, 0, 0);
         }
         __syncthreads();
         if (tid == 0) P.wg_used[wg] = misc[0];
@@ -1553,15 +1442,13 @@ __device__ __forceinline__ void load_list_u(const uint32_t* __restrict__ list, u
 }
 
 // NT: non-temporal chunk loads (the chunks are read once)
-template <int NPQ, bool C22 = false, bool NT = false>
+template <int NPQ, bool NT = false>
 __device__ __forceinline__ void load_chunks_u(const uint32_t* __restrict__ pool, const uint32_t (&ent)[NPQ],
                                               uint32_t lb, uint32_t le, Sweep<NPQ>& S) {
     const uint32_t l8 = threadIdx.x & 7, cslot = threadIdx.x >> 3;
 #pragma unroll
     for (int j = 0; j < NPQ; j++) {
-        if (C22)  // 16 bytes at a dword-aligned offset of the 88-byte chunk (c22_unpack decodes them)
-            __builtin_memcpy(&S.v[j], &pool[(uint64_t) (ent[j] & kListIdMask) * 22 + c22_load_dword(l8)], 16);
-        else if (NT) {
+        if (NT) {
             const v4u v = __builtin_nontemporal_load((const v4u*) &pool[(uint64_t) (ent[j] & kListIdMask) * 32 + l8 * 4]);
             S.v[j]      = make_uint4(v.x, v.y, v.z, v.w);
         } else
@@ -1637,14 +1524,14 @@ __global__ __launch_bounds__(1024) void k_build(BuildParams P) {
             load_list_u<kBPQ>(P.list, l0, l1, eA);
             const uint32_t n1 = min(l0 + GRP, l1 - 1u);
             load_list_u<kBPQ>(P.list, n1, min(n1 + GRP, l1), eB);
-            load_chunks_u<kBPQ, false, kBdNT>(P.pool, eA, l0, l1, SA);
+            load_chunks_u<kBPQ, kBdNT>(P.pool, eA, l0, l1, SA);
             if (PAY) load_chunks_u<kBPQ>(P.ppool, eA, l0, l1, PA);
         }
         for (uint32_t lb = l0; lb < l1; lb += GRP) {
             const uint32_t nb = min(lb + GRP, l1 - 1u);  // next group (re-reads the last entry past the end)
             const uint32_t ne = min(nb + GRP, l1);
             const uint32_t nnb = min(nb + GRP, l1 - 1u);  // the group after it (its list entries)
-            load_chunks_u<kBPQ, false, kBdNT>(P.pool, eB, nb, ne, SB);
+            load_chunks_u<kBPQ, kBdNT>(P.pool, eB, nb, ne, SB);
             if (PAY) load_chunks_u<kBPQ>(P.ppool, eB, nb, ne, PB);
             load_list_u<kBPQ>(P.list, nnb, min(nnb + GRP, l1), eC);
 #pragma unroll
@@ -1769,7 +1656,7 @@ constexpr uint32_t kProbeCH = 128u * kPC;     // chunks per probe item (1024 thr
 #define HWBRJ_SCRK 256
 #endif
 template <int KIND> constexpr uint32_t scr_cap() {
-    return KIND == KIND_BLOCK_PKK || KIND == KIND_BASIC_KK || KIND == KIND_BLOCK_ZK ? (uint32_t) HWBRJ_SCRK
+    return KIND == KIND_BLOCK_PKK || KIND == KIND_BASIC_KK ? (uint32_t) HWBRJ_SCRK
                                                                                      : (uint32_t) HWBRJ_SCR1;
 }
 // Dev ablations of the probe's parts (dev builds only; results invalid except `filtered`):
@@ -1815,11 +1702,10 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
     const uint32_t  F      = 1u << g.log2F;
     const uint32_t  NSUB   = 1u << g.log2NSUB;
     constexpr bool  slices = KIND != KIND_PASS;
-    constexpr bool  zfmt   = KIND == KIND_BLOCK_Z1 || KIND == KIND_BLOCK_ZK;  // FMT_C22 chunks
     constexpr bool  onebit = KIND == KIND_BLOCK_PK1 || KIND == KIND_BASIC_K1 || KIND == KIND_BLOCK_PKK ||
-                             KIND == KIND_BASIC_KK || zfmt;
+                             KIND == KIND_BASIC_KK;
     // onebit tests only the first bit: test the rest (basic: from the global bitmap)
-    constexpr bool  refine = KIND == KIND_BLOCK_PKK || KIND == KIND_BASIC_KK || KIND == KIND_BLOCK_ZK;
+    constexpr bool  refine = KIND == KIND_BLOCK_PKK || KIND == KIND_BASIC_KK;
     constexpr int   NW     = kPC * 4;   // words per thread per item
     const uint32_t  segw   = slices ? g.seg_words : 0;  // multiple of 4
     const uint32_t  scap   = P.stage_cap;               // survivor words per stage buffer
@@ -1946,27 +1832,22 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
             load_list_u<kPC>(P.list, lb_of(p0), le_of(p0), eA);
             load_list_u<kPC>(P.list, lb_of(pa), le_of(pa), eB);
             load_list_u<kPC>(P.list, lb_of(pb), le_of(pb), eC);
-            load_chunks_u<kPC, zfmt, kPrNT>(P.pool, eA, lb_of(p0), le_of(p0), SA);
-            load_chunks_u<kPC, zfmt, kPrNT>(P.pool, eB, lb_of(pa), le_of(pa), SB);
+            load_chunks_u<kPC, kPrNT>(P.pool, eA, lb_of(p0), le_of(p0), SA);
+            load_chunks_u<kPC, kPrNT>(P.pool, eB, lb_of(pa), le_of(pa), SB);
         }
         if (slices) {
             __syncthreads();  // every wave is done with the previous slice
             slice_to_lds(slice, P.slices + ((uint64_t) q * nseg + seg) * segw, segw);
             __syncthreads();
         }
-        const uint32_t cq = zfmt ? z_const(zinv, q) : 0u;  // (zinv complete: the barriers above)
         // Sc: words of piece p (registers); en: list entries of p+2 -> Sl; enn <- list of p+3.
         auto step = [&](uint32_t p, Sweep<kPC>& Sc, Sweep<kPC>& Sl, const uint32_t (&en)[kPC],
                         uint32_t (&enn)[kPC]) {
             const uint32_t p2  = min(p + 2, p1 - 1);
             const uint32_t p3  = min(p + 3, p1 - 1);
             const uint32_t cb3 = nstep % 3;  // counter buffer of this piece
-            load_chunks_u<kPC, zfmt, kPrNT>(P.pool, en, lb_of(p2), le_of(p2), Sl);
+            load_chunks_u<kPC, kPrNT>(P.pool, en, lb_of(p2), le_of(p2), Sl);
             load_list_u<kPC>(P.list, lb_of(p3), le_of(p3), enn);
-            if (zfmt) {  // the 22-bit words of this piece, in place
-#pragma unroll
-                for (int j = 0; j < kPC; j++) Sc.v[j] = c22_unpack(Sc.v[j], (uint32_t) tid & 7u);
-            }
             stamp(0);
             uint32_t* cnt = subc + cb3 * 128;
             uint32_t* scr = scratch + wave * kScrCap;
@@ -1988,9 +1869,6 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeParams P) {
                         bb[i] = w;  // (the test below uses only its low 5 bits)
                         wv[i] = slice[__builtin_amdgcn_ubfe(w, 5u, lw)];
                         continue;
-                    } else if (zfmt && SEG1) {  // first bit = crapwow(key) & (B - 1) (add_generic)
-                        const uint32_t key = z_key(zinv, w, q, cq);
-                        bb[i] = ((w & g.lbmask) << g.log2B) + (crapwow(kSeed, key) & (g.B - 1u));
                     } else {
                         const Loc L = locate<KIND>(w, g, inv, q);
                         bb[i]       = L.base + L.h;
@@ -4173,7 +4051,7 @@ static void scatter_pay_inst(const ScatterParams& p, int side, uint32_t grid, hi
 
 void launch_scatter(const ScatterParams& p, int src, int side, uint32_t grid, hipStream_t st) {
     const Geometry& g = p.g;
-    if (p.ppool) {  // tuples with payloads (materialization): no FMT_C22, no global-mode codes
+    if (p.ppool) {  // tuples with payloads (materialization): no global-mode codes
         switch (g.mode) {
             case MODE_SLICE_BLOCK:
                 if (g.format == FMT_PACKED) return scatter_pay_inst<MODE_SLICE_BLOCK, FMT_PACKED>(p, side, grid, st);
@@ -4189,8 +4067,6 @@ void launch_scatter(const ScatterParams& p, int src, int side, uint32_t grid, hi
     }
     switch (g.mode) {
         case MODE_SLICE_BLOCK:
-            if (side == SIDE_S && g.s_format == FMT_C22)
-                return scatter_inst<SRC_TUPLES, MODE_SLICE_BLOCK, FMT_C22>(p, side, grid, st);
             if (g.format == FMT_PACKED)
                 return scatter_inst<SRC_TUPLES, MODE_SLICE_BLOCK, FMT_PACKED>(p, side, grid, st);
             return scatter_inst<SRC_TUPLES, MODE_SLICE_BLOCK, FMT_CODE>(p, side, grid, st);
@@ -4232,12 +4108,6 @@ int consumer_kind(const Geometry& g) {
     if (g.mode == MODE_SLICE_BLOCK)
         return g.format == FMT_PACKED ? (g.k == 1 ? KIND_BLOCK_PK1 : KIND_BLOCK_PKK) : KIND_BLOCK;
     return KIND_PASS;
-}
-
-// the probe's kind: the S partitions' word format (g.s_format) decides
-static int probe_kind(const Geometry& g) {
-    if (g.mode == MODE_SLICE_BLOCK && g.s_format == FMT_C22) return g.k == 1 ? KIND_BLOCK_Z1 : KIND_BLOCK_ZK;
-    return consumer_kind(g);
 }
 
 
@@ -4289,8 +4159,8 @@ void launch_build(const BuildParams& p, uint32_t F, hipStream_t st) {
 size_t probe_lds_bytes(const Geometry& g, uint32_t* stage_cap, bool pay) {
     const bool   slices = g.mode == MODE_SLICE_BLOCK || g.mode == MODE_SLICE_BASIC;
     const size_t NSUB   = (size_t) 1 << g.log2NSUB;
-    const int    kind   = probe_kind(g);
-    const size_t scap   = pay ? 0 : kind == KIND_BLOCK_PKK || kind == KIND_BASIC_KK || kind == KIND_BLOCK_ZK
+    const int    kind   = consumer_kind(g);
+    const size_t scap   = pay ? 0 : kind == KIND_BLOCK_PKK || kind == KIND_BASIC_KK
                               ? scr_cap<KIND_BLOCK_PKK>() : scr_cap<KIND_PASS>();
     const size_t base   = ((slices ? g.seg_words : 0) + 3 * 128 + 16 * NSUB + 16 * scap + 64) * sizeof(uint32_t);
     // 2 buffers of cap words + 64 dummy slots each, in what the 512-byte static table leaves
@@ -4304,9 +4174,7 @@ size_t probe_lds_bytes(const Geometry& g, uint32_t* stage_cap, bool pay) {
 void launch_probe(const ProbeParams& p0, uint32_t grid, hipStream_t st) {
     ProbeParams p = p0;
     const size_t lds = probe_lds_bytes(p.g, &p.stage_cap, p.surv_pos != nullptr);
-    switch (probe_kind(p.g)) {
-        case KIND_BLOCK_Z1: return probe_inst<KIND_BLOCK_Z1>(p, grid, lds, st);
-        case KIND_BLOCK_ZK: return probe_inst<KIND_BLOCK_ZK>(p, grid, lds, st);
+    switch (consumer_kind(p.g)) {
         case KIND_BLOCK_PK1: return probe_inst<KIND_BLOCK_PK1>(p, grid, lds, st);
         case KIND_BLOCK_PKK: return probe_inst<KIND_BLOCK_PKK>(p, grid, lds, st);
         case KIND_BLOCK: return probe_inst<KIND_BLOCK>(p, grid, lds, st);

@@ -106,7 +106,7 @@ int Engine::join_partitioned(const hwbrj_exchange_t* x, int rank, int world, con
         set_last_error("the partitioned join needs partition slices (blocked/sectorized, basic k = 1, or no filter)");
         return 9;
     }
-    g.s_format = g.format;  // (FMT_C22 is a single-GPU experiment)
+    g.s_format = g.format;
     const uint32_t F = 1u << g.log2F, NSUB = 1u << g.log2NSUB;
     if (world < 1 || rank < 0 || rank >= world || F % (uint32_t) world != 0) {
         set_last_error("world must divide the partition count F = " + std::to_string(F));

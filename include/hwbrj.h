@@ -120,7 +120,7 @@ typedef struct hwbrj_stats_t {
     uint64_t filtered;      /* "S-tuples after filter" (= |S| without a filter) */
     int64_t  matches;       /* "Results" */
     int      mode;          /* 0 nobloom, 1 slice-blocked, 2 slice-basic, 3 global fallback */
-    int      format;        /* S partition words: 0 codes, 1 packed (code + bit), 2 22-bit codes */
+    int      format;        /* S partition words: 0 codes, 1 packed (code + bit) */
     uint32_t partitions;    /* F */
     uint32_t subparts;      /* join sub-partitions per partition */
     uint32_t slice_segments;
