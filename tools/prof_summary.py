@@ -2,7 +2,9 @@
 
     python tools/prof_summary.py <trace_dir> <pmc_fetch_dir> <pmc_write_dir> <out.json> [config...]
 
-Kernel-trace: per-dispatch durations of the last join of the run. PMC: FETCH_SIZE and WRITE_SIZE
+Kernel-trace: per-dispatch durations of the last synchronous (one-queue) join of the run. PMC
+(bytes, the same in either schedule): the last join, index kernels labelled by their queue's last
+scatter. PMC: FETCH_SIZE and WRITE_SIZE
 (KiB per dispatch; printed below as KiB x 1024 / 1e9 = GB) from two separate --pmc passes; on gfx950 FETCH_SIZE reports half the bytes of
 wide coalesced reads (MI355X_MICROARCH.md, HBM), so hbm_bytes = (2*FETCH_SIZE + WRITE_SIZE)*1024.
 Infinity-Cache hits are included in these counters.
@@ -39,16 +41,35 @@ def last_join(names):
     return list(range(b, ends[-1] + 1))
 
 
-def label(names, idx):
-    """Phase of each dispatch: plan / list-fill kernels belong to the side of the last scatter."""
-    out, side = [], "r"
+def joins(names):
+    """Dispatch index ranges of every join (each ends with its k_join)."""
+    ends = [i for i, n in enumerate(names) if n == "k_join"]
+    return [list(range(b, e + 1)) for b, e in zip([0] + [x + 1 for x in ends[:-1]], ends)]
+
+
+def last_one_queue_join(names, queues):
+    """The last join whose dispatches all ran on one queue (a synchronous join: its kernel times
+    are its own; in an async join the R side's kernels wait behind the S scatter's, and their
+    durations include that wait). Falls back to the last join."""
+    for idx in reversed(joins(names)):
+        if len({queues[i] for i in idx if not names[i].startswith("__amd")}) == 1:  # (runtime blits: own queue)
+            return idx
+    return last_join(names)
+
+
+def label(names, idx, queues=None):
+    """Phase of each dispatch: plan / list-fill kernels belong to the side of the last scatter on
+    their own queue (async joins run the S pass on a second stream, so the R side's plan can start
+    after the S scatter; one-stream joins have one queue, where this is the last scatter)."""
+    out, side = [], {}
+    q = queues or [0] * len(names)
     for i in idx:
         n = names[i]
         if n in ("k_scatter_r", "k_scatter_s"):
-            side = n[-1]
-            out.append(side + "_scatter")
+            side[q[i]] = n[-1]
+            out.append(n[-1] + "_scatter")
         elif n in ("k_plan", "k_list_fill"):
-            out.append(side + "_index")
+            out.append(side.get(q[i], "r") + "_index")
         else:
             out.append(PHASE_OF.get(n, "other"))
     return out
@@ -59,8 +80,9 @@ def main():
     tr = list(csv.DictReader(open(one(f"{tdir}/**/*kernel_trace.csv"))))
     tr.sort(key=lambda r: int(r["Start_Timestamp"]))
     names = [r["Kernel_Name"] for r in tr]
-    idx = last_join(names)
-    labs = label(names, idx)
+    tq = [r["Queue_Id"] for r in tr]
+    idx = last_one_queue_join(names, tq)  # kernel times: the last synchronous join's
+    labs = label(names, idx, tq)
     phases = defaultdict(lambda: {"ms": 0.0, "kernels": []})
     for i, lab in zip(idx, labs):
         r = tr[i]
@@ -74,7 +96,7 @@ def main():
         rows.sort(key=lambda r: int(r["Start_Timestamp"]))
         nm = [r["Kernel_Name"] for r in rows]
         ix = last_join(nm)
-        return list(zip(label(nm, ix), (float(rows[i]["Counter_Value"]) for i in ix)))
+        return list(zip(label(nm, ix, [r["Queue_Id"] for r in rows]), (float(rows[i]["Counter_Value"]) for i in ix)))
 
     fetch, write = defaultdict(float), defaultdict(float)
     for lab, v in counters(fdir, "FETCH_SIZE"):
