@@ -442,10 +442,10 @@ int Engine::enqueue(const uint2* dR, uint64_t nR, const uint2* dS, uint64_t nS,
     }
     const uint64_t GF = (uint64_t) G * F;
     bool ok = true;
-    ok &= poolR.ensure(LR * 128) && metaR.ensure(LR * 4) && listR.ensure(LR * 4);
+    ok &= poolR.ensure(LR * 128) && metaR.ensure(LR * 2) && listR.ensure(LR * 4);
     ok &= usedR.ensure(G * 4) && wgqcR.ensure(GF * 4) && wgqeR.ensure(GF * 4) && wgqoR.ensure(GF * 4);
     ok &= lstartR.ensure((F + 1) * 4) && estartR.ensure((F + 1) * 8) && istartR.ensure((F + 1) * 4);
-    ok &= poolS.ensure(LS * 128) && metaS.ensure(LS * 4) && listS.ensure(LS * 4);
+    ok &= poolS.ensure(LS * 128) && metaS.ensure(LS * 2) && listS.ensure(LS * 4);
     ok &= usedS.ensure(G * 4) && wgqcS.ensure(GF * 4) && wgqeS.ensure(GF * 4) && wgqoS.ensure(GF * 4);
     ok &= lstartS.ensure((F + 1) * 4) && estartS.ensure((F + 1) * 8) && istartS.ensure((F + 1) * 4);
     const uint64_t BSW = build_chunks_per_sweep(), SLOT = build_sweep_slot();
@@ -852,10 +852,10 @@ int Engine::enqueue_basic_kk(const uint2* dR, uint64_t nR, const uint2* dS, uint
     }
     const uint64_t GF = (uint64_t) G * Fm;
     bool ok = true;
-    ok &= poolR.ensure(LR * 128) && metaR.ensure(LR * 4) && listR.ensure(LR * 4);
+    ok &= poolR.ensure(LR * 128) && metaR.ensure(LR * 2) && listR.ensure(LR * 4);
     ok &= usedR.ensure(G * 4) && wgqcR.ensure(GF * 4) && wgqeR.ensure(GF * 4) && wgqoR.ensure(GF * 4);
     ok &= lstartR.ensure((Fm + 1) * 4) && estartR.ensure((Fm + 1) * 8) && istartR.ensure((Fm + 1) * 4);
-    ok &= poolS.ensure(LS * 128) && metaS.ensure(LS * 4) && listS.ensure(LS * 4);
+    ok &= poolS.ensure(LS * 128) && metaS.ensure(LS * 2) && listS.ensure(LS * 4);
     ok &= usedS.ensure(G * 4) && wgqcS.ensure(GF * 4) && wgqeS.ensure(GF * 4) && wgqoS.ensure(GF * 4);
     ok &= lstartS.ensure((Fm + 1) * 4) && estartS.ensure((Fm + 1) * 8) && istartS.ensure((Fm + 1) * 4);
     const uint64_t BSW = build_chunks_per_sweep(), SLOT = build_sweep_slot();

@@ -20,7 +20,7 @@ struct ScatterParams {
     const uint64_t*  n_dev;        // optional device-resident element count
     uint32_t*        pool;         // [G * cap][32] chunk words
     uint32_t*        ppool;        // [G * cap][32] the words' payloads (materialization), or nullptr
-    uint32_t*        meta;         // [G * cap]: partition | count << 16
+    uint32_t*        meta;         // [G * cap] 16-bit entries (meta16): partition | (count - 1) << 10
     uint32_t*        wg_used;      // [G] chunks used by each workgroup
     uint32_t*        wgq_chunks;   // [G][F] chunks of partition q in workgroup wg's region
     uint32_t*        wgq_elems;    // [G][F] elements of partition q in workgroup wg's region

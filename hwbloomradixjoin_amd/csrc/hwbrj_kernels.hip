@@ -410,8 +410,12 @@ __global__ __launch_bounds__(1024) void k_probe_global(const uint2* S, uint64_t 
 //   B2 (barrier).
 // A plan turns floor(fill/32) chunks into consecutive chunk ids: the first is the stage
 // line, further ones (only when a round overfills a partition by > 32, i.e. skew) are written
-// directly by the threads holding those overflow words. Chunk metadata = partition | count << 16.
+// directly by the threads holding those overflow words. Chunk metadata (16 bits, meta16):
+// partition | (count - 1) << 10, which is the low 15 bits of k_list_fill's sort entry.
 // (Reference pass-1: src/parallel_radix_join_bloom.c:758-852, SWWC variant :611-700.)
+__device__ __forceinline__ uint16_t meta16(uint32_t q, uint32_t count) {  // q < 1024, count 1..32
+    return (uint16_t) (q | ((count - 1u) << 10));
+}
 #ifndef HWBRJ_SC_T
 #define HWBRJ_SC_T 1024  // threads per scatter workgroup (A/B: 512)
 #endif
@@ -582,11 +586,11 @@ __device__ __forceinline__ void scatter_body(const ScatterParams& P) {
     }
     constexpr uint32_t CW = 32u;  // dwords per chunk
     uint32_t* __restrict__ pool = P.pool + wg * P.cap * CW;
-    uint32_t* __restrict__ meta = P.meta + wg * P.cap;
+    uint16_t* __restrict__ meta = (uint16_t*) P.meta + wg * P.cap;
     constexpr uint32_t EB = SRC == SRC_TUPLES ? 8u : 4u;  // bytes per element
     const auto rsrc = buf_rsrc((const uint8_t*) P.src + e0 * EB, len * EB);  // OOB loads return 0
     const auto rpool = buf_rsrc(pool, (uint32_t) (P.cap * CW * 4));
-    const auto rmeta = buf_rsrc(meta, (uint32_t) (P.cap * 4));
+    const auto rmeta = buf_rsrc(meta, (uint32_t) (P.cap * 2));
     __syncthreads();
 
     // MODE_BASIC_POS: element e0 + i is bit jj of tuple e0 + i - jj |R| (a workgroup's range
@@ -660,7 +664,7 @@ __device__ __forceinline__ void scatter_body(const ScatterParams& P) {
             if (v.x == 0x12345678u && v.y == 0x9abcdef0u)  // dev ablation: practically never stores
 #endif
             __builtin_amdgcn_raw_buffer_store_b128(v, rpool, ok ? (cb * 32 + l8 * 4) * 4 : kOob, 0, SAUX);
-            __builtin_amdgcn_raw_buffer_store_b32(qq | (32u << 16), rmeta, ok && l8 == 0 ? cb * 4 : kOob, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b16((short) meta16(qq, 32u), rmeta, ok && l8 == 0 ? cb * 2 : kOob, 0, 0);
         };
 #pragma unroll
         for (int i = 0; i < kScK; i++) task(tid + i * kScThreads);
@@ -809,7 +813,7 @@ __device__ __forceinline__ void scatter_body(const ScatterParams& P) {
                 fill[qq]          = f & 31u;
                 my_tch[pp] += nch;
                 my_tel[pp] += nch * 32;
-                for (uint32_t c = 1; c < nch; c++) meta[cb + c] = qq | (32u << 16);  // direct chunks
+                for (uint32_t c = 1; c < nch; c++) meta[cb + c] = meta16(qq, 32u);  // direct chunks
             }
         }
         stamp(4);
@@ -846,7 +850,7 @@ __device__ __forceinline__ void scatter_body(const ScatterParams& P) {
             if (has) {
                 const uint32_t cb = wb + incl - 1u;
                 ncb[qq]  = cb;
-                meta[cb] = qq | (f << 16);
+                meta[cb] = meta16(qq, f);
                 my_tch[pp] += 1;
                 my_tel[pp] += f;
             }
@@ -940,11 +944,11 @@ __device__ __forceinline__ void scatter_body_pay(const ScatterParams& P) {
     const uint64_t e1r = 4 * ((wg + 1) * units / G);
     const uint64_t e1  = e1r < n ? e1r : n;
     const uint32_t len = __builtin_amdgcn_readfirstlane(e1 > e0 ? (uint32_t) (e1 - e0) : 0u);
-    uint32_t* __restrict__ meta = P.meta + wg * P.cap;
+    uint16_t* __restrict__ meta = (uint16_t*) P.meta + wg * P.cap;
     const auto rsrc   = buf_rsrc((const uint8_t*) P.src + e0 * 8, len * 8);  // OOB loads return 0
     const auto rpool  = buf_rsrc(P.pool + wg * P.cap * 32, (uint32_t) (P.cap * 128));
     const auto rppool = buf_rsrc(P.ppool + wg * P.cap * 32, (uint32_t) (P.cap * 128));
-    const auto rmeta  = buf_rsrc(meta, (uint32_t) (P.cap * 4));
+    const auto rmeta  = buf_rsrc(meta, (uint32_t) (P.cap * 2));
     __syncthreads();
 
 #ifdef HWBRJ_ABL_SPLITH  // dev ablation (results invalid): second halves in a separate array
@@ -985,7 +989,7 @@ __device__ __forceinline__ void scatter_body_pay(const ScatterParams& P) {
             if (vp.x == 0x12345678u && vp.y == 0x9abcdef0u)
 #endif
             __builtin_amdgcn_raw_buffer_store_b128(vp, rppool, o, 0, 0);
-            __builtin_amdgcn_raw_buffer_store_b32(qq | (32u << 16), rmeta, ok && l4 == 0 && (H & 1u) ? (H >> 1) * 4 : kOob, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b16((short) meta16(qq, 32u), rmeta, ok && l4 == 0 && (H & 1u) ? (H >> 1) * 2 : kOob, 0, 0);
         };
 #pragma unroll
         for (int i = 0; i < kScKP; i++) task(tid + i * kScPayThreads);
@@ -1094,7 +1098,7 @@ __device__ __forceinline__ void scatter_body_pay(const ScatterParams& P) {
                 fill[qq] = f & (kPayDepth - 1u);
                 tel[qq] += nh * kPayDepth;
                 for (uint32_t k = 1; k < nh; k++)  // chunks completed by a direct half
-                    if ((Bk + k) & 1u) meta[(Bk + k) >> 1] = qq | (32u << 16);
+                    if ((Bk + k) & 1u) meta[(Bk + k) >> 1] = meta16(qq, 32u);
                 const uint32_t Hl = nh == 1 ? H0 : Bk + nh - 1u;  // last half written
                 cst[qq] = (Hl & 1u) ? 0u : (Hl | 1u);
             }
@@ -1123,7 +1127,7 @@ __device__ __forceinline__ void scatter_body_pay(const ScatterParams& P) {
             wb = __builtin_amdgcn_readfirstlane(wb);
             if (f > 0 || hcur) {
                 const uint32_t ch = hcur ? cs >> 1 : wb + incl - 1u;
-                meta[ch] = qq | ((hcur * kPayDepth + f) << 16);
+                meta[ch] = meta16(qq, hcur * kPayDepth + f);
                 pl0[qq]  = ch * 2u + hcur;
                 tel[qq] += f;
             }
@@ -1328,7 +1332,7 @@ __global__ __launch_bounds__(kLfThreads) void k_list_fill(const uint32_t* __rest
     __syncthreads();
     const uint64_t region = (uint64_t) wg * cap;
     const uint32_t used   = wg_used[wg];
-    const uint32_t* __restrict__ rmeta = meta + region;
+    const uint16_t* __restrict__ rmeta = (const uint16_t*) meta + region;  // meta16 entries
     // the next batch's metas are loaded while the current one is sorted and written
     uint32_t nx[kLfPer];
 #pragma unroll
@@ -1344,10 +1348,7 @@ __global__ __launch_bounds__(kLfThreads) void k_list_fill(const uint32_t* __rest
         for (int j = 0; j < (int) kLfPer; j++) {
             const uint32_t m = nx[j];
             p[j]             = kNoEntry;
-            if (m != kNoEntry) {
-                const uint32_t q = m & 0xFFFFu;
-                p[j] = q | ((((m >> 16) - 1u) & 31u) << 10) | (atomicAdd(&cnt[q], 1u) << 15);
-            }
+            if (m != kNoEntry) p[j] = m | (atomicAdd(&cnt[m & 1023u], 1u) << 15);  // (m: meta16)
         }
         if (b0 + kLfBatch < used) {
 #pragma unroll

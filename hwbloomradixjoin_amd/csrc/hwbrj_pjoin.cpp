@@ -227,10 +227,10 @@ int Engine::join_partitioned(const hwbrj_exchange_t* x, int rank, int world, con
         }
         const uint64_t GF = (uint64_t) G * F;
         bool ok = true;
-        ok &= poolR.ensure(LR * 128) && metaR.ensure(LR * 4) && listR.ensure(LR * 4);
+        ok &= poolR.ensure(LR * 128) && metaR.ensure(LR * 2) && listR.ensure(LR * 4);
         ok &= usedR.ensure(G * 4) && wgqcR.ensure(GF * 4) && wgqeR.ensure(GF * 4) && wgqoR.ensure(GF * 4);
         ok &= lstartR.ensure((F + 1) * 4) && estartR.ensure((F + 1) * 8) && istartR.ensure((F + 1) * 4);
-        ok &= poolS.ensure(LS * 128) && metaS.ensure(LS * 4) && listS.ensure(LS * 4);
+        ok &= poolS.ensure(LS * 128) && metaS.ensure(LS * 2) && listS.ensure(LS * 4);
         ok &= usedS.ensure(G * 4) && wgqcS.ensure(GF * 4) && wgqeS.ensure(GF * 4) && wgqoS.ensure(GF * 4);
         ok &= lstartS.ensure((F + 1) * 4) && estartS.ensure((F + 1) * 8) && istartS.ensure((F + 1) * 4);
         const uint64_t items_max = (LS / CH + F + 1) * nseg;
