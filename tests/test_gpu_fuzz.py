@@ -7,8 +7,12 @@ src/parallel_radix_join_bloom.c:259-555), relation sizes with ragged tails and a
 probes, one hot key). The bar is the other parity tests' bar: `filtered` and `Results` equal the
 oracle's `orc.bpro` on the same tuples; every fourth case also materializes the result and its pair
 multiset equals `orc.join_pairs`, and every third runs the partitioned multi-GPU join on one rank
-(hwbrj_join_partitioned, every exchange a local copy) where its geometry allows. The cases are fixed by their seeds, so a failure names a
-reproducible configuration (see `case()`).
+(hwbrj_join_partitioned, every exchange a local copy) where its geometry allows. The same cases also
+go through the schedule bench.py times: groups of 8 enqueued back to back with
+hwbrj_join_device_async (empty R, one-tuple S, global-bitmap and basic k >= 2 launches mixed in a
+group), every join's counts collected with hwbrj_join_wait_all and compared with its own oracle
+result. The cases are fixed by their seeds, so a failure names a reproducible configuration (see
+`case()`).
 """
 import numpy as np
 import pytest
@@ -51,6 +55,26 @@ def case(seed: int):
     return variant, m, k, B, algorithm, Rk.astype(np.int32), np.asarray(Sk).astype(np.int32)
 
 
+_ORC = {}  # seed -> the oracle's (filtered, results), shared by the synchronous and async tests
+
+
+def _inputs(hw, seed):
+    variant, m, k, B, algorithm, Rk, Sk = case(seed)
+    rng = np.random.default_rng(seed)
+    R, S = _rel(Rk, rng), _rel(Sk, rng)
+    return R, S, hw.BloomFilterArgs.from_flag(variant, m, k, B), algorithm
+
+
+def _oracle(orc, seed, R, S, args):
+    if seed not in _ORC:
+        if args is None:
+            res, filt, _ = orc.bpro(R, S, 4, 0, 0, 0, 0, use_bloom=False)
+        else:
+            res, filt, _ = orc.bpro(R, S, 4, args.variant, args.m, args.k, args.B)
+        _ORC[seed] = (filt, res)
+    return _ORC[seed]
+
+
 def _rel(keys, rng):
     return np.stack([keys, rng.integers(INT_MIN, INT_MAX, size=keys.size, endpoint=True).astype(np.int32)], 1)
 
@@ -71,18 +95,12 @@ def test_fuzz_cases_are_reference_configurations(hw):
 @pytest.mark.gpu
 @pytest.mark.parametrize("seed", range(NCASES))
 def test_fuzz_counts_vs_oracle(hw, cuda, orc, seed):
-    variant, m, k, B, algorithm, Rk, Sk = case(seed)
-    rng = np.random.default_rng(seed)
-    R, S = _rel(Rk, rng), _rel(Sk, rng)
-    args = hw.BloomFilterArgs.from_flag(variant, m, k, B)
+    R, S, args, algorithm = _inputs(hw, seed)
     dR = cuda.from_numpy(R).cuda()
     dS = cuda.from_numpy(S).cuda()
     st = hw.join_device(dR, dS, args, algorithm=algorithm)
-    if args is None:
-        res, filt, _ = orc.bpro(R, S, 4, 0, 0, 0, 0, use_bloom=False)
-    else:
-        res, filt, _ = orc.bpro(R, S, 4, args.variant, args.m, args.k, args.B)
-    assert (st.filtered, st.matches) == (filt, res), (seed, variant, m, k, B, algorithm, st)
+    filt, res = _oracle(orc, seed, R, S, args)
+    assert (st.filtered, st.matches) == (filt, res), (seed, case(seed)[:5], st)
     if seed % 3 == 1:
         from hwbloomradixjoin_amd import pjoin
         try:
@@ -96,3 +114,25 @@ def test_fuzz_counts_vs_oracle(hw, cuda, orc, seed):
         want = orc.join_pairs(R, S)
         assert st2.matches == want.shape[0] == pairs.shape[0] == res
         assert np.array_equal(_sorted_pairs(pairs.cpu().numpy()), _sorted_pairs(want))
+
+
+GROUP = 8
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("group", range(NCASES // GROUP))
+def test_fuzz_async_back_to_back(hw, cuda, orc, group):
+    """Cases 8g .. 8g + 7 enqueued back to back through hwbrj_join_device_async on one stream (no
+    host wait between them: consecutive joins differ in filter, mode and sizes), then one
+    hwbrj_join_wait_all: every join's (filtered, matches) against its own oracle result."""
+    seeds = range(group * GROUP, (group + 1) * GROUP)
+    ins = [_inputs(hw, s) for s in seeds]
+    dev = [(cuda.from_numpy(R).cuda(), cuda.from_numpy(S).cuda()) for R, S, _, _ in ins]
+    want = [_oracle(orc, s, R, S, a) for s, (R, S, a, _) in zip(seeds, ins)]
+    stream = cuda.cuda.Stream()
+    for (dR, dS), (_, _, a, _) in zip(dev, ins):
+        hw.join_device_async(dR, dS, a, stream=stream)
+    sts = hw.join_wait_all()
+    assert len(sts) == GROUP
+    got = [(st.filtered, st.matches) for st in sts]
+    assert got == want, [(s, case(s)[:4], g, w) for s, g, w in zip(seeds, got, want) if g != w]
