@@ -2278,6 +2278,10 @@ constexpr uint32_t kJoinDesc    = 256;                 // run descriptors per ba
 #define HWBRJ_JTU 8
 #endif
 constexpr uint32_t kJoinTailU   = HWBRJ_JTU;           // loads in flight per lane in a long run
+#ifndef HWBRJ_JTS
+#define HWBRJ_JTS 2
+#endif
+constexpr uint32_t kJoinTailS   = HWBRJ_JTS;           // ... in the rest of a run (< 64 kJoinTailU words)
 constexpr uint32_t kEmpty       = 0xFFFFFFFFu;  // codes of one job share their low hash_shift >= 1
                                                 // bits, so (code >> hash_shift) never equals it
 
@@ -2483,19 +2487,32 @@ __device__ __forceinline__ void join_job(const JoinParams& P, const uint32_t blk
         return (x >> (((b7 + kw7 * o) & 7u) + ksh)) & kmk;
     };
     auto b7_of = [&](uint64_t tb) -> uint32_t { return !kB8 && (tb & kPk) ? (uint32_t) tb & 7u : 0u; };
-    // The words [from, n) of one run (long runs: high-selectivity survivors, large R runs), with
-    // kJoinTailU loads in flight per lane instead of one dependent load per iteration.
+    // The words [from, n) of one run (long runs: high-selectivity survivors, large R runs): whole
+    // rounds of kJoinTailU loads in flight per lane (no per-load predicate) while the run has them,
+    // then the rest kJoinTailS per lane, not a predicated full-width round (q = 1 join 0.99 ->
+    // 0.96 ms, PRO 1.03 -> 0.97 ms, the north star within 0.002 ms: profiles/r06/join_tail_ab.txt).
+    // b stays a multiple of 64 (from is), so word b + lane + 64 u is lane mod 8 for the packed keys.
     auto tail_run = [&](auto side_c, uint64_t bb, uint32_t from, uint32_t n, auto&& op) {
-        for (uint32_t o = from + lane; o < n; o += 64u * kJoinTailU) {
+        const bool     pk = (bb & kPk) != 0;
+        const uint32_t b7 = b7_of(bb);
+        uint32_t       b  = from;  // (uniform)
+        for (; b + 64u * kJoinTailU <= n; b += 64u * kJoinTailU) {
             uint32_t v[kJoinTailU];
 #pragma unroll
-            for (int u = 0; u < (int) kJoinTailU; u++) {
-                const uint32_t oo = o + 64u * u;
+            for (int u = 0; u < (int) kJoinTailU; u++) v[u] = ldv(side_c, bb, b + lane + 64u * u);
+#pragma unroll
+            for (int u = 0; u < (int) kJoinTailU; u++) op(key(side_c, v[u], pk, b7, lane));
+        }
+        for (; b < n; b += 64u * kJoinTailS) {
+            uint32_t v[kJoinTailS];
+#pragma unroll
+            for (int u = 0; u < (int) kJoinTailS; u++) {
+                const uint32_t oo = b + lane + 64u * u;
                 v[u]              = oo < n ? ldv(side_c, bb, oo) : 0u;
             }
 #pragma unroll
-            for (int u = 0; u < (int) kJoinTailU; u++)
-                if (o + 64u * u < n) op(key(side_c, v[u], (bb & kPk) != 0, b7_of(bb), lane));  // (from: a multiple of 64)
+            for (int u = 0; u < (int) kJoinTailS; u++)
+                if (b + lane + 64u * u < n) op(key(side_c, v[u], pk, b7, lane));
         }
     };
     // Every word of runs [da, db) of a descriptor batch through op(word): a wave per run, RUNS runs
@@ -2503,6 +2520,7 @@ __device__ __forceinline__ void join_job(const JoinParams& P, const uint32_t blk
     auto walk = [&](auto runs_c, auto wpl_c, auto side_c, const uint32_t* nc,
                     const uint64_t* nb, uint32_t da, uint32_t db, auto&& op) {
         constexpr int RUNS = decltype(runs_c)::value, WPL = decltype(wpl_c)::value;
+        static_assert(3 * RUNS <= 32, "b7m holds 3 bits per run in flight (HWBRJ_JRR / HWBRJ_JSR <= 10)");
         for (uint32_t d = da + wave; d < db; d += kJoinWaves * RUNS) {
             uint32_t v[RUNS][WPL], n[RUNS], pkm = 0, b7m = 0;  // pkm bit r: run r packed; b7m: its tb & 7
 #pragma unroll
@@ -2616,6 +2634,7 @@ __device__ __forceinline__ void join_job(const JoinParams& P, const uint32_t blk
 #define HWBRJ_JFS HWBRJ_JSR
 #endif
         constexpr int FS = HWBRJ_JFS, FSW = HWBRJ_JSW;  // survivor runs per wave loaded with R's
+        static_assert(3 * FR <= 32 && 3 * FS <= 32, "r7m / s7m hold 3 bits per run (HWBRJ_JFR / HWBRJ_JFS <= 10)");
         uint32_t rv[FR][FW], rn[FR], sv[FS][FSW], sn[FS], spk = 0;  // spk bit r: survivor run r packed
         uint32_t r7m = 0, s7m = 0;  // tb & 7 of the packed runs (3 bits per run)
 #pragma unroll
@@ -4243,6 +4262,7 @@ const char* kernel_build_knobs() {
         num("HWBRJ_PR_NT", HWBRJ_PR_NT, 0);
         num("HWBRJ_SCRK", HWBRJ_SCRK, 256);
         num("HWBRJ_JTU", HWBRJ_JTU, 8);
+        num("HWBRJ_JTS", HWBRJ_JTS, 2);
         num("HWBRJ_JT", HWBRJ_JT, 256);
         num("HWBRJ_JXCD", HWBRJ_JXCD, 1);
         num("HWBRJ_PACK3", HWBRJ_PACK3, 1);
