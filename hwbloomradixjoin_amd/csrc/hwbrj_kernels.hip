@@ -2631,7 +2631,7 @@ __device__ __forceinline__ void join_job(const JoinParams& P, const uint32_t blk
         }
         __syncthreads();
 #ifndef HWBRJ_JFS
-#define HWBRJ_JFS HWBRJ_JSR
+#define HWBRJ_JFS 5  // (round 6: 5 of 8 -> join 0.294 -> 0.284 ms, profiles/r06/join_fs_ab.txt)
 #endif
         constexpr int FS = HWBRJ_JFS, FSW = HWBRJ_JSW;  // survivor runs per wave loaded with R's
         static_assert(3 * FR <= 32 && 3 * FS <= 32, "r7m / s7m hold 3 bits per run (HWBRJ_JFR / HWBRJ_JFS <= 10)");
@@ -4270,7 +4270,7 @@ const char* kernel_build_knobs() {
         num("HWBRJ_JRR", HWBRJ_JRR, 4);
         num("HWBRJ_JRW", HWBRJ_JRW, 4);
         num("HWBRJ_JSR", HWBRJ_JSR, 8);
-        num("HWBRJ_JFS", HWBRJ_JFS, HWBRJ_JSR);
+        num("HWBRJ_JFS", HWBRJ_JFS, 5);
         num("HWBRJ_JSW", HWBRJ_JSW, 2);
         num("HWBRJ_JFR", HWBRJ_JFR, 8);
         num("HWBRJ_JFW", HWBRJ_JFW, 5);
